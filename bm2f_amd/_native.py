@@ -1,0 +1,79 @@
+"""ctypes binding of ``libbm2f.so`` (the C ABI declared in ``include/bm2f.h``).
+
+The library is built in-tree (``bm2f_amd/lib/libbm2f.so``, see ``bm2f_amd/build.py``) so it travels
+with the repository snapshot to the GPU box.  There is no fallback: if the library is missing or
+fails to load, every op raises.  This mirrors the reference's hard dependency on its compiled
+``MultiScaleDeformableAttention`` module (ops/functions/ms_deform_attn_func.py:21-29), minus the
+reference's silent pure-PyTorch fallback (ops/modules/ms_deform_attn.py:116-121).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libbm2f.so")
+_lock = threading.Lock()
+_lib = None
+
+ABI_VERSION = 1
+
+_p = ctypes.c_void_p
+_i = ctypes.c_int
+
+# name -> argtypes (all return int status)
+_SIGNATURES = {
+    "m2f_msda_fwd_f32": [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p],
+    "m2f_msda_fwd_f64": [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p],
+    "m2f_msda_bwd_f32": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p],
+    "m2f_msda_bwd_f64": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p],
+}
+
+
+class NativeError(RuntimeError):
+    """A nonzero status returned by libbm2f (message from ``m2f_last_error``)."""
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def load():
+    """Load (once) and return the ctypes handle; raises ImportError when the library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(_LIB_PATH):
+            raise ImportError(
+                f"libbm2f.so not found at {_LIB_PATH}; build it with `python -c \"import __graft_entry__ as g; g.build()\"` "
+                "or `python -m bm2f_amd.build`")
+        lib = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        lib.m2f_last_error.restype = ctypes.c_char_p
+        lib.m2f_last_error.argtypes = []
+        lib.m2f_abi_version.restype = ctypes.c_int
+        lib.m2f_abi_version.argtypes = []
+        got = lib.m2f_abi_version()
+        if got != ABI_VERSION:
+            raise ImportError(f"libbm2f.so ABI version {got} != expected {ABI_VERSION}; rebuild it")
+        for name, argtypes in _SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.argtypes = argtypes
+            fn.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def exported_symbols():
+    return ["m2f_last_error", "m2f_abi_version", *_SIGNATURES.keys()]
+
+
+def call(name: str, *args) -> None:
+    """Invoke ``name`` and raise NativeError (a RuntimeError) on a nonzero status."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.m2f_last_error().decode("utf-8", "replace")
+        raise NativeError(f"{name} failed (code {rc}): {msg}")

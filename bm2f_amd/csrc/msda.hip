@@ -1,0 +1,467 @@
+// Multi-scale deformable attention (MSDA) forward / backward for gfx950.
+//
+// Semantics follow the reference op exactly (mask2former/modeling/pixel_decoder/ops):
+//   * sampling point:  h = loc_y * H_l - 0.5, w = loc_x * W_l - 0.5; the point contributes only if
+//     -1 < h < H_l and -1 < w < W_l (ms_deform_im2col_cuda.cuh:290-296);
+//   * bilinear with per-corner zero padding, value = w1*v1 + w2*v2 + w3*v3 + w4*v4 (.cuh:38-89);
+//   * backward: grad_value[corner] += w_corner * g * a; grad_attn = sum_c g * val;
+//     grad_loc = (W * sum_c dval/dw * g * a, H * sum_c dval/dh * g * a)  (.cuh:92-164).
+//
+// Layout choices (MI355X-first, not the reference's thread-per-channel/1024-thread blocks):
+//   * fp32 fast path: a pair (n, q, m) is served by G = D/4 lanes, each owning 4 consecutive
+//     channels (one float4).  A wave64 therefore handles 64/G pairs; for D = 32 that is the 8 heads
+//     of one query, every corner fetch is one 128-byte row per pair, and the channel reductions of
+//     the backward are an in-lane sum of 4 followed by log2(G) xor-shuffles (no LDS, no barriers).
+//   * the backward's grad_value scatter is the costly part (one 128-B row add per corner per
+//     point).  With host spatial shapes and Lq == S (the encoder), queries are grouped into spatial
+//     tiles and the adds go to a per-workgroup LDS window of the sampled neighbourhood, flushed to
+//     HBM once with row-contiguous atomics; samples falling outside the window take the direct path.
+//   * fp64 and channel counts the fast path does not cover use straightforward generic kernels.
+#include "common.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace m2f {
+std::string& last_error() {
+  static thread_local std::string s;
+  return s;
+}
+}  // namespace m2f
+
+extern "C" const char* m2f_last_error(void) { return m2f::last_error().c_str(); }
+extern "C" int m2f_abi_version(void) { return 1; }
+
+namespace {
+
+using f4 = float __attribute__((ext_vector_type(4)));
+
+constexpr int kMaxLevels = 16;
+
+// ------------------------------------------------------------------------------------------------
+// Generic kernels (any channel count, float or double).  Thread per output element for the forward,
+// block per (n, q, m) pair for the backward.
+// ------------------------------------------------------------------------------------------------
+
+template <typename T>
+__device__ __forceinline__ T bilinear_gather(const T* __restrict__ v, int H, int W, int64_t rs, T h, T w) {
+  const int h0 = static_cast<int>(floor(h));
+  const int w0 = static_cast<int>(floor(w));
+  const T lh = h - h0, lw = w - w0;
+  const T hh = T(1) - lh, hw = T(1) - lw;
+  T v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+  if (h0 >= 0 && w0 >= 0) v1 = v[(static_cast<int64_t>(h0) * W + w0) * rs];
+  if (h0 >= 0 && w0 + 1 <= W - 1) v2 = v[(static_cast<int64_t>(h0) * W + w0 + 1) * rs];
+  if (h0 + 1 <= H - 1 && w0 >= 0) v3 = v[(static_cast<int64_t>(h0 + 1) * W + w0) * rs];
+  if (h0 + 1 <= H - 1 && w0 + 1 <= W - 1) v4 = v[(static_cast<int64_t>(h0 + 1) * W + w0 + 1) * rs];
+  const T w1 = hh * hw, w2 = hh * lw, w3 = lh * hw, w4 = lh * lw;
+  return w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) msda_fwd_generic(
+    const T* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
+    const T* __restrict__ loc, const T* __restrict__ attn, int64_t total, int S, int M, int D, int L,
+    int Lq, int P, T* __restrict__ out) {
+  const int64_t rs = static_cast<int64_t>(M) * D;
+  for (int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; idx < total;
+       idx += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int c = static_cast<int>(idx % D);
+    const int64_t pair = idx / D;
+    const int m = static_cast<int>(pair % M);
+    const int64_t n = pair / M / Lq;
+    const T* vb = value + (n * S * M + m) * D + c;
+    const T* lp = loc + pair * L * P * 2;
+    const T* ap = attn + pair * L * P;
+    T col = 0;
+    for (int l = 0; l < L; ++l) {
+      const int H = static_cast<int>(shapes[2 * l]);
+      const int W = static_cast<int>(shapes[2 * l + 1]);
+      const T* vl = vb + lsi[l] * rs;
+      for (int p = 0; p < P; ++p, lp += 2, ++ap) {
+        const T h = lp[1] * H - T(0.5);
+        const T w = lp[0] * W - T(0.5);
+        if (h > T(-1) && w > T(-1) && h < T(H) && w < T(W))
+          col += bilinear_gather(vl, H, W, rs, h, w) * ap[0];
+      }
+    }
+    out[idx] = col;
+  }
+}
+
+template <typename T, int BS>
+__device__ __forceinline__ T block_sum(T v, T* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wid = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[wid] = v;
+  __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int i = 0; i < BS / 64; ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+template <typename T, int BS>
+__global__ void __launch_bounds__(BS) msda_bwd_generic(
+    const T* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
+    const T* __restrict__ loc, const T* __restrict__ attn, const T* __restrict__ gout, int S, int M, int D,
+    int L, int Lq, int P, T* __restrict__ gvalue, T* __restrict__ gloc, T* __restrict__ gattn) {
+  __shared__ T red[3][BS / 64];
+  const int64_t pair = blockIdx.x;
+  const int m = static_cast<int>(pair % M);
+  const int64_t n = pair / M / Lq;
+  const int64_t rs = static_cast<int64_t>(M) * D;
+  const int64_t vbase = (n * S * M + m) * D;
+  const T* go = gout + pair * D;
+  for (int l = 0; l < L; ++l) {
+    const int H = static_cast<int>(shapes[2 * l]);
+    const int W = static_cast<int>(shapes[2 * l + 1]);
+    const int64_t lbase = vbase + lsi[l] * rs;
+    for (int p = 0; p < P; ++p) {
+      const int64_t k = (pair * L + l) * P + p;
+      const T lw = loc[2 * k], lh = loc[2 * k + 1], a = attn[k];
+      const T h = lh * H - T(0.5), w = lw * W - T(0.5);
+      const bool ok = h > T(-1) && w > T(-1) && h < T(H) && w < T(W);
+      T pa = 0, px = 0, py = 0;
+      if (ok) {  // uniform across the block
+        const int h0 = static_cast<int>(floor(h)), w0 = static_cast<int>(floor(w));
+        const T lh_ = h - h0, lw_ = w - w0, hh = T(1) - lh_, hw = T(1) - lw_;
+        const T w1 = hh * hw, w2 = hh * lw_, w3 = lh_ * hw, w4 = lh_ * lw_;
+        const bool c1 = h0 >= 0 && w0 >= 0, c2 = h0 >= 0 && w0 + 1 <= W - 1;
+        const bool c3 = h0 + 1 <= H - 1 && w0 >= 0, c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
+        const int64_t o1 = lbase + (static_cast<int64_t>(h0) * W + w0) * rs;
+        const int64_t o2 = o1 + rs, o3 = o1 + static_cast<int64_t>(W) * rs, o4 = o3 + rs;
+        for (int c = threadIdx.x; c < D; c += BS) {
+          const T g = go[c];
+          const T tg = g * a;
+          T gh = 0, gw = 0, v1 = 0, v2 = 0, v3 = 0, v4 = 0;
+          if (c1) { v1 = value[o1 + c]; gh -= hw * v1; gw -= hh * v1; atomicAdd(gvalue + o1 + c, w1 * tg); }
+          if (c2) { v2 = value[o2 + c]; gh -= lw_ * v2; gw += hh * v2; atomicAdd(gvalue + o2 + c, w2 * tg); }
+          if (c3) { v3 = value[o3 + c]; gh += hw * v3; gw -= lh_ * v3; atomicAdd(gvalue + o3 + c, w3 * tg); }
+          if (c4) { v4 = value[o4 + c]; gh += lw_ * v4; gw += lh_ * v4; atomicAdd(gvalue + o4 + c, w4 * tg); }
+          pa += g * (w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4);
+          px += W * gw * tg;
+          py += H * gh * tg;
+        }
+      }
+      pa = block_sum<T, BS>(pa, red[0]);
+      px = block_sum<T, BS>(px, red[1]);
+      py = block_sum<T, BS>(py, red[2]);
+      if (threadIdx.x == 0) {
+        gattn[k] = pa;
+        gloc[2 * k] = px;
+        gloc[2 * k + 1] = py;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// fp32 fast path: G = D/4 lanes per (n,q,m) pair, float4 per lane.
+// ------------------------------------------------------------------------------------------------
+
+struct Corners {
+  int64_t o1, o2, o3, o4;     // element offsets of the 4 corner rows (clamped to valid rows)
+  float w1, w2, w3, w4;       // bilinear weights
+  float hy, ly, hx, lx;       // 1-lh, lh, 1-lw, lw
+  bool c1, c2, c3, c4;        // corner inside the level
+  bool ok;                    // sample inside (-1,H)x(-1,W)
+};
+
+__device__ __forceinline__ Corners make_corners(float locx, float locy, int H, int W, int64_t lbase, int64_t rs) {
+  Corners k;
+  const float h = locy * H - 0.5f;
+  const float w = locx * W - 0.5f;
+  k.ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
+  const float hs = k.ok ? h : -2.f, ws = k.ok ? w : -2.f;   // invalid point: every corner outside
+  const float fh = floorf(hs), fw = floorf(ws);
+  const int h0 = static_cast<int>(fh), w0 = static_cast<int>(fw);
+  k.ly = hs - fh; k.lx = ws - fw;
+  k.hy = 1.f - k.ly; k.hx = 1.f - k.lx;
+  k.w1 = k.hy * k.hx; k.w2 = k.hy * k.lx; k.w3 = k.ly * k.hx; k.w4 = k.ly * k.lx;
+  k.c1 = h0 >= 0 && w0 >= 0;
+  k.c2 = h0 >= 0 && w0 + 1 <= W - 1;
+  k.c3 = h0 + 1 <= H - 1 && w0 >= 0;
+  k.c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
+  const int y0 = max(h0, 0), y1 = min(h0 + 1, H - 1), x0 = max(w0, 0), x1 = min(w0 + 1, W - 1);
+  k.o1 = lbase + (static_cast<int64_t>(y0) * W + x0) * rs;
+  k.o2 = lbase + (static_cast<int64_t>(y0) * W + x1) * rs;
+  k.o3 = lbase + (static_cast<int64_t>(y1) * W + x0) * rs;
+  k.o4 = lbase + (static_cast<int64_t>(y1) * W + x1) * rs;
+  return k;
+}
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+template <int D, int PT>
+__global__ void __launch_bounds__(256) msda_fwd_f32_vec(
+    const float* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
+    const float* __restrict__ loc, const float* __restrict__ attn, int64_t npairs, int S, int M, int L,
+    int Lq, int Prt, float* __restrict__ out) {
+  constexpr int G = D / 4;
+  const int P = PT > 0 ? PT : Prt;
+  __shared__ int sH[kMaxLevels], sW[kMaxLevels];
+  __shared__ int64_t sSt[kMaxLevels];
+  if (threadIdx.x < L) {
+    sH[threadIdx.x] = static_cast<int>(shapes[2 * threadIdx.x]);
+    sW[threadIdx.x] = static_cast<int>(shapes[2 * threadIdx.x + 1]);
+    sSt[threadIdx.x] = lsi[threadIdx.x];
+  }
+  __syncthreads();
+  const int64_t pair = static_cast<int64_t>(blockIdx.x) * (256 / G) + threadIdx.x / G;
+  if (pair >= npairs) return;
+  const int j = threadIdx.x % G;
+  const int m = static_cast<int>(pair % M);
+  const int64_t n = pair / M / Lq;
+  const int64_t rs = static_cast<int64_t>(M) * D;
+  const int64_t vbase = (n * S * M + m) * D + 4 * j;
+  const float* lp = loc + pair * L * P * 2;
+  const float* ap = attn + pair * L * P;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int l = 0; l < L; ++l) {
+    const int H = sH[l], W = sW[l];
+    const int64_t lbase = vbase + sSt[l] * rs;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int kk = l * P + p;
+      const float2 xy = *reinterpret_cast<const float2*>(lp + 2 * kk);
+      const float a = ap[kk];
+      const Corners k = make_corners(xy.x, xy.y, H, W, lbase, rs);
+      f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
+      const f4 z = {0.f, 0.f, 0.f, 0.f};
+      v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
+      const f4 val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
+      acc += k.ok ? val * a : z;
+    }
+  }
+  *reinterpret_cast<f4*>(out + pair * D + 4 * j) = acc;
+}
+
+// Backward, direct-atomic variant: every corner contribution goes straight to HBM.
+template <int D, int PT>
+__global__ void __launch_bounds__(256) msda_bwd_f32_vec(
+    const float* __restrict__ value, const int64_t* __restrict__ shapes, const int64_t* __restrict__ lsi,
+    const float* __restrict__ loc, const float* __restrict__ attn, const float* __restrict__ gout,
+    int64_t npairs, int S, int M, int L, int Lq, int Prt, float* __restrict__ gvalue,
+    float* __restrict__ gloc, float* __restrict__ gattn) {
+  constexpr int G = D / 4;
+  const int P = PT > 0 ? PT : Prt;
+  __shared__ int sH[kMaxLevels], sW[kMaxLevels];
+  __shared__ int64_t sSt[kMaxLevels];
+  if (threadIdx.x < L) {
+    sH[threadIdx.x] = static_cast<int>(shapes[2 * threadIdx.x]);
+    sW[threadIdx.x] = static_cast<int>(shapes[2 * threadIdx.x + 1]);
+    sSt[threadIdx.x] = lsi[threadIdx.x];
+  }
+  __syncthreads();
+  const int64_t pair = static_cast<int64_t>(blockIdx.x) * (256 / G) + threadIdx.x / G;
+  if (pair >= npairs) return;
+  const int j = threadIdx.x % G;
+  const int m = static_cast<int>(pair % M);
+  const int64_t n = pair / M / Lq;
+  const int64_t rs = static_cast<int64_t>(M) * D;
+  const int64_t vbase = (n * S * M + m) * D + 4 * j;
+  const f4 g = ld4(gout + pair * D + 4 * j);
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  for (int l = 0; l < L; ++l) {
+    const int H = sH[l], W = sW[l];
+    const int64_t lbase = vbase + sSt[l] * rs;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int64_t kk = (pair * L + l) * P + p;
+      const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * kk);
+      const float a = attn[kk];
+      const Corners k = make_corners(xy.x, xy.y, H, W, lbase, rs);
+      f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
+      v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
+      const f4 tg = g * a;
+      const f4 val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
+      // d val / d w and d val / d h per channel, in the reference's accumulation order (.cuh:125-157)
+      const f4 gw = -k.hy * v1 + k.hy * v2 - k.ly * v3 + k.ly * v4;
+      const f4 gh = -k.hx * v1 - k.lx * v2 + k.hx * v3 + k.lx * v4;
+      const f4 ta = g * val, tx = gw * tg, ty = gh * tg;
+      float pa = ta.x + ta.y + ta.z + ta.w;
+      float px = tx.x + tx.y + tx.z + tx.w;
+      float py = ty.x + ty.y + ty.z + ty.w;
+#pragma unroll
+      for (int o = G / 2; o > 0; o >>= 1) {
+        pa += __shfl_xor(pa, o);
+        px += __shfl_xor(px, o);
+        py += __shfl_xor(py, o);
+      }
+      if (k.ok) {
+        float* gv = gvalue;
+        if (k.c1) { const f4 c = k.w1 * tg; atomicAdd(gv + k.o1, c.x); atomicAdd(gv + k.o1 + 1, c.y); atomicAdd(gv + k.o1 + 2, c.z); atomicAdd(gv + k.o1 + 3, c.w); }
+        if (k.c2) { const f4 c = k.w2 * tg; atomicAdd(gv + k.o2, c.x); atomicAdd(gv + k.o2 + 1, c.y); atomicAdd(gv + k.o2 + 2, c.z); atomicAdd(gv + k.o2 + 3, c.w); }
+        if (k.c3) { const f4 c = k.w3 * tg; atomicAdd(gv + k.o3, c.x); atomicAdd(gv + k.o3 + 1, c.y); atomicAdd(gv + k.o3 + 2, c.z); atomicAdd(gv + k.o3 + 3, c.w); }
+        if (k.c4) { const f4 c = k.w4 * tg; atomicAdd(gv + k.o4, c.x); atomicAdd(gv + k.o4 + 1, c.y); atomicAdd(gv + k.o4 + 2, c.z); atomicAdd(gv + k.o4 + 3, c.w); }
+      }
+      if (j == 0) {
+        gattn[kk] = k.ok ? pa : 0.f;
+        *reinterpret_cast<float2*>(gloc + 2 * kk) =
+            k.ok ? make_float2(W * px, H * py) : make_float2(0.f, 0.f);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host side
+// ------------------------------------------------------------------------------------------------
+
+struct Dims {
+  int N, S, M, D, L, Lq, P;
+  int64_t npairs() const { return static_cast<int64_t>(N) * Lq * M; }
+};
+
+int check_dims(const char* fn, const void* value, const void* shapes, const void* lsi, const void* loc,
+               const void* attn, const Dims& d, int im2col_step) {
+  if (!value || !shapes || !lsi || !loc || !attn)
+    return m2f::fail(M2F_EINVAL, "%s: null input pointer", fn);
+  if (d.N <= 0 || d.S <= 0 || d.M <= 0 || d.D <= 0 || d.L <= 0 || d.Lq <= 0 || d.P <= 0)
+    return m2f::fail(M2F_EINVAL, "%s: non-positive size (N=%d S=%d M=%d D=%d L=%d Lq=%d P=%d)", fn, d.N,
+                     d.S, d.M, d.D, d.L, d.Lq, d.P);
+  if (im2col_step <= 0) return m2f::fail(M2F_EINVAL, "%s: im2col_step must be positive", fn);
+  const int step = std::min(d.N, im2col_step);
+  if (d.N % step != 0)
+    return m2f::fail(M2F_EINVAL, "%s: batch(%d) must divide im2col_step(%d)", fn, d.N, step);
+  return M2F_OK;
+}
+
+bool fast_f32_ok(const Dims& d, const void* value, const void* loc, const void* out4) {
+  const bool dims = (d.D == 16 || d.D == 32 || d.D == 64) && d.L <= kMaxLevels;
+  return dims && m2f::aligned(value, 16) && m2f::aligned(loc, 8) && m2f::aligned(out4, 16);
+}
+
+template <int D>
+void launch_fwd_vec(const float* value, const int64_t* shapes, const int64_t* lsi, const float* loc,
+                    const float* attn, const Dims& d, float* out, hipStream_t st) {
+  constexpr int G = D / 4;
+  const unsigned grid = m2f::ceil_div(d.npairs(), 256 / G);
+  if (d.P == 4)
+    msda_fwd_f32_vec<D, 4><<<grid, 256, 0, st>>>(value, shapes, lsi, loc, attn, d.npairs(), d.S, d.M, d.L,
+                                                  d.Lq, d.P, out);
+  else
+    msda_fwd_f32_vec<D, 0><<<grid, 256, 0, st>>>(value, shapes, lsi, loc, attn, d.npairs(), d.S, d.M, d.L,
+                                                  d.Lq, d.P, out);
+}
+
+template <int D>
+void launch_bwd_vec(const float* value, const int64_t* shapes, const int64_t* lsi, const float* loc,
+                    const float* attn, const float* gout, const Dims& d, float* gv, float* gl, float* ga,
+                    hipStream_t st) {
+  constexpr int G = D / 4;
+  const unsigned grid = m2f::ceil_div(d.npairs(), 256 / G);
+  if (d.P == 4)
+    msda_bwd_f32_vec<D, 4><<<grid, 256, 0, st>>>(value, shapes, lsi, loc, attn, gout, d.npairs(), d.S, d.M,
+                                                  d.L, d.Lq, d.P, gv, gl, ga);
+  else
+    msda_bwd_f32_vec<D, 0><<<grid, 256, 0, st>>>(value, shapes, lsi, loc, attn, gout, d.npairs(), d.S, d.M,
+                                                  d.L, d.Lq, d.P, gv, gl, ga);
+}
+
+template <typename T>
+int fwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_t* lsi, const T* loc,
+             const T* attn, const Dims& d, int im2col_step, T* out, hipStream_t st) {
+  int rc = check_dims(fn, value, shapes, lsi, loc, attn, d, im2col_step);
+  if (rc) return rc;
+  if (!out) return m2f::fail(M2F_EINVAL, "%s: null output", fn);
+  bool done = false;
+  if constexpr (std::is_same<T, float>::value) {
+    if (fast_f32_ok(d, value, loc, out)) {
+      if (d.D == 16) launch_fwd_vec<16>(value, shapes, lsi, loc, attn, d, out, st);
+      else if (d.D == 32) launch_fwd_vec<32>(value, shapes, lsi, loc, attn, d, out, st);
+      else launch_fwd_vec<64>(value, shapes, lsi, loc, attn, d, out, st);
+      done = true;
+    }
+  }
+  if (!done) {
+    const int64_t total = d.npairs() * d.D;
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>((total + 255) / 256, 256 * 64));
+    msda_fwd_generic<T><<<grid, 256, 0, st>>>(value, shapes, lsi, loc, attn, total, d.S, d.M, d.D, d.L, d.Lq,
+                                               d.P, out);
+  }
+  return m2f::check_launch(fn);
+}
+
+template <typename T>
+int bwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_t* lsi, const T* loc,
+             const T* attn, const T* gout, const Dims& d, int im2col_step, const int64_t* host_shapes, T* gv,
+             T* gl, T* ga, hipStream_t st) {
+  (void)host_shapes;
+  int rc = check_dims(fn, value, shapes, lsi, loc, attn, d, im2col_step);
+  if (rc) return rc;
+  if (!gout || !gv || !gl || !ga) return m2f::fail(M2F_EINVAL, "%s: null gradient pointer", fn);
+  const size_t gv_bytes = static_cast<size_t>(d.N) * d.S * d.M * d.D * sizeof(T);
+  hipError_t e = hipMemsetAsync(gv, 0, gv_bytes, st);
+  if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
+  bool done = false;
+  if constexpr (std::is_same<T, float>::value) {
+    if (fast_f32_ok(d, value, loc, gout) && m2f::aligned(gv, 16) && m2f::aligned(gl, 8)) {
+      if (d.D == 16) launch_bwd_vec<16>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
+      else if (d.D == 32) launch_bwd_vec<32>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
+      else launch_bwd_vec<64>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
+      done = true;
+    }
+  }
+  if (!done) {
+    const int64_t npairs = d.npairs();
+    if (npairs > 0x7fffffffLL) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many (n,q,m) pairs", fn);
+    if (d.D <= 64)
+      msda_bwd_generic<T, 64><<<static_cast<unsigned>(npairs), 64, 0, st>>>(
+          value, shapes, lsi, loc, attn, gout, d.S, d.M, d.D, d.L, d.Lq, d.P, gv, gl, ga);
+    else
+      msda_bwd_generic<T, 256><<<static_cast<unsigned>(npairs), 256, 0, st>>>(
+          value, shapes, lsi, loc, attn, gout, d.S, d.M, d.D, d.L, d.Lq, d.P, gv, gl, ga);
+  }
+  return m2f::check_launch(fn);
+}
+
+}  // namespace
+
+extern "C" int m2f_msda_fwd_f32(const float* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
+                                const float* sampling_loc, const float* attn_weight, int batch, int spatial_size,
+                                int num_heads, int channels, int num_levels, int num_query, int num_point,
+                                int im2col_step, const int64_t* host_spatial_shapes, float* output, void* stream) {
+  (void)host_spatial_shapes;
+  const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
+  return fwd_impl<float>("m2f_msda_fwd_f32", value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
+                         d, im2col_step, output, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int m2f_msda_fwd_f64(const double* value, const int64_t* spatial_shapes,
+                                const int64_t* level_start_index, const double* sampling_loc,
+                                const double* attn_weight, int batch, int spatial_size, int num_heads, int channels,
+                                int num_levels, int num_query, int num_point, int im2col_step,
+                                const int64_t* host_spatial_shapes, double* output, void* stream) {
+  (void)host_spatial_shapes;
+  const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
+  return fwd_impl<double>("m2f_msda_fwd_f64", value, spatial_shapes, level_start_index, sampling_loc,
+                          attn_weight, d, im2col_step, output, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int m2f_msda_bwd_f32(const float* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
+                                const float* sampling_loc, const float* attn_weight, const float* grad_output,
+                                int batch, int spatial_size, int num_heads, int channels, int num_levels,
+                                int num_query, int num_point, int im2col_step, const int64_t* host_spatial_shapes,
+                                float* grad_value, float* grad_sampling_loc, float* grad_attn_weight,
+                                void* stream) {
+  const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
+  return bwd_impl<float>("m2f_msda_bwd_f32", value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
+                         grad_output, d, im2col_step, host_spatial_shapes, grad_value, grad_sampling_loc,
+                         grad_attn_weight, static_cast<hipStream_t>(stream));
+}
+
+extern "C" int m2f_msda_bwd_f64(const double* value, const int64_t* spatial_shapes,
+                                const int64_t* level_start_index, const double* sampling_loc,
+                                const double* attn_weight, const double* grad_output, int batch, int spatial_size,
+                                int num_heads, int channels, int num_levels, int num_query, int num_point,
+                                int im2col_step, const int64_t* host_spatial_shapes, double* grad_value,
+                                double* grad_sampling_loc, double* grad_attn_weight, void* stream) {
+  const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
+  return bwd_impl<double>("m2f_msda_bwd_f64", value, spatial_shapes, level_start_index, sampling_loc,
+                          attn_weight, grad_output, d, im2col_step, host_spatial_shapes, grad_value,
+                          grad_sampling_loc, grad_attn_weight, static_cast<hipStream_t>(stream));
+}

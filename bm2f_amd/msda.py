@@ -1,0 +1,244 @@
+"""Multi-scale deformable attention: native op binding, autograd Function and nn.Module.
+
+Drop-in for the reference's op stack (paths relative to the reference root,
+``ops`` = ``mask2former/modeling/pixel_decoder/ops``):
+
+* :func:`ms_deform_attn_forward` / :func:`ms_deform_attn_backward` replace the pybind functions of the
+  compiled ``MultiScaleDeformableAttention`` module (``ops/src/vision.cpp:18-21``) with the same
+  argument order, preconditions and error behaviour (``ops/src/cuda/ms_deform_attn_cuda.cu:33-57,
+  98-124``: RuntimeError on non-contiguous / non-device inputs or a batch that ``im2col_step`` does not
+  divide), backed by the HIP kernels in ``csrc/msda.hip`` through the C ABI.
+* :class:`MSDeformAttnFunction` replaces ``ops/functions/ms_deform_attn_func.py:32-49``.
+* :class:`MSDeformAttn` replaces ``ops/modules/ms_deform_attn.py:34-125`` (same parameters, init and
+  forward), without the bare ``try/except`` that silently falls back to the CPU core (:116-121):
+  here a failure raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import warnings
+from typing import Optional, Sequence, Tuple
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+from torch.nn.init import constant_, xavier_uniform_
+
+from . import _native
+
+__all__ = [
+    "ms_deform_attn_forward",
+    "ms_deform_attn_backward",
+    "MSDeformAttnFunction",
+    "MSDeformAttn",
+    "attach_host_shapes",
+]
+
+_HOST_ATTR = "_bm2f_host_shapes"
+
+
+def attach_host_shapes(spatial_shapes: torch.Tensor, shapes: Sequence[Tuple[int, int]]) -> torch.Tensor:
+    """Record the host-side (H, W) list on a device ``spatial_shapes`` tensor.
+
+    The kernels only need the device tensor; the host copy lets the backward pick its spatially tiled
+    grad_value accumulation without a device->host sync.  Results are identical either way.
+    """
+    setattr(spatial_shapes, _HOST_ATTR, tuple((int(h), int(w)) for h, w in shapes))
+    return spatial_shapes
+
+
+def _host_shapes(spatial_shapes: torch.Tensor):
+    return getattr(spatial_shapes, _HOST_ATTR, None)
+
+
+def _check(t: torch.Tensor, name: str) -> None:
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} tensor has to be contiguous")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+
+
+def _ptr(t: torch.Tensor) -> int:
+    return t.data_ptr()
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _host_shape_buffer(shapes):
+    if shapes is None:
+        return None
+    flat = [v for hw in shapes for v in hw]
+    return (ctypes.c_int64 * len(flat))(*flat)
+
+
+def _dims(value, spatial_shapes, sampling_loc):
+    if value.dim() != 4:
+        raise RuntimeError(f"value must be (N, S, M, D), got shape {tuple(value.shape)}")
+    if sampling_loc.dim() != 6 or sampling_loc.shape[-1] != 2:
+        raise RuntimeError(f"sampling_loc must be (N, Lq, M, L, P, 2), got shape {tuple(sampling_loc.shape)}")
+    N, S, M, D = value.shape
+    L = spatial_shapes.shape[0]
+    Lq, P = sampling_loc.shape[1], sampling_loc.shape[4]
+    if sampling_loc.shape[0] != N or sampling_loc.shape[2] != M or sampling_loc.shape[3] != L:
+        raise RuntimeError("sampling_loc shape does not match value / spatial_shapes")
+    return N, S, M, D, L, Lq, P
+
+
+def _suffix(dtype: torch.dtype) -> str:
+    if dtype == torch.float32:
+        return "f32"
+    if dtype == torch.float64:
+        return "f64"
+    # the reference dispatches AT_DISPATCH_FLOATING_TYPES (ms_deform_attn_cuda.cu:69, :139)
+    raise RuntimeError(f'"ms_deform_attn_forward_cuda" not implemented for \'{dtype}\'')
+
+
+def ms_deform_attn_forward(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, im2col_step):
+    """Native forward; returns (N, Lq, M*D).  Same contract as the reference binding."""
+    for t, n in ((value, "value"), (spatial_shapes, "spatial_shapes"), (level_start_index, "level_start_index"),
+                 (sampling_loc, "sampling_loc"), (attn_weight, "attn_weight")):
+        _check(t, n)
+    sfx = _suffix(value.dtype)
+    if sampling_loc.dtype != value.dtype or attn_weight.dtype != value.dtype:
+        raise RuntimeError("value, sampling_loc and attn_weight must share a dtype")
+    if spatial_shapes.dtype != torch.int64 or level_start_index.dtype != torch.int64:
+        raise RuntimeError("spatial_shapes and level_start_index must be int64")
+    N, S, M, D, L, Lq, P = _dims(value, spatial_shapes, sampling_loc)
+    out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
+    host = _host_shape_buffer(_host_shapes(spatial_shapes))
+    _native.call(f"m2f_msda_fwd_{sfx}", _ptr(value), _ptr(spatial_shapes), _ptr(level_start_index),
+                 _ptr(sampling_loc), _ptr(attn_weight), N, S, M, D, L, Lq, P, int(im2col_step),
+                 ctypes.cast(host, ctypes.c_void_p) if host is not None else None, _ptr(out), _stream(value.device))
+    return out
+
+
+def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_loc, attn_weight, grad_output,
+                            im2col_step):
+    """Native backward; returns [grad_value, grad_sampling_loc, grad_attn_weight]."""
+    for t, n in ((value, "value"), (spatial_shapes, "spatial_shapes"), (level_start_index, "level_start_index"),
+                 (sampling_loc, "sampling_loc"), (attn_weight, "attn_weight"), (grad_output, "grad_output")):
+        _check(t, n)
+    sfx = _suffix(value.dtype)
+    if grad_output.dtype != value.dtype:
+        raise RuntimeError("grad_output must have the dtype of value")
+    N, S, M, D, L, Lq, P = _dims(value, spatial_shapes, sampling_loc)
+    grad_value = torch.empty_like(value)
+    grad_loc = torch.empty_like(sampling_loc)
+    grad_attn = torch.empty_like(attn_weight)
+    host = _host_shape_buffer(_host_shapes(spatial_shapes))
+    _native.call(f"m2f_msda_bwd_{sfx}", _ptr(value), _ptr(spatial_shapes), _ptr(level_start_index),
+                 _ptr(sampling_loc), _ptr(attn_weight), _ptr(grad_output), N, S, M, D, L, Lq, P, int(im2col_step),
+                 ctypes.cast(host, ctypes.c_void_p) if host is not None else None,
+                 _ptr(grad_value), _ptr(grad_loc), _ptr(grad_attn), _stream(value.device))
+    return [grad_value, grad_loc, grad_attn]
+
+
+class MSDeformAttnFunction(Function):
+    """Autograd wrapper, same ``apply`` signature as ops/functions/ms_deform_attn_func.py:32-49."""
+
+    @staticmethod
+    def forward(ctx, value, value_spatial_shapes, value_level_start_index, sampling_locations, attention_weights,
+                im2col_step):
+        ctx.im2col_step = im2col_step
+        ctx.host_shapes = _host_shapes(value_spatial_shapes)
+        output = ms_deform_attn_forward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
+                                        attention_weights, ctx.im2col_step)
+        ctx.save_for_backward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
+                              attention_weights)
+        return output
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_output):
+        value, shapes, lsi, loc, attn = ctx.saved_tensors
+        if ctx.host_shapes is not None and _host_shapes(shapes) is None:
+            attach_host_shapes(shapes, ctx.host_shapes)
+        grad_value, grad_loc, grad_attn = ms_deform_attn_backward(
+            value, shapes, lsi, loc, attn, grad_output.contiguous(), ctx.im2col_step)
+        return grad_value, None, None, grad_loc, grad_attn, None
+
+
+def _is_power_of_2(n):
+    if (not isinstance(n, int)) or (n < 0):
+        raise ValueError("invalid input for _is_power_of_2: {} (type: {})".format(n, type(n)))
+    return (n & (n - 1) == 0) and n != 0
+
+
+class MSDeformAttn(nn.Module):
+    """Multi-scale deformable attention layer (ops/modules/ms_deform_attn.py:34-125).
+
+    Parameters and their initialisation match the reference so checkpoints load unchanged:
+    ``sampling_offsets`` (M*L*P*2, C), ``attention_weights`` (M*L*P, C), ``value_proj``, ``output_proj``.
+    """
+
+    def __init__(self, d_model=256, n_levels=4, n_heads=8, n_points=4):
+        super().__init__()
+        if d_model % n_heads != 0:
+            raise ValueError("d_model must be divisible by n_heads, but got {} and {}".format(d_model, n_heads))
+        _d_per_head = d_model // n_heads
+        if not _is_power_of_2(_d_per_head):
+            warnings.warn("MSDeformAttn: a power-of-2 head dimension selects the vectorised gfx950 kernels; "
+                          f"{_d_per_head} runs on the generic kernels.")
+        self.im2col_step = 128
+        self.d_model = d_model
+        self.n_levels = n_levels
+        self.n_heads = n_heads
+        self.n_points = n_points
+        self.sampling_offsets = nn.Linear(d_model, n_heads * n_levels * n_points * 2)
+        self.attention_weights = nn.Linear(d_model, n_heads * n_levels * n_points)
+        self.value_proj = nn.Linear(d_model, d_model)
+        self.output_proj = nn.Linear(d_model, d_model)
+        self._reset_parameters()
+
+    def _reset_parameters(self):
+        # ms_deform_attn.py:66-80: offsets start on 8 rays at distance 1..P, uniform attention
+        constant_(self.sampling_offsets.weight.data, 0.0)
+        thetas = torch.arange(self.n_heads, dtype=torch.float32) * (2.0 * math.pi / self.n_heads)
+        grid = torch.stack([thetas.cos(), thetas.sin()], -1)
+        grid = grid / grid.abs().max(-1, keepdim=True)[0]
+        grid = grid.view(self.n_heads, 1, 1, 2).repeat(1, self.n_levels, self.n_points, 1)
+        grid = grid * torch.arange(1, self.n_points + 1, dtype=torch.float32).view(1, 1, -1, 1)
+        with torch.no_grad():
+            self.sampling_offsets.bias = nn.Parameter(grid.reshape(-1))
+        constant_(self.attention_weights.weight.data, 0.0)
+        constant_(self.attention_weights.bias.data, 0.0)
+        xavier_uniform_(self.value_proj.weight.data)
+        constant_(self.value_proj.bias.data, 0.0)
+        xavier_uniform_(self.output_proj.weight.data)
+        constant_(self.output_proj.bias.data, 0.0)
+
+    def sampling(self, query, reference_points, input_spatial_shapes):
+        """Sampling locations (N, Lq, M, L, P, 2) and softmaxed weights (N, Lq, M, L, P)."""
+        N, Len_q, _ = query.shape
+        M, L, P = self.n_heads, self.n_levels, self.n_points
+        offsets = self.sampling_offsets(query).view(N, Len_q, M, L, P, 2)
+        attn = self.attention_weights(query).view(N, Len_q, M, L * P)
+        attn = F.softmax(attn, -1).view(N, Len_q, M, L, P)
+        if reference_points.shape[-1] == 2:
+            normalizer = torch.stack([input_spatial_shapes[..., 1], input_spatial_shapes[..., 0]], -1)
+            loc = reference_points[:, :, None, :, None, :] + offsets / normalizer[None, None, None, :, None, :]
+        elif reference_points.shape[-1] == 4:
+            loc = (reference_points[:, :, None, :, None, :2]
+                   + offsets / P * reference_points[:, :, None, :, None, 2:] * 0.5)
+        else:
+            raise ValueError("Last dim of reference_points must be 2 or 4, but get {} instead.".format(
+                reference_points.shape[-1]))
+        return loc, attn
+
+    def forward(self, query, reference_points, input_flatten, input_spatial_shapes, input_level_start_index,
+                input_padding_mask=None):
+        N, Len_q, _ = query.shape
+        N, Len_in, _ = input_flatten.shape
+        value = self.value_proj(input_flatten)
+        if input_padding_mask is not None:
+            value = value.masked_fill(input_padding_mask[..., None], float(0))
+        value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
+        loc, attn = self.sampling(query, reference_points, input_spatial_shapes)
+        output = MSDeformAttnFunction.apply(value.contiguous(), input_spatial_shapes, input_level_start_index,
+                                            loc.contiguous(), attn.contiguous(), self.im2col_step)
+        return self.output_proj(output)

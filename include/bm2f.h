@@ -1,0 +1,93 @@
+/*
+ * bm2f.h — C ABI of the MI355X (gfx950) Mask2Former hot-path library `libbm2f.so`.
+ *
+ * Every entry point takes plain device pointers, sizes and a `hipStream_t` passed as `void*`
+ * (torch's current stream on the Python side), launches asynchronously on that stream and
+ * returns 0 on success or a nonzero M2F_E* code; `m2f_last_error()` then holds a message for the
+ * calling thread.  Outputs are allocated by the caller; each function fully initialises them
+ * (the reference zero-fills with at::zeros, ms_deform_attn_cuda.cu:59 / :126-128).
+ *
+ * Reference interfaces replaced (paths relative to the reference root,
+ * ops = mask2former/modeling/pixel_decoder/ops):
+ *   m2f_msda_fwd_{f32,f64}  <- ms_deform_attn_forward   (ops/src/vision.cpp:19, ops/src/ms_deform_attn.h:25-44,
+ *                                                        ops/src/cuda/ms_deform_attn_cuda.cu:25-85)
+ *   m2f_msda_bwd_{f32,f64}  <- ms_deform_attn_backward  (ops/src/vision.cpp:20, ops/src/ms_deform_attn.h:46-67,
+ *                                                        ops/src/cuda/ms_deform_attn_cuda.cu:88-157)
+ *   m2f_attn_mask_*         <- MultiScaleMaskedTransformerDecoder.forward_prediction_heads resize+threshold
+ *                              (transformer_decoder/mask2former_transformer_decoder.py:446-450) and the
+ *                              fully-masked-row fix (:400)
+ *   m2f_masked_attn_*       <- the attention core of nn.MultiheadAttention(attn_mask=bool) used by
+ *                              CrossAttentionLayer.forward_post (mask2former_transformer_decoder.py:98-110)
+ *   m2f_mask_einsum_*       <- torch.einsum("bqc,bchw->bqhw") (mask2former_transformer_decoder.py:442)
+ *
+ * Preconditions mirrored from the reference (ms_deform_attn_cuda.cu:33-43, :55-57, :98-124):
+ *   batch % min(batch, im2col_step) == 0, else M2F_EINVAL.  All tensors contiguous (checked by the
+ *   Python wrapper, which owns the strides).  spatial_shapes / level_start_index are int64 device
+ *   arrays of (L,2) and (L,).
+ */
+#ifndef BM2F_H_
+#define BM2F_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  M2F_OK = 0,
+  M2F_EINVAL = 1,      /* bad sizes / null pointers / precondition violated */
+  M2F_ELAUNCH = 2,     /* HIP launch or runtime error */
+  M2F_EUNSUPPORTED = 3 /* configuration this build does not implement */
+};
+
+/* Message for the last nonzero return on this thread ("" if none). */
+const char* m2f_last_error(void);
+/* ABI version, bumped whenever a signature below changes. */
+int m2f_abi_version(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Multi-scale deformable attention.
+ *   value            (N, S, M, D)          S = sum_l H_l*W_l
+ *   spatial_shapes   (L, 2) int64 [H, W]   device
+ *   level_start_index(L,)   int64          device
+ *   sampling_loc     (N, Lq, M, L, P, 2)   [x, y] normalised to [0,1]
+ *   attn_weight      (N, Lq, M, L, P)
+ *   output           (N, Lq, M*D)
+ * host_spatial_shapes: optional host copy of spatial_shapes (L*2 int64, may be NULL).  When given
+ * and Lq == S (encoder self-attention over the flattened pyramid) the backward groups queries by
+ * spatial tile and accumulates grad_value in LDS windows; results do not depend on it.
+ * ------------------------------------------------------------------------------------------- */
+int m2f_msda_fwd_f32(const float* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
+                     const float* sampling_loc, const float* attn_weight,
+                     int batch, int spatial_size, int num_heads, int channels,
+                     int num_levels, int num_query, int num_point, int im2col_step,
+                     const int64_t* host_spatial_shapes, float* output, void* stream);
+
+int m2f_msda_fwd_f64(const double* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
+                     const double* sampling_loc, const double* attn_weight,
+                     int batch, int spatial_size, int num_heads, int channels,
+                     int num_levels, int num_query, int num_point, int im2col_step,
+                     const int64_t* host_spatial_shapes, double* output, void* stream);
+
+/* grad_value (N,S,M,D) is zeroed and accumulated; grad_sampling_loc / grad_attn_weight are
+ * written for every element (zero where the sample fell outside its level). */
+int m2f_msda_bwd_f32(const float* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
+                     const float* sampling_loc, const float* attn_weight, const float* grad_output,
+                     int batch, int spatial_size, int num_heads, int channels,
+                     int num_levels, int num_query, int num_point, int im2col_step,
+                     const int64_t* host_spatial_shapes,
+                     float* grad_value, float* grad_sampling_loc, float* grad_attn_weight, void* stream);
+
+int m2f_msda_bwd_f64(const double* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
+                     const double* sampling_loc, const double* attn_weight, const double* grad_output,
+                     int batch, int spatial_size, int num_heads, int channels,
+                     int num_levels, int num_query, int num_point, int im2col_step,
+                     const int64_t* host_spatial_shapes,
+                     double* grad_value, double* grad_sampling_loc, double* grad_attn_weight, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BM2F_H_ */
