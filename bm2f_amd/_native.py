@@ -20,6 +20,8 @@ ABI_VERSION = 1
 
 _p = ctypes.c_void_p
 _i = ctypes.c_int
+_f = ctypes.c_float
+_l = ctypes.c_int64
 
 # name -> argtypes (all return int status)
 _SIGNATURES = {
@@ -27,6 +29,11 @@ _SIGNATURES = {
     "m2f_msda_fwd_f64": [_p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p],
     "m2f_msda_bwd_f32": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p],
     "m2f_msda_bwd_f64": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _p, _p],
+    "m2f_attn_mask_bits": [_p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _i, _p],
+    "m2f_masked_attn_plan": [_i, _i, _i, _i, _p, _p, _p, _p],
+    "m2f_masked_attn_fwd": [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _f, _p, _p, _p, _l, _p],
+    "m2f_masked_attn_bwd": [_i, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _f, _p, _p, _p, _p,
+                            _l, _p],
 }
 
 

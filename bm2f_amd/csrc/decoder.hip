@@ -1,0 +1,835 @@
+// Masked-attention decoder kernels for gfx950 (reference
+// mask2former/modeling/transformer_decoder/mask2former_transformer_decoder.py).
+//
+// 1. attn-mask bitmask: forward_prediction_heads' bilinear resize of the mask logits (:446), the
+//    `sigmoid() < 0.5` threshold in the logits' dtype (:449) and the next layer's fully-masked-row
+//    fix (:400), fused into one pass that writes ONE bit per (b, q, key) shared by all heads instead
+//    of the reference's head-repeated (B*h, Q, HW) bool tensor.
+// 2. masked cross-attention core: softmax(scale * q k^T  +  mask) v per (b, head), flash style
+//    (online softmax, no score matrix in HBM), on 16x16 MFMA tiles (bf16 / fp16: 16x16x16, fp32:
+//    16x16x4), key range split over workgroups with a combine pass; backward recomputes P from the
+//    saved log-sum-exp.  Replaces the math path of nn.MultiheadAttention(attn_mask=bool) used by
+//    CrossAttentionLayer.forward_post (:98-110); the q/k/v/out projections stay dense GEMMs.
+//
+// MFMA operand maps used throughout (16x16xK, lane = 16*g + r):
+//   A: lane holds A[row r][k = kw*g + j]   B: lane holds B[k = kw*g + j][col r]   (kw = 4 for 16-bit, 1 for f32)
+//   C: lane holds C[row 4*g + i][col r], i = 0..3
+#include "common.h"
+
+#include <cmath>
+
+namespace {
+
+using f4 = float __attribute__((ext_vector_type(4)));
+using s4 = short __attribute__((ext_vector_type(4)));
+using h4 = _Float16 __attribute__((ext_vector_type(4)));
+using lds_s4 = __attribute__((address_space(3))) s4;
+
+constexpr int kD = 32;       // head dim (hidden 256 / 8 heads)
+constexpr int kDP = kD + 4;  // padded LDS row (elements) for 16-bit images: 72 B rows, 8 B aligned
+constexpr float kLog2e = 1.4426950408889634f;
+
+// ----------------------------------------------------------------------------------------------
+// element traits
+// ----------------------------------------------------------------------------------------------
+template <typename T> struct Elt;
+template <> struct Elt<float> {
+  static constexpr bool k16 = false;
+  __device__ static float to_f(float x) { return x; }
+  __device__ static float from_f(float x) { return x; }
+};
+template <> struct Elt<__bf16> {
+  static constexpr bool k16 = true;
+  __device__ static float to_f(__bf16 x) { return static_cast<float>(x); }
+  __device__ static __bf16 from_f(float x) { return static_cast<__bf16>(x); }
+};
+template <> struct Elt<_Float16> {
+  static constexpr bool k16 = true;
+  __device__ static float to_f(_Float16 x) { return static_cast<float>(x); }
+  __device__ static _Float16 from_f(float x) { return static_cast<_Float16>(x); }
+};
+
+template <typename T>
+__device__ __forceinline__ f4 mma16(s4 a, s4 b, f4 c) {
+  if constexpr (std::is_same<T, _Float16>::value)
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(__builtin_bit_cast(h4, a), __builtin_bit_cast(h4, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ f4 mma32(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <typename T>
+__device__ __forceinline__ s4 pack4(float a, float b, float c, float d) {
+  T t[4] = {Elt<T>::from_f(a), Elt<T>::from_f(b), Elt<T>::from_f(c), Elt<T>::from_f(d)};
+  return *reinterpret_cast<s4*>(t);
+}
+
+// Transposed 4x16 read: lane 4q+p of each 16-lane group passes the address of row q, columns
+// 4p..4p+3 of its block; lane i receives column i of the 4 rows (row q in element q).
+__device__ __forceinline__ s4 tr_read(const void* lds_ptr) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_s4*)(reinterpret_cast<uintptr_t>(lds_ptr)));
+}
+
+__device__ __forceinline__ float wave_max16(float x) {  // reduce over the 4 lane groups (same r)
+  x = fmaxf(x, __shfl_xor(x, 16));
+  return fmaxf(x, __shfl_xor(x, 32));
+}
+__device__ __forceinline__ float wave_sum16(float x) {
+  x += __shfl_xor(x, 16);
+  return x + __shfl_xor(x, 32);
+}
+
+// ----------------------------------------------------------------------------------------------
+// 1. attention-mask bits
+// ----------------------------------------------------------------------------------------------
+// One workgroup per (b, q) row.  value at target pixel (y, x) follows upsample_bilinear2d
+// (align_corners=False): src = max(scale*(dst+0.5)-0.5, 0), i0 = (int)src, i1 = i0 + (i0 < in-1),
+// lambda = src - i0; accumulated in fp32 and rounded to T; then s = T(1/(1+exp(-v))) and
+// blocked = s < 0.5.  Contraction is disabled so the arithmetic is the literal formula.
+template <typename T>
+__global__ void __launch_bounds__(256) attn_mask_bits_kernel(const T* __restrict__ logits, int frames, int Hin,
+                                                             int Win, int Hout, int Wout, int nwords, int row_fix,
+                                                             uint32_t* __restrict__ bits) {
+#pragma clang fp contract(off)
+  extern __shared__ uint32_t sbits[];
+  __shared__ int sblocked;
+  const int64_t row = blockIdx.x;
+  const int64_t frame_elems = static_cast<int64_t>(Hin) * Win;
+  const T* src_row = logits + row * frames * frame_elems;
+  const int HWo = Hout * Wout;
+  const int HW = frames * HWo;  // keys of the row: frame-major, then row-major pixels
+  const float rh = static_cast<float>(Hin) / static_cast<float>(Hout);
+  const float rw = static_cast<float>(Win) / static_cast<float>(Wout);
+  if (threadIdx.x == 0) sblocked = 0;
+  __syncthreads();
+  int count = 0;
+  for (int base = 0; base < nwords * 32; base += 256) {
+    const int pix = base + threadIdx.x;
+    bool blocked = false;
+    if (pix < HW) {
+      const int f = pix / HWo, fp = pix - f * HWo;
+      const T* src = src_row + f * frame_elems;
+      const int y = fp / Wout, x = fp - y * Wout;
+      float sy = rh * (static_cast<float>(y) + 0.5f) - 0.5f;
+      sy = sy < 0.f ? 0.f : sy;
+      float sx = rw * (static_cast<float>(x) + 0.5f) - 0.5f;
+      sx = sx < 0.f ? 0.f : sx;
+      const int y0 = static_cast<int>(sy), x0 = static_cast<int>(sx);
+      const int yp = (y0 < Hin - 1) ? 1 : 0, xp = (x0 < Win - 1) ? 1 : 0;
+      const float ly1 = sy - static_cast<float>(y0), ly0 = 1.f - ly1;
+      const float lx1 = sx - static_cast<float>(x0), lx0 = 1.f - lx1;
+      const float a = Elt<T>::to_f(src[y0 * Win + x0]);
+      const float b = Elt<T>::to_f(src[y0 * Win + x0 + xp]);
+      const float c = Elt<T>::to_f(src[(y0 + yp) * Win + x0]);
+      const float d = Elt<T>::to_f(src[(y0 + yp) * Win + x0 + xp]);
+      const float v = ly0 * (lx0 * a + lx1 * b) + ly1 * (lx0 * c + lx1 * d);
+      const float vt = Elt<T>::to_f(Elt<T>::from_f(v));
+      const float s = Elt<T>::to_f(Elt<T>::from_f(1.f / (1.f + expf(-vt))));
+      blocked = s < 0.5f;
+    }
+    const unsigned long long bal = __ballot(blocked);
+    count += blocked ? 1 : 0;
+    const int lane = threadIdx.x & 63;
+    const int word = (base + (threadIdx.x & ~63)) >> 5;
+    if (lane == 0 && word < nwords) sbits[word] = static_cast<uint32_t>(bal);
+    if (lane == 32 && word + 1 < nwords) sbits[word + 1] = static_cast<uint32_t>(bal >> 32);
+  }
+  // row total
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) count += __shfl_xor(count, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&sblocked, count);
+  __syncthreads();
+  const bool all_blocked = row_fix && sblocked == HW;
+  uint32_t* dst = bits + row * nwords;
+  for (int w = threadIdx.x; w < nwords; w += 256) dst[w] = all_blocked ? 0u : sbits[w];
+}
+
+// ----------------------------------------------------------------------------------------------
+// 2. masked attention forward
+// ----------------------------------------------------------------------------------------------
+// grid (B*H, nchunks), 256 threads.  Wave w owns query tiles w, w+4, ... (TPW of them).  Keys are
+// streamed in blocks of 64 through a double-buffered LDS image; S^T = K Q^T is computed so that the
+// query is the lane's MFMA column: the online-softmax row statistics are in-lane plus two shuffles,
+// and P^T is already the B operand of O^T += V^T P^T.
+template <typename T>
+struct KVImage {
+  static constexpr int RS = Elt<T>::k16 ? kDP : (kD + 1);  // row stride (elements)
+  static constexpr int ELEMS = 64 * RS;
+};
+
+template <typename T>
+__device__ __forceinline__ void stage_load(const T* __restrict__ src, int64_t row0, int nrows_valid, int stride,
+                                           int col0, f4 (&reg)[2]) {
+  // 64 rows x 32 elements; 16-bit: 256 x 16 B (one per thread); f32: 512 x 16 B (two per thread)
+  constexpr int PER = Elt<T>::k16 ? 8 : 4;
+  constexpr int PARTS = kD / PER;
+  constexpr int ITERS = Elt<T>::k16 ? 1 : 2;
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int idx = threadIdx.x + it * 256;
+    const int rr = idx / PARTS, part = idx % PARTS;
+    if (rr < nrows_valid)
+      reg[it] = *reinterpret_cast<const f4*>(src + (row0 + rr) * stride + col0 + part * PER);
+    else
+      reg[it] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void stage_store(T* img, const f4 (&reg)[2]) {
+  constexpr int PER = Elt<T>::k16 ? 8 : 4;
+  constexpr int PARTS = kD / PER;
+  constexpr int ITERS = Elt<T>::k16 ? 1 : 2;
+  constexpr int RS = KVImage<T>::RS;
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    const int idx = threadIdx.x + it * 256;
+    const int rr = idx / PARTS, part = idx % PARTS;
+    T* dst = img + rr * RS + part * PER;
+    if constexpr (Elt<T>::k16) {
+      // 72 B rows: 8 B aligned, store as two 8 B halves
+      const s4* s = reinterpret_cast<const s4*>(&reg[it]);
+      reinterpret_cast<s4*>(dst)[0] = s[0];
+      reinterpret_cast<s4*>(dst)[1] = s[1];
+    } else {
+      const float* s = reinterpret_cast<const float*>(&reg[it]);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[e] = s[e];
+    }
+  }
+}
+
+template <typename T, int TPW>
+__global__ void __launch_bounds__(256) mattn_fwd_kernel(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
+    int Lq, int Lk, int H, int qs, int kvs, int nw, float sl2, int chunk_len, T* __restrict__ out,
+    float* __restrict__ lse2, float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+  constexpr bool k16 = Elt<T>::k16;
+  constexpr int RS = KVImage<T>::RS;
+  __shared__ T Ks[2][KVImage<T>::ELEMS];
+  __shared__ T Vs[2][KVImage<T>::ELEMS];
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int nchunks = gridDim.y, c = blockIdx.y;
+  const int key_begin = c * chunk_len;
+  const int key_end = min(Lk, key_begin + chunk_len);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  const int64_t kvrow0 = static_cast<int64_t>(b) * Lk;
+
+  // query operands (B of S^T = K Q^T): lane holds Q[q = tile*16 + r][d = dc + kw*g + j]
+  s4 qb16[TPW][2];
+  float qb32[TPW][8];
+  f4 o[TPW][2];
+  float m_run[TPW], l_run[TPW];
+  uint32_t mrow_ok[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int qi = (w + 4 * t) * 16 + r;
+    const bool ok = qi < Lq;
+    mrow_ok[t] = ok;
+    const T* qrow = q + (static_cast<int64_t>(b) * Lq + (ok ? qi : 0)) * qs + h * kD;
+    if constexpr (k16) {
+#pragma unroll
+      for (int dc = 0; dc < 2; ++dc) {
+        const s4 val = *reinterpret_cast<const s4*>(qrow + dc * 16 + 4 * g);
+        qb16[t][dc] = ok ? val : s4{0, 0, 0, 0};
+      }
+    } else {
+#pragma unroll
+      for (int dc = 0; dc < 8; ++dc) qb32[t][dc] = ok ? Elt<T>::to_f(qrow[dc * 4 + g]) : 0.f;
+    }
+    o[t][0] = f4{0.f, 0.f, 0.f, 0.f};
+    o[t][1] = f4{0.f, 0.f, 0.f, 0.f};
+    m_run[t] = -INFINITY;
+    l_run[t] = 0.f;
+  }
+
+  f4 kreg[2], vreg[2];
+  int buf = 0;
+  if (key_begin < key_end) {
+    stage_load<T>(k, kvrow0 + key_begin, key_end - key_begin, kvs, h * kD, kreg);
+    stage_load<T>(v, kvrow0 + key_begin, key_end - key_begin, kvs, h * kD, vreg);
+    stage_store<T>(Ks[0], kreg);
+    stage_store<T>(Vs[0], vreg);
+  }
+  __syncthreads();
+
+  for (int kb0 = key_begin; kb0 < key_end; kb0 += 64) {
+    const int next = kb0 + 64;
+    if (next < key_end) {  // prefetch the next block into registers
+      stage_load<T>(k, kvrow0 + next, key_end - next, kvs, h * kD, kreg);
+      stage_load<T>(v, kvrow0 + next, key_end - next, kvs, h * kD, vreg);
+    }
+    const T* Kc = Ks[buf];
+    const T* Vc = Vs[buf];
+    const int kvalid = key_end - kb0;  // keys of this block that exist
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      if ((w + 4 * t) * 16 >= Lq) continue;  // wave-uniform
+      const int qi = (w + 4 * t) * 16 + r;
+      uint32_t w0 = 0xffffffffu, w1 = 0xffffffffu;
+      if (mrow_ok[t]) {
+        const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + qi) * nw + (kb0 >> 5);
+        w0 = mr[0];
+        w1 = ((kb0 >> 5) + 1 < nw) ? mr[1] : 0xffffffffu;
+      }
+      f4 st[4];
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+        if constexpr (k16) {
+#pragma unroll
+          for (int dc = 0; dc < 2; ++dc) {
+            const s4 a = *reinterpret_cast<const s4*>(Kc + (16 * kt + r) * RS + dc * 16 + 4 * g);
+            acc = mma16<T>(a, qb16[t][dc], acc);
+          }
+        } else {
+#pragma unroll
+          for (int dc = 0; dc < 8; ++dc) acc = mma32(Elt<T>::to_f(Kc[(16 * kt + r) * RS + dc * 4 + g]), qb32[t][dc], acc);
+        }
+        st[kt] = acc;
+      }
+      // mask + scale, block max
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int off = 16 * kt + 4 * g + i;
+          const uint32_t word = off < 32 ? w0 : w1;
+          const bool blocked = ((word >> (off & 31)) & 1u) || off >= kvalid;
+          const float s = blocked ? -INFINITY : st[kt][i] * sl2;
+          st[kt][i] = s;
+          mx = fmaxf(mx, s);
+        }
+      }
+      mx = wave_max16(mx);
+      const float m_new = fmaxf(m_run[t], mx);
+      const float m_use = m_new == -INFINITY ? 0.f : m_new;
+      const float alpha = exp2f(m_run[t] - m_use);
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float p = exp2f(st[kt][i] - m_use);
+          st[kt][i] = p;
+          rs += p;
+        }
+      }
+      rs = wave_sum16(rs);
+      l_run[t] = l_run[t] * alpha + rs;
+      m_run[t] = m_new;
+      o[t][0] *= alpha;
+      o[t][1] *= alpha;
+      // O^T[d][q] += V^T[d][key] P^T[key][q]
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        if constexpr (k16) {
+          const s4 pb = pack4<T>(st[kt][0], st[kt][1], st[kt][2], st[kt][3]);
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const s4 va = tr_read(Vc + (16 * kt + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3));
+            o[t][dt] = mma16<T>(va, pb, o[t][dt]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+              o[t][dt] = mma32(Elt<T>::to_f(Vc[(16 * kt + 4 * g + i) * RS + dt * 16 + r]), st[kt][i], o[t][dt]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (next < key_end) {
+      stage_store<T>(Ks[buf ^ 1], kreg);
+      stage_store<T>(Vs[buf ^ 1], vreg);
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // epilogue: lane holds O^T[d = dt*16 + 4g + i][q = r]
+  const int BH = gridDim.x;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    if (!mrow_ok[t]) continue;
+    const int qi = (w + 4 * t) * 16 + r;
+    if (nchunks == 1) {
+      const float inv = l_run[t] > 0.f ? 1.f / l_run[t] : 0.f;
+      T* orow = out + (static_cast<int64_t>(b) * Lq + qi) * (H * kD) + h * kD;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const f4 val = o[t][dt] * inv;
+        if constexpr (k16) {
+          *reinterpret_cast<s4*>(orow + dt * 16 + 4 * g) = pack4<T>(val[0], val[1], val[2], val[3]);
+        } else {
+          *reinterpret_cast<f4*>(orow + dt * 16 + 4 * g) = val;
+        }
+      }
+      if (g == 0) lse2[static_cast<int64_t>(bh) * Lq + qi] = l_run[t] > 0.f ? m_run[t] + log2f(l_run[t]) : INFINITY;
+    } else {
+      const int64_t prow = (static_cast<int64_t>(c) * BH + bh) * Lq + qi;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) *reinterpret_cast<f4*>(ws_o + prow * kD + dt * 16 + 4 * g) = o[t][dt];
+      if (g == 0) {
+        ws_ml[2 * prow] = m_run[t];
+        ws_ml[2 * prow + 1] = l_run[t];
+      }
+    }
+  }
+}
+
+// Combine the per-chunk partials: one thread per (b*h, q, 4 channels).
+template <typename T>
+__global__ void __launch_bounds__(256) mattn_combine_kernel(const float* __restrict__ ws_o,
+                                                            const float* __restrict__ ws_ml, int nchunks, int BH,
+                                                            int H, int Lq, T* __restrict__ out,
+                                                            float* __restrict__ lse2) {
+  const int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  const int64_t total = static_cast<int64_t>(BH) * Lq * (kD / 4);
+  if (idx >= total) return;
+  const int part = static_cast<int>(idx % (kD / 4));
+  const int64_t row = idx / (kD / 4);  // bh * Lq + q
+  const int bh = static_cast<int>(row / Lq), qi = static_cast<int>(row % Lq);
+  const int b = bh / H, h = bh % H;
+  float M = -INFINITY;
+  for (int c = 0; c < nchunks; ++c) M = fmaxf(M, ws_ml[2 * ((static_cast<int64_t>(c) * BH) * Lq + row)]);
+  const float Mu = M == -INFINITY ? 0.f : M;
+  float L = 0.f;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < nchunks; ++c) {
+    const int64_t prow = static_cast<int64_t>(c) * BH * Lq + row;
+    const float wgt = exp2f(ws_ml[2 * prow] - Mu);
+    L += ws_ml[2 * prow + 1] * wgt;
+    acc += *reinterpret_cast<const f4*>(ws_o + prow * kD + part * 4) * wgt;
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  acc *= inv;
+  T* orow = out + (static_cast<int64_t>(b) * Lq + qi) * (H * kD) + h * kD + part * 4;
+  if constexpr (Elt<T>::k16) {
+    *reinterpret_cast<s4*>(orow) = pack4<T>(acc[0], acc[1], acc[2], acc[3]);
+  } else {
+    *reinterpret_cast<f4*>(orow) = acc;
+  }
+  if (part == 0) lse2[row] = L > 0.f ? M + log2f(L) : INFINITY;
+}
+
+// ----------------------------------------------------------------------------------------------
+// 3. masked attention backward
+// ----------------------------------------------------------------------------------------------
+// grid (B*H, nchunks), 256 threads.  Per 64-key block wave w owns key tile w: dK^T and dV^T stay in
+// registers; S = Q K^T is computed with the query on rows so that P and dS (C layout) are directly
+// the B operands of dV^T += dO^T P and dK^T += Q^T dS; dQ^T += K^T dS^T needs dS^T, transposed
+// through a per-wave 16x16 LDS scratch, and is summed over the workgroup's waves with LDS float
+// atomics, then over chunks by a reduce pass (deterministic across chunks).
+template <typename T>
+__global__ void __launch_bounds__(256) mattn_bwd_kernel(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
+    const T* __restrict__ out, const T* __restrict__ dout, const float* __restrict__ lse2, int Lq, int Lk, int H,
+    int qs, int kvs, int nw, float sl2, float scale, int chunk_len, int Lqp, T* __restrict__ dq,
+    T* __restrict__ dk, T* __restrict__ dv, float* __restrict__ ws_dq) {
+  constexpr bool k16 = Elt<T>::k16;
+  constexpr int RS = KVImage<T>::RS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // carve: Qs, dOs [Lqp][RS] T | Ks, Vs [64][RS] T | lse, delta [Lqp] f32 | mw [Lqp][2] u32 |
+  //        scr [4][16][17] f32 | dQacc [Lqp][kD] f32
+  T* Qs = reinterpret_cast<T*>(smem);
+  T* dOs = Qs + Lqp * RS;
+  T* Ks = dOs + Lqp * RS;
+  T* Vs = Ks + 64 * RS;
+  size_t off = (reinterpret_cast<unsigned char*>(Vs + 64 * RS) - smem + 15) & ~size_t(15);
+  float* lse_s = reinterpret_cast<float*>(smem + off);
+  float* del_s = lse_s + Lqp;
+  uint32_t* mw = reinterpret_cast<uint32_t*>(del_s + Lqp);
+  float* scr = reinterpret_cast<float*>(mw + 2 * Lqp);
+  float* dqa = scr + 4 * 16 * 17;
+
+  const int bh = blockIdx.x, b = bh / H, h = bh % H;
+  const int nchunks = gridDim.y, c = blockIdx.y;
+  const int key_begin = c * chunk_len;
+  const int key_end = min(Lk, key_begin + chunk_len);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  const int64_t kvrow0 = static_cast<int64_t>(b) * Lk;
+  const int NT = Lqp / 16;
+  const int HD = H * kD;
+
+  // stage Q, dO (rows >= Lq zero), lse, delta; clear dQ accumulator
+  for (int idx = threadIdx.x; idx < Lqp * kD; idx += 256) {
+    const int qi = idx / kD, d = idx % kD;
+    T qv = Elt<T>::from_f(0.f), gv = Elt<T>::from_f(0.f);
+    if (qi < Lq) {
+      qv = q[(static_cast<int64_t>(b) * Lq + qi) * qs + h * kD + d];
+      gv = dout[(static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + d];
+    }
+    Qs[qi * RS + d] = qv;
+    dOs[qi * RS + d] = gv;
+    dqa[idx] = 0.f;
+  }
+  for (int qi = threadIdx.x; qi < Lqp; qi += 256) {
+    float dl = 0.f, ls = INFINITY;
+    if (qi < Lq) {
+      const T* orow = out + (static_cast<int64_t>(b) * Lq + qi) * HD + h * kD;
+      const T* grow = dout + (static_cast<int64_t>(b) * Lq + qi) * HD + h * kD;
+      for (int d = 0; d < kD; ++d) dl += Elt<T>::to_f(orow[d]) * Elt<T>::to_f(grow[d]);
+      ls = lse2[static_cast<int64_t>(bh) * Lq + qi];
+    }
+    del_s[qi] = dl;
+    lse_s[qi] = ls;
+  }
+
+  float* myscr = scr + w * 16 * 17;
+  for (int kb0 = key_begin; kb0 < key_end; kb0 += 64) {
+    __syncthreads();  // previous block's images fully consumed (and the prologue staged)
+    f4 kreg[2], vreg[2];
+    stage_load<T>(k, kvrow0 + kb0, key_end - kb0, kvs, h * kD, kreg);
+    stage_load<T>(v, kvrow0 + kb0, key_end - kb0, kvs, h * kD, vreg);
+    stage_store<T>(Ks, kreg);
+    stage_store<T>(Vs, vreg);
+    for (int qi = threadIdx.x; qi < Lqp; qi += 256) {
+      uint32_t a0 = 0xffffffffu, a1 = 0xffffffffu;
+      if (qi < Lq) {
+        const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + qi) * nw + (kb0 >> 5);
+        a0 = mr[0];
+        a1 = ((kb0 >> 5) + 1 < nw) ? mr[1] : 0xffffffffu;
+      }
+      mw[2 * qi] = a0;
+      mw[2 * qi + 1] = a1;
+    }
+    __syncthreads();
+    const int kvalid = key_end - kb0;
+    const int koff = 16 * w + r;  // this lane's key (column) within the block
+    if (16 * w >= kvalid) continue;  // whole tile beyond the chunk (wave-uniform); barriers are at loop top
+
+    // per-key-tile operands: K, V as B[k = d][col = key]
+    s4 kb16[2], vb16[2];
+    float kb32[8], vb32[8];
+    if constexpr (k16) {
+#pragma unroll
+      for (int dc = 0; dc < 2; ++dc) {
+        kb16[dc] = *reinterpret_cast<const s4*>(Ks + koff * RS + dc * 16 + 4 * g);
+        vb16[dc] = *reinterpret_cast<const s4*>(Vs + koff * RS + dc * 16 + 4 * g);
+      }
+    } else {
+#pragma unroll
+      for (int dc = 0; dc < 8; ++dc) {
+        kb32[dc] = Elt<T>::to_f(Ks[koff * RS + dc * 4 + g]);
+        vb32[dc] = Elt<T>::to_f(Vs[koff * RS + dc * 4 + g]);
+      }
+    }
+    f4 dkacc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+    f4 dvacc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+    const int word_sel = koff >> 5, bit = koff & 31;
+    const bool key_ok = koff < kvalid;
+
+    for (int qt = 0; qt < NT; ++qt) {
+      f4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (k16) {
+#pragma unroll
+        for (int dc = 0; dc < 2; ++dc) {
+          const s4 qa = *reinterpret_cast<const s4*>(Qs + (qt * 16 + r) * RS + dc * 16 + 4 * g);
+          const s4 ga = *reinterpret_cast<const s4*>(dOs + (qt * 16 + r) * RS + dc * 16 + 4 * g);
+          s = mma16<T>(qa, kb16[dc], s);
+          dp = mma16<T>(ga, vb16[dc], dp);
+        }
+      } else {
+#pragma unroll
+        for (int dc = 0; dc < 8; ++dc) {
+          s = mma32(Elt<T>::to_f(Qs[(qt * 16 + r) * RS + dc * 4 + g]), kb32[dc], s);
+          dp = mma32(Elt<T>::to_f(dOs[(qt * 16 + r) * RS + dc * 4 + g]), vb32[dc], dp);
+        }
+      }
+      // C layout: [q = qt*16 + 4g + i][key = koff]
+      f4 p, ds;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qi = qt * 16 + 4 * g + i;
+        const bool blocked = !key_ok || ((mw[2 * qi + word_sel] >> bit) & 1u);
+        const float pv = blocked ? 0.f : exp2f(s[i] * sl2 - lse_s[qi]);
+        p[i] = pv;
+        ds[i] = pv * (dp[i] - del_s[qi]);
+      }
+      // dV^T += dO^T P ; dK^T += Q^T dS      (A[row d][k = q])
+      if constexpr (k16) {
+        const s4 pb = pack4<T>(p[0], p[1], p[2], p[3]);
+        const s4 sb = pack4<T>(ds[0], ds[1], ds[2], ds[3]);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const int ro = (qt * 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
+          dvacc[dt] = mma16<T>(tr_read(dOs + ro), pb, dvacc[dt]);
+          dkacc[dt] = mma16<T>(tr_read(Qs + ro), sb, dkacc[dt]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt) {
+            const int ro = (qt * 16 + 4 * g + i) * RS + dt * 16 + r;
+            dvacc[dt] = mma32(Elt<T>::to_f(dOs[ro]), p[i], dvacc[dt]);
+            dkacc[dt] = mma32(Elt<T>::to_f(Qs[ro]), ds[i], dkacc[dt]);
+          }
+        }
+      }
+      // dQ^T[d][q] += K^T[d][key] dS^T[key][q]: transpose dS through the wave's scratch
+#pragma unroll
+      for (int i = 0; i < 4; ++i) myscr[(4 * g + i) * 17 + r] = ds[i];  // scr[q][key]
+      __builtin_amdgcn_wave_barrier();
+      float dst4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst4[j] = myscr[r * 17 + 4 * g + j];  // dS^T[key = 4g+j][q = r]
+      __builtin_amdgcn_wave_barrier();
+      f4 dqt[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+      if constexpr (k16) {
+        const s4 sb = pack4<T>(dst4[0], dst4[1], dst4[2], dst4[3]);
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const s4 ka = tr_read(Ks + (16 * w + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3));
+          dqt[dt] = mma16<T>(ka, sb, dqt[dt]);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+            dqt[dt] = mma32(Elt<T>::to_f(Ks[(16 * w + 4 * g + i) * RS + dt * 16 + r]), dst4[i], dqt[dt]);
+        }
+      }
+      // lane holds dQ^T[d = dt*16 + 4g + i][q = qt*16 + r]
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) atomicAdd(&dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i], dqt[dt][i]);
+    }
+    // write dK, dV for this key tile: lane holds [d = dt*16 + 4g + i][key = koff]
+    if (key_ok) {
+      const int64_t krow = (kvrow0 + kb0 + koff) * HD + h * kD;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const f4 kk = dkacc[dt] * scale;
+        const f4 vv = dvacc[dt];
+        if constexpr (k16) {
+          *reinterpret_cast<s4*>(dk + krow + dt * 16 + 4 * g) = pack4<T>(kk[0], kk[1], kk[2], kk[3]);
+          *reinterpret_cast<s4*>(dv + krow + dt * 16 + 4 * g) = pack4<T>(vv[0], vv[1], vv[2], vv[3]);
+        } else {
+          *reinterpret_cast<f4*>(dk + krow + dt * 16 + 4 * g) = kk;
+          *reinterpret_cast<f4*>(dv + krow + dt * 16 + 4 * g) = vv;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // dQ partial for this chunk
+  const int BH = gridDim.x;
+  for (int idx = threadIdx.x; idx < Lq * kD; idx += 256) {
+    const int qi = idx / kD, d = idx % kD;
+    const float val = dqa[idx] * scale;
+    if (nchunks == 1)
+      dq[(static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + d] = Elt<T>::from_f(val);
+    else
+      ws_dq[((static_cast<int64_t>(c) * BH + bh) * Lq + qi) * kD + d] = val;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) mattn_dq_reduce_kernel(const float* __restrict__ ws_dq, int nchunks, int BH,
+                                                              int H, int Lq, T* __restrict__ dq) {
+  const int64_t idx = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  const int64_t total = static_cast<int64_t>(BH) * Lq * kD;
+  if (idx >= total) return;
+  float acc = 0.f;
+  for (int c = 0; c < nchunks; ++c) acc += ws_dq[static_cast<int64_t>(c) * total + idx];
+  const int d = static_cast<int>(idx % kD);
+  const int64_t row = idx / kD;
+  const int bh = static_cast<int>(row / Lq), qi = static_cast<int>(row % Lq);
+  const int b = bh / H, h = bh % H;
+  dq[(static_cast<int64_t>(b) * Lq + qi) * (H * kD) + h * kD + d] = Elt<T>::from_f(acc);
+}
+
+// ----------------------------------------------------------------------------------------------
+// host
+// ----------------------------------------------------------------------------------------------
+int plan_chunks(int B, int H, int Lk, int* chunk_len, int* nchunks) {
+  const int BH = B * H;
+  const int nblocks = (Lk + 63) / 64;
+  // aim for >= ~1024 workgroups, but no chunk shorter than 2 key blocks
+  int per = (nblocks * BH + 1023) / 1024;
+  per = per < 2 ? 2 : per;
+  if (per > nblocks) per = nblocks;
+  *chunk_len = per * 64;
+  *nchunks = (Lk + *chunk_len - 1) / *chunk_len;
+  return 0;
+}
+
+size_t bwd_lds_bytes(int Lqp, bool k16, int elt) {
+  const int RS = k16 ? kDP : kD + 1;
+  size_t bytes = static_cast<size_t>(2 * Lqp + 128) * RS * elt;
+  bytes = (bytes + 15) & ~size_t(15);
+  bytes += sizeof(float) * (2 * Lqp) + sizeof(uint32_t) * 2 * Lqp + sizeof(float) * 4 * 16 * 17 +
+           sizeof(float) * Lqp * kD;
+  return bytes;
+}
+
+template <typename T>
+int attn_mask_impl(const char* fn, const void* logits, int B, int Q, int F, int Hin, int Win, int Hout, int Wout,
+                   int row_fix, uint32_t* bits, int nwords, hipStream_t st) {
+  if (!logits || !bits) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (B <= 0 || Q <= 0 || F <= 0 || Hin <= 0 || Win <= 0 || Hout <= 0 || Wout <= 0)
+    return m2f::fail(M2F_EINVAL, "%s: non-positive size", fn);
+  const int need = (F * Hout * Wout + 31) / 32;
+  if (nwords < need) return m2f::fail(M2F_EINVAL, "%s: nwords %d < %d", fn, nwords, need);
+  const size_t lds = static_cast<size_t>(nwords) * 4;
+  if (lds > 60 * 1024) return m2f::fail(M2F_EUNSUPPORTED, "%s: target %dx%d too large", fn, Hout, Wout);
+  attn_mask_bits_kernel<T><<<static_cast<unsigned>(B) * Q, 256, lds, st>>>(
+      static_cast<const T*>(logits), F, Hin, Win, Hout, Wout, nwords, row_fix, bits);
+  return m2f::check_launch(fn);
+}
+
+template <typename T>
+int mattn_fwd_impl(const char* fn, const void* q, const void* k, const void* v, const uint32_t* bits, int B, int Lq,
+                   int Lk, int H, int D, int qs, int kvs, int nw, float scale, void* out, float* lse2, float* ws,
+                   size_t ws_bytes, hipStream_t st) {
+  if (!q || !k || !v || !bits || !out || !lse2) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (D != kD) return m2f::fail(M2F_EUNSUPPORTED, "%s: head dim %d (only %d)", fn, D, kD);
+  if (B <= 0 || Lq <= 0 || Lk <= 0 || H <= 0) return m2f::fail(M2F_EINVAL, "%s: non-positive size", fn);
+  if (Lq > 512) return m2f::fail(M2F_EUNSUPPORTED, "%s: %d queries (max 512)", fn, Lq);
+  if (nw < (Lk + 31) / 32) return m2f::fail(M2F_EINVAL, "%s: mask words %d < %d", fn, nw, (Lk + 31) / 32);
+  const int vec = Elt<T>::k16 ? 8 : 4;
+  if (qs % 4 || kvs % vec || !m2f::aligned(q, 8) || !m2f::aligned(k, 16) || !m2f::aligned(v, 16) ||
+      !m2f::aligned(out, 16))
+    return m2f::fail(M2F_EINVAL, "%s: misaligned operand or stride", fn);
+  int chunk, nch;
+  plan_chunks(B, H, Lk, &chunk, &nch);
+  const size_t need = nch > 1 ? sizeof(float) * static_cast<size_t>(nch) * B * H * Lq * (kD + 2) : 0;
+  if (ws_bytes < need || (need && !ws)) return m2f::fail(M2F_EINVAL, "%s: workspace %zu < %zu", fn, ws_bytes, need);
+  float* ws_o = ws;
+  float* ws_ml = ws ? ws + static_cast<size_t>(nch) * B * H * Lq * kD : nullptr;
+  const float sl2 = scale * kLog2e;
+  const dim3 grid(B * H, nch);
+  const int tiles = (Lq + 15) / 16, tpw = (tiles + 3) / 4;
+  const T* qq = static_cast<const T*>(q);
+  const T* kk = static_cast<const T*>(k);
+  const T* vv = static_cast<const T*>(v);
+  T* oo = static_cast<T*>(out);
+  if (tpw <= 1)
+    mattn_fwd_kernel<T, 1><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml);
+  else if (tpw <= 2)
+    mattn_fwd_kernel<T, 2><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml);
+  else if (tpw <= 4)
+    mattn_fwd_kernel<T, 4><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml);
+  else
+    mattn_fwd_kernel<T, 8><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml);
+  int rc = m2f::check_launch(fn);
+  if (rc || nch == 1) return rc;
+  const int64_t total = static_cast<int64_t>(B) * H * Lq * (kD / 4);
+  mattn_combine_kernel<T><<<m2f::ceil_div(total, 256), 256, 0, st>>>(ws_o, ws_ml, nch, B * H, H, Lq, oo, lse2);
+  return m2f::check_launch(fn);
+}
+
+template <typename T>
+int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, const uint32_t* bits,
+                   const void* out, const void* dout, const float* lse2, int B, int Lq, int Lk, int H, int D, int qs,
+                   int kvs, int nw, float scale, void* dq, void* dk, void* dv, float* ws, size_t ws_bytes,
+                   hipStream_t st) {
+  if (!q || !k || !v || !bits || !out || !dout || !lse2 || !dq || !dk || !dv)
+    return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (D != kD) return m2f::fail(M2F_EUNSUPPORTED, "%s: head dim %d (only %d)", fn, D, kD);
+  if (B <= 0 || Lq <= 0 || Lk <= 0 || H <= 0) return m2f::fail(M2F_EINVAL, "%s: non-positive size", fn);
+  if (Lq > 512) return m2f::fail(M2F_EUNSUPPORTED, "%s: %d queries (max 512)", fn, Lq);
+  if (nw < (Lk + 31) / 32) return m2f::fail(M2F_EINVAL, "%s: mask words %d < %d", fn, nw, (Lk + 31) / 32);
+  const int vec = Elt<T>::k16 ? 8 : 4;
+  if (qs % 4 || kvs % vec || !m2f::aligned(k, 16) || !m2f::aligned(v, 16) || !m2f::aligned(dk, 16) ||
+      !m2f::aligned(dv, 16))
+    return m2f::fail(M2F_EINVAL, "%s: misaligned operand or stride", fn);
+  int chunk, nch;
+  plan_chunks(B, H, Lk, &chunk, &nch);
+  const size_t need = nch > 1 ? sizeof(float) * static_cast<size_t>(nch) * B * H * Lq * kD : 0;
+  if (ws_bytes < need || (need && !ws)) return m2f::fail(M2F_EINVAL, "%s: workspace %zu < %zu", fn, ws_bytes, need);
+  const int Lqp = (Lq + 15) / 16 * 16;
+  const size_t lds = bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T));
+  if (lds > 160 * 1024) return m2f::fail(M2F_EUNSUPPORTED, "%s: %zu B of LDS", fn, lds);
+  static bool attr_set[3] = {false, false, false};
+  const int ai = std::is_same<T, float>::value ? 0 : (std::is_same<T, __bf16>::value ? 1 : 2);
+  if (!attr_set[ai]) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mattn_bwd_kernel<T>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set[ai] = true;
+  }
+  const dim3 grid(B * H, nch);
+  mattn_bwd_kernel<T><<<grid, 256, lds, st>>>(
+      static_cast<const T*>(q), static_cast<const T*>(k), static_cast<const T*>(v), bits, static_cast<const T*>(out),
+      static_cast<const T*>(dout), lse2, Lq, Lk, H, qs, kvs, nw, scale * kLog2e, scale, chunk, Lqp,
+      static_cast<T*>(dq), static_cast<T*>(dk), static_cast<T*>(dv), ws);
+  int rc = m2f::check_launch(fn);
+  if (rc || nch == 1) return rc;
+  const int64_t total = static_cast<int64_t>(B) * H * Lq * kD;
+  mattn_dq_reduce_kernel<T><<<m2f::ceil_div(total, 256), 256, 0, st>>>(ws, nch, B * H, H, Lq, static_cast<T*>(dq));
+  return m2f::check_launch(fn);
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
+extern "C" int m2f_attn_mask_bits(const void* logits, int dtype, int batch, int num_queries, int frames, int in_h,
+                                  int in_w, int out_h, int out_w, int row_fix, uint32_t* bits, int nwords,
+                                  void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const char* fn = "m2f_attn_mask_bits";
+  switch (dtype) {
+    case M2F_F32: return attn_mask_impl<float>(fn, logits, batch, num_queries, frames, in_h, in_w, out_h, out_w, row_fix, bits, nwords, st);
+    case M2F_BF16: return attn_mask_impl<__bf16>(fn, logits, batch, num_queries, frames, in_h, in_w, out_h, out_w, row_fix, bits, nwords, st);
+    case M2F_F16: return attn_mask_impl<_Float16>(fn, logits, batch, num_queries, frames, in_h, in_w, out_h, out_w, row_fix, bits, nwords, st);
+    default: return m2f::fail(M2F_EUNSUPPORTED, "m2f_attn_mask_bits: dtype %d", dtype);
+  }
+}
+
+extern "C" int m2f_masked_attn_plan(int batch, int num_queries, int num_keys, int num_heads, int* chunk_len,
+                                    int* num_chunks, int64_t* fwd_workspace_bytes, int64_t* bwd_workspace_bytes) {
+  int cl, nc;
+  plan_chunks(batch, num_heads, num_keys, &cl, &nc);
+  if (chunk_len) *chunk_len = cl;
+  if (num_chunks) *num_chunks = nc;
+  const int64_t rows = static_cast<int64_t>(nc) * batch * num_heads * num_queries;
+  if (fwd_workspace_bytes) *fwd_workspace_bytes = nc > 1 ? rows * (kD + 2) * 4 : 0;
+  if (bwd_workspace_bytes) *bwd_workspace_bytes = nc > 1 ? rows * kD * 4 : 0;
+  return m2f::ok();
+}
+
+extern "C" int m2f_masked_attn_fwd(int dtype, const void* q, const void* k, const void* v, const uint32_t* bits,
+                                   int batch, int num_queries, int num_keys, int num_heads, int head_dim,
+                                   int q_row_stride, int kv_row_stride, int mask_words, float scale, void* out,
+                                   float* lse, void* workspace, int64_t workspace_bytes, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* ws = static_cast<float*>(workspace);
+  const size_t wb = workspace_bytes > 0 ? static_cast<size_t>(workspace_bytes) : 0;
+  const char* fn = "m2f_masked_attn_fwd";
+  switch (dtype) {
+    case M2F_F32: return mattn_fwd_impl<float>(fn, q, k, v, bits, batch, num_queries, num_keys, num_heads, head_dim, q_row_stride, kv_row_stride, mask_words, scale, out, lse, ws, wb, st);
+    case M2F_BF16: return mattn_fwd_impl<__bf16>(fn, q, k, v, bits, batch, num_queries, num_keys, num_heads, head_dim, q_row_stride, kv_row_stride, mask_words, scale, out, lse, ws, wb, st);
+    case M2F_F16: return mattn_fwd_impl<_Float16>(fn, q, k, v, bits, batch, num_queries, num_keys, num_heads, head_dim, q_row_stride, kv_row_stride, mask_words, scale, out, lse, ws, wb, st);
+    default: return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  }
+}
+
+extern "C" int m2f_masked_attn_bwd(int dtype, const void* q, const void* k, const void* v, const uint32_t* bits,
+                                   const void* out, const void* grad_out, const float* lse, int batch,
+                                   int num_queries, int num_keys, int num_heads, int head_dim, int q_row_stride,
+                                   int kv_row_stride, int mask_words, float scale, void* grad_q, void* grad_k,
+                                   void* grad_v, void* workspace, int64_t workspace_bytes, void* stream) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* ws = static_cast<float*>(workspace);
+  const size_t wb = workspace_bytes > 0 ? static_cast<size_t>(workspace_bytes) : 0;
+  const char* fn = "m2f_masked_attn_bwd";
+  switch (dtype) {
+    case M2F_F32: return mattn_bwd_impl<float>(fn, q, k, v, bits, out, grad_out, lse, batch, num_queries, num_keys, num_heads, head_dim, q_row_stride, kv_row_stride, mask_words, scale, grad_q, grad_k, grad_v, ws, wb, st);
+    case M2F_BF16: return mattn_bwd_impl<__bf16>(fn, q, k, v, bits, out, grad_out, lse, batch, num_queries, num_keys, num_heads, head_dim, q_row_stride, kv_row_stride, mask_words, scale, grad_q, grad_k, grad_v, ws, wb, st);
+    case M2F_F16: return mattn_bwd_impl<_Float16>(fn, q, k, v, bits, out, grad_out, lse, batch, num_queries, num_keys, num_heads, head_dim, q_row_stride, kv_row_stride, mask_words, scale, grad_q, grad_k, grad_v, ws, wb, st);
+    default: return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  }
+}

@@ -185,7 +185,9 @@ __device__ __forceinline__ Corners make_corners(float locx, float locy, int H, i
   k.c2 = h0 >= 0 && w0 + 1 <= W - 1;
   k.c3 = h0 + 1 <= H - 1 && w0 >= 0;
   k.c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
-  const int y0 = max(h0, 0), y1 = min(h0 + 1, H - 1), x0 = max(w0, 0), x1 = min(w0 + 1, W - 1);
+  // clamp every corner into the level so the (masked) loads never leave it, valid point or not
+  const int y0 = min(max(h0, 0), H - 1), y1 = min(max(h0 + 1, 0), H - 1);
+  const int x0 = min(max(w0, 0), W - 1), x1 = min(max(w0 + 1, 0), W - 1);
   k.o1 = lbase + (static_cast<int64_t>(y0) * W + x0) * rs;
   k.o2 = lbase + (static_cast<int64_t>(y0) * W + x1) * rs;
   k.o3 = lbase + (static_cast<int64_t>(y1) * W + x0) * rs;

@@ -1,0 +1,170 @@
+"""Decoder ops on the gfx950 kernels: attention-mask bitmask, masked cross-attention, mask einsum.
+
+* :func:`attn_mask_bits` — reference forward_prediction_heads resize + ``sigmoid() < 0.5``
+  (mask2former_transformer_decoder.py:446-449) and the fully-masked-row fix (:400) in one kernel,
+  emitting one bit per (b, q, pixel) for all heads.
+* :class:`MaskedAttention` — the attention core of ``nn.MultiheadAttention(attn_mask=bool)`` as used by
+  CrossAttentionLayer (:98-110), flash style, fwd + bwd.
+* :class:`MaskEinsum` — ``einsum("bqc,bchw->bqhw")`` (:442) with the low-precision copy of the mask
+  features cast once per decoder forward (the reference re-casts the 1 GB fp32 map on every one of its 10
+  calls under AMP); its gradient is returned in the features' dtype, as the reference's cast would.
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import torch
+from torch.autograd import Function
+
+from . import _native
+
+_DTYPE_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}
+
+
+def _code(dtype):
+    try:
+        return _DTYPE_CODE[dtype]
+    except KeyError:
+        raise RuntimeError(f"bm2f_amd decoder ops: unsupported dtype {dtype}") from None
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _require_device(*ts):
+    for t in ts:
+        if t.device.type != "cuda":
+            raise RuntimeError("bm2f_amd decoder ops need HIP device tensors")
+
+
+def num_words(hw: int) -> int:
+    return (hw + 31) // 32
+
+
+def attn_mask_bits(logits: torch.Tensor, size, row_fix: bool = True) -> torch.Tensor:
+    """logits (B, Q, H, W) or (B, Q, T, H, W) -> int32 bits (B, Q, ceil(T*h*w/32)); set bit = blocked."""
+    _require_device(logits)
+    logits = logits.detach().contiguous()
+    if logits.dim() == 4:
+        B, Q, Hin, Win = logits.shape
+        T = 1
+    else:
+        B, Q, T, Hin, Win = logits.shape
+    Hout, Wout = int(size[0]), int(size[1])
+    nw = num_words(T * Hout * Wout)
+    bits = torch.empty((B, Q, nw), dtype=torch.int32, device=logits.device)
+    _native.call("m2f_attn_mask_bits", logits.data_ptr(), _code(logits.dtype), B, Q, T, Hin, Win, Hout, Wout,
+                 1 if row_fix else 0, bits.data_ptr(), nw, _stream(logits))
+    return bits
+
+
+def bits_to_bool(bits: torch.Tensor, hw: int, num_heads: int = 1) -> torch.Tensor:
+    """Expand bits to the reference's bool layout (B*num_heads, Q, hw); for tests and interop only."""
+    B, Q, nw = bits.shape
+    shifts = torch.arange(32, device=bits.device, dtype=torch.int32)
+    b = ((bits.unsqueeze(-1) >> shifts) & 1).bool().flatten(2)[..., :hw]
+    return b.unsqueeze(1).expand(B, num_heads, Q, hw).flatten(0, 1)
+
+
+def _plan(B, Lq, Lk, H):
+    cl, nc = ctypes.c_int(), ctypes.c_int()
+    fw, bw = ctypes.c_int64(), ctypes.c_int64()
+    _native.call("m2f_masked_attn_plan", B, Lq, Lk, H, ctypes.byref(cl), ctypes.byref(nc), ctypes.byref(fw),
+                 ctypes.byref(bw))
+    return cl.value, nc.value, fw.value, bw.value
+
+
+def _rows(t: torch.Tensor):
+    """(B, L, H*32) view with unit inner stride -> (tensor, row_stride)."""
+    if t.stride(-1) != 1 or t.stride(0) != t.shape[1] * t.stride(1):
+        t = t.contiguous()
+    return t, t.stride(1)
+
+
+class MaskedAttention(Function):
+    """softmax(q k^T * scale, blocked by bits) v; q (B, Lq, H*32), k/v (B, Lk, H*32) -> (B, Lq, H*32)."""
+
+    @staticmethod
+    def forward(ctx, q, k, v, bits, num_heads, scale):
+        _require_device(q, k, v, bits)
+        if not (q.dtype == k.dtype == v.dtype):
+            raise RuntimeError("masked attention: q, k, v must share a dtype")
+        q, qs = _rows(q)
+        k, ks = _rows(k)
+        v, vs = _rows(v)
+        if ks != vs:
+            k, v = k.contiguous(), v.contiguous()
+            ks = k.stride(1)
+        B, Lq, C = q.shape
+        Lk = k.shape[1]
+        if C != num_heads * 32:
+            raise RuntimeError(f"masked attention: channels {C} != {num_heads} heads x 32")
+        bits = bits.contiguous()
+        _, _, fwb, _ = _plan(B, Lq, Lk, num_heads)
+        out = torch.empty((B, Lq, C), dtype=q.dtype, device=q.device)
+        lse = torch.empty((B, num_heads, Lq), dtype=torch.float32, device=q.device)
+        ws = torch.empty((max(fwb, 4) // 4,), dtype=torch.float32, device=q.device)
+        _native.call("m2f_masked_attn_fwd", _code(q.dtype), q.data_ptr(), k.data_ptr(), v.data_ptr(), bits.data_ptr(),
+                     B, Lq, Lk, num_heads, 32, qs, ks, bits.shape[-1], ctypes.c_float(scale), out.data_ptr(),
+                     lse.data_ptr(), ws.data_ptr(), ctypes.c_int64(fwb), _stream(q))
+        ctx.save_for_backward(q, k, v, bits, out, lse)
+        ctx.meta = (num_heads, scale, qs, ks)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        q, k, v, bits, out, lse = ctx.saved_tensors
+        num_heads, scale, qs, ks = ctx.meta
+        B, Lq, C = q.shape
+        Lk = k.shape[1]
+        grad_out = grad_out.to(q.dtype).contiguous()
+        _, _, _, bwb = _plan(B, Lq, Lk, num_heads)
+        dq = torch.empty((B, Lq, C), dtype=q.dtype, device=q.device)
+        dk = torch.empty((B, Lk, C), dtype=q.dtype, device=q.device)
+        dv = torch.empty((B, Lk, C), dtype=q.dtype, device=q.device)
+        ws = torch.empty((max(bwb, 4) // 4,), dtype=torch.float32, device=q.device)
+        _native.call("m2f_masked_attn_bwd", _code(q.dtype), q.data_ptr(), k.data_ptr(), v.data_ptr(), bits.data_ptr(),
+                     out.data_ptr(), grad_out.data_ptr(), lse.data_ptr(), B, Lq, Lk, num_heads, 32, qs, ks,
+                     bits.shape[-1], ctypes.c_float(scale), dq.data_ptr(), dk.data_ptr(), dv.data_ptr(),
+                     ws.data_ptr(), ctypes.c_int64(bwb), _stream(q))
+        return dq, dk, dv, None, None, None
+
+
+def masked_attention(q, k, v, bits, num_heads, scale=None):
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1] // num_heads)
+    return MaskedAttention.apply(q, k, v, bits, num_heads, float(scale))
+
+
+class MaskEinsum(Function):
+    """out[b,q,h,w] = sum_c e[b,q,c] f[b,c,h,w] on a precast copy ``f_lp`` of ``f``."""
+
+    @staticmethod
+    def forward(ctx, embed, feats, feats_lp):
+        dt = feats_lp.dtype
+        B, C, H, W = feats_lp.shape
+        e = embed.to(dt)
+        out = torch.bmm(e, feats_lp.view(B, C, H * W)).view(B, e.shape[1], H, W)
+        ctx.save_for_backward(e, feats_lp)
+        ctx.dtypes = (embed.dtype, feats.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        e, f = ctx.saved_tensors
+        B, C, H, W = f.shape
+        g = grad.to(f.dtype).reshape(B, -1, H * W)
+        de = de_f = None
+        if ctx.needs_input_grad[0]:
+            de = torch.bmm(g, f.view(B, C, H * W).transpose(1, 2)).to(ctx.dtypes[0])
+        if ctx.needs_input_grad[1]:
+            de_f = torch.bmm(e.transpose(1, 2), g).view(B, C, H, W).to(ctx.dtypes[1])
+        return de, de_f, None
+
+
+def mask_einsum(embed, feats, feats_lp=None):
+    if feats_lp is None:
+        feats_lp = feats
+    return MaskEinsum.apply(embed, feats, feats_lp)

@@ -41,6 +41,9 @@ enum {
   M2F_EUNSUPPORTED = 3 /* configuration this build does not implement */
 };
 
+/* Element types of the decoder entry points (`dtype` arguments). */
+enum { M2F_F32 = 0, M2F_F16 = 1, M2F_BF16 = 2 };
+
 /* Message for the last nonzero return on this thread ("" if none). */
 const char* m2f_last_error(void);
 /* ABI version, bumped whenever a signature below changes. */
@@ -85,6 +88,43 @@ int m2f_msda_bwd_f64(const double* value, const int64_t* spatial_shapes, const i
                      int num_levels, int num_query, int num_point, int im2col_step,
                      const int64_t* host_spatial_shapes,
                      double* grad_value, double* grad_sampling_loc, double* grad_attn_weight, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Masked-attention decoder (mask2former_transformer_decoder.py).
+ *
+ * m2f_attn_mask_bits: logits (B, Q, frames, in_h, in_w) of `dtype` -> bits (B, Q, nwords) uint32, bit k
+ * of word w = 1 when key 32*w + k (frame-major, then row-major in out_h x out_w) is BLOCKED, i.e.
+ *   dtype( sigmoid( dtype( bilinear_resize(logits, (out_h, out_w), align_corners=False) ) ) ) < 0.5
+ * exactly as F.interpolate(...).sigmoid() < 0.5 in that dtype (reference :446-449).  With row_fix != 0
+ * a row whose every pixel is blocked is cleared, the fix the reference applies before each
+ * cross-attention (:400).  One bit per (b, q, pixel) serves all heads (the reference repeats the
+ * bool mask per head).  nwords >= ceil(frames*out_h*out_w / 32); unused tail bits are 0.  frames > 1 is
+ * the video decoder's per-frame resize of (B, Q, T, H, W) logits (video_..._decoder.py:453-458).
+ * ------------------------------------------------------------------------------------------- */
+int m2f_attn_mask_bits(const void* logits, int dtype, int batch, int num_queries, int frames, int in_h,
+                       int in_w, int out_h, int out_w, int row_fix, uint32_t* bits, int nwords, void* stream);
+
+/* Work split of the masked attention for these sizes: keys are processed in `num_chunks` ranges of
+ * `chunk_len`; the forward / backward need the returned fp32 workspace sizes (0 when one chunk). */
+int m2f_masked_attn_plan(int batch, int num_queries, int num_keys, int num_heads, int* chunk_len,
+                         int* num_chunks, int64_t* fwd_workspace_bytes, int64_t* bwd_workspace_bytes);
+
+/* out = softmax(scale * q k^T, masked by bits) v, per (batch, head); head_dim must be 32.
+ *   q   (B, Lq, H*32) with row stride q_row_stride elements;  k, v (B, Lk, H*32), row stride kv_row_stride
+ *   out (B, Lq, H*32) contiguous;  lse (B, H, Lq) fp32 log-sum-exp (base-2, internal) for the backward.
+ * A query row with every key blocked yields zeros (the reference never passes one: row_fix). */
+int m2f_masked_attn_fwd(int dtype, const void* q, const void* k, const void* v, const uint32_t* bits,
+                        int batch, int num_queries, int num_keys, int num_heads, int head_dim,
+                        int q_row_stride, int kv_row_stride, int mask_words, float scale, void* out,
+                        float* lse, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* Gradients of m2f_masked_attn_fwd: grad_q (B, Lq, H*32), grad_k / grad_v (B, Lk, H*32), all
+ * contiguous and fully written.  grad_q is summed over key chunks in a fixed order. */
+int m2f_masked_attn_bwd(int dtype, const void* q, const void* k, const void* v, const uint32_t* bits,
+                        const void* out, const void* grad_out, const float* lse, int batch,
+                        int num_queries, int num_keys, int num_heads, int head_dim, int q_row_stride,
+                        int kv_row_stride, int mask_words, float scale, void* grad_q, void* grad_k,
+                        void* grad_v, void* workspace, int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,63 @@
+"""Module structure and numerics on CPU: the bm2f_amd modules with the oracle's MSDA core patched in,
+against the golden outputs of the reference modules (tests/golden/*.npz)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from module_cases import build_decoder, build_pixdec, build_video_decoder, oracle_msda, rel_err, run_pixdec
+
+
+def test_pixdec_state_dict_keys_match_reference():
+    m = build_pixdec()
+    assert sorted(m.state_dict().keys()) == list(golden("pixdec.npz")["state_dict_keys"])
+    assert sum(p.numel() for p in m.parameters()) == 6035904  # SURVEY §8(b), measured on the reference
+
+
+def test_decoder_state_dict_keys_match_reference():
+    d = build_decoder()
+    assert sorted(d.state_dict().keys()) == list(golden("decoder.npz")["state_dict_keys"])
+    assert sum(p.numel() for p in d.parameters()) == 14493062
+
+
+def test_video_decoder_state_dict_keys_match_reference():
+    d = build_video_decoder()
+    assert sorted(d.state_dict().keys()) == list(golden("video_decoder.npz")["state_dict_keys"])
+
+
+def test_pixdec_forward_backward_cpu():
+    m = build_pixdec()
+    with oracle_msda():
+        g, feats, outs = run_pixdec(m, torch.device("cpu"))
+    names = ["out_mask_features", "out_out0", "out_ms0", "out_ms1", "out_ms2"]
+    for name, o in zip(names, outs):
+        assert rel_err(o.detach(), g[name]) < 1e-4, name
+    for k, v in feats.items():
+        assert rel_err(v.grad, g[f"ingrad_{k}"]) < 1e-4, k
+    params = dict(m.named_parameters())
+    for key in g.files:
+        if key.startswith("pgrad_"):
+            assert rel_err(params[key[6:]].grad, g[key]) < 1e-4, key
+
+
+@pytest.mark.parametrize("fixture,video", [("decoder.npz", False), ("video_decoder.npz", True)])
+def test_decoder_forward_backward_cpu(fixture, video):
+    from module_cases import run_decoder
+    from torch_ref_ops import torch_decoder_ops, unpack_bits
+    d = build_video_decoder() if video else build_decoder()
+    with torch_decoder_ops():
+        g, x, mf, logits, masks, captured = run_decoder(d, torch.device("cpu"), fixture, video)
+    assert rel_err(torch.stack([t.detach() for t in logits]), g["pred_logits"]) < 1e-4
+    assert rel_err(torch.stack([t.detach() for t in masks]), g["pred_masks"]) < 1e-4
+    for i, bits in enumerate(captured):
+        want = g[f"attn_mask{i}"]
+        got = unpack_bits(bits, want.shape[-1]).numpy()
+        assert (got == want).all(), f"attn mask of layer {i} differs"
+    for i, t in enumerate(x):
+        assert rel_err(t.grad, g[f"ingrad_x{i}"]) < 1e-4
+    assert rel_err(mf.grad, g["ingrad_mask_features"]) < 1e-4
+    if not video:
+        params = dict(d.named_parameters())
+        for key in g.files:
+            if key.startswith("pgrad_"):
+                assert rel_err(params[key[6:]].grad, g[key]) < 1e-4, key

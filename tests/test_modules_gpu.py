@@ -1,0 +1,53 @@
+"""Pixel decoder / decoder / video decoder on the GPU kernels vs the reference's golden outputs."""
+import numpy as np
+import pytest
+import torch
+
+from module_cases import build_decoder, build_pixdec, build_video_decoder, rel_err, run_decoder, run_pixdec
+from torch_ref_ops import unpack_bits
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pixdec_gpu(device):
+    m = build_pixdec().to(device)
+    g, feats, outs = run_pixdec(m, device)
+    names = ["out_mask_features", "out_out0", "out_ms0", "out_ms1", "out_ms2"]
+    for name, o in zip(names, outs):
+        assert rel_err(o.detach().cpu(), g[name]) < 1e-3, name
+    for k, v in feats.items():
+        assert rel_err(v.grad.cpu(), g[f"ingrad_{k}"]) < 1e-3, k
+    params = dict(m.named_parameters())
+    for key in g.files:
+        if key.startswith("pgrad_"):
+            assert rel_err(params[key[6:]].grad.cpu(), g[key]) < 1e-3, key
+
+
+@pytest.mark.parametrize("fixture,video", [("decoder.npz", False), ("video_decoder.npz", True)])
+def test_decoder_gpu_fp32(device, fixture, video):
+    d = (build_video_decoder() if video else build_decoder()).to(device)
+    g, x, mf, logits, masks, captured = run_decoder(d, device, fixture, video)
+    assert rel_err(torch.stack([t.detach().cpu() for t in logits]), g["pred_logits"]) < 1e-3
+    assert rel_err(torch.stack([t.detach().cpu() for t in masks]), g["pred_masks"]) < 1e-3
+    for i, bits in enumerate(captured):
+        want = g[f"attn_mask{i}"]
+        got = unpack_bits(bits.cpu(), want.shape[-1]).numpy()
+        # bit-exact unless a logit sits within fp32 rounding of the sigmoid threshold
+        assert (got != want).mean() < 1e-3, f"layer {i}: {(got != want).sum()} bits differ"
+    for i, t in enumerate(x):
+        assert rel_err(t.grad.cpu(), g[f"ingrad_x{i}"]) < 1e-3
+    assert rel_err(mf.grad.cpu(), g["ingrad_mask_features"]) < 1e-3
+
+
+def test_decoder_teacher_forced_masks_exact(device):
+    """Feed the reference's own mask logits to the kernel: the masks must match bit for bit."""
+    from bm2f_amd import decoder_ops
+    from conftest import golden
+    g = golden("decoder.npz")
+    sizes = [(2, 2), (4, 4), (8, 8)]
+    pm = torch.from_numpy(g["pred_masks"]).to(device)  # (10, B, Q, 16, 16) fp32
+    for i in range(9):
+        bits = decoder_ops.attn_mask_bits(pm[i], sizes[i % 3])
+        want = g[f"attn_mask{i}"]
+        got = unpack_bits(bits.cpu(), want.shape[-1]).numpy()
+        assert (got == want).all(), f"head {i}: {(got != want).sum()} bits differ"
