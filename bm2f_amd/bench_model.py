@@ -1,0 +1,140 @@
+"""The training step the benchmark times: R50 backbone -> MSDeformAttn pixel decoder -> masked decoder.
+
+Mirrors the reference's training forward (maskformer_model.py:258-320, mask_former_head.py:115-132)
+with the criterion replaced by the sum of means of every head's outputs (the
+Hungarian matcher / weak-supervision losses are outside the hot path).  The backbone is
+detectron2's R50 as configured by the reference (Base-COCO-*.yaml: depth 50, STRIDE_IN_1X1 False,
+FrozenBN, FREEZE_AT 0, res2..res5), written here in plain PyTorch (MIOpen convs, channels-last) since
+detectron2 / torchvision are absent; FrozenBN is folded into the conv weights on the fly (same
+function, one op fewer per conv).  Optimizer: AdamW + full-model grad-norm clipping
+(train_net.py:185-263, SOLVER: BASE_LR 1e-4, WEIGHT_DECAY 0.05, CLIP_VALUE 0.01).
+"""
+from __future__ import annotations
+
+import types
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from .pixel_decoder import MSDeformAttnPixelDecoder
+from .registry import ShapeSpec
+from .transformer_decoder import MultiScaleMaskedTransformerDecoder
+
+PIXEL_MEAN = (123.675, 116.280, 103.530)
+PIXEL_STD = (58.395, 57.120, 57.375)
+
+
+class FrozenBNConv(nn.Module):
+    """conv (no bias) + FrozenBatchNorm2d, applied as one conv with folded weights."""
+
+    def __init__(self, cin, cout, k, stride=1, padding=0):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, k, stride=stride, padding=padding, bias=False)
+        nn.init.kaiming_normal_(self.conv.weight, mode="fan_out", nonlinearity="relu")
+        self.register_buffer("weight", torch.ones(cout))
+        self.register_buffer("bias", torch.zeros(cout))
+        self.register_buffer("running_mean", torch.zeros(cout))
+        self.register_buffer("running_var", torch.ones(cout))
+        self.eps = 1e-5
+
+    def forward(self, x):
+        scale = self.weight * (self.running_var + self.eps).rsqrt()
+        shift = self.bias - self.running_mean * scale
+        w = self.conv.weight * scale.view(-1, 1, 1, 1)
+        return F.conv2d(x, w, shift, self.conv.stride, self.conv.padding)
+
+
+class Bottleneck(nn.Module):
+    def __init__(self, cin, cb, cout, stride):
+        super().__init__()
+        self.shortcut = FrozenBNConv(cin, cout, 1, stride) if (cin != cout or stride != 1) else None
+        self.conv1 = FrozenBNConv(cin, cb, 1, 1)             # STRIDE_IN_1X1: False
+        self.conv2 = FrozenBNConv(cb, cb, 3, stride, 1)
+        self.conv3 = FrozenBNConv(cb, cout, 1, 1)
+
+    def forward(self, x):
+        out = F.relu_(self.conv1(x))
+        out = F.relu_(self.conv2(out))
+        out = self.conv3(out)
+        sc = self.shortcut(x) if self.shortcut is not None else x
+        return F.relu_(out + sc)
+
+
+class ResNet50(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.stem = FrozenBNConv(3, 64, 7, 2, 3)
+        cfg = [("res2", 3, 64, 256, 1), ("res3", 4, 128, 512, 2), ("res4", 6, 256, 1024, 2),
+               ("res5", 3, 512, 2048, 2)]
+        cin = 64
+        self.stage_names = []
+        for name, n, cb, cout, stride in cfg:
+            blocks = [Bottleneck(cin if i == 0 else cout, cb, cout, stride if i == 0 else 1) for i in range(n)]
+            self.add_module(name, nn.Sequential(*blocks))
+            self.stage_names.append(name)
+            cin = cout
+
+    def output_shape(self):
+        ch = {"res2": 256, "res3": 512, "res4": 1024, "res5": 2048}
+        st = {"res2": 4, "res3": 8, "res4": 16, "res5": 32}
+        return {k: ShapeSpec(channels=ch[k], stride=st[k]) for k in self.stage_names}
+
+    def forward(self, x):
+        x = F.relu_(self.stem(x))
+        x = F.max_pool2d(x, kernel_size=3, stride=2, padding=1)
+        out = {}
+        for name in self.stage_names:
+            x = getattr(self, name)(x)
+            out[name] = x
+        return out
+
+
+def default_cfg(num_queries=100, num_classes=133):
+    """The model-shape keys of configs/coco/panoptic-segmentation/maskformer2_R50_bs16_50ep.yaml."""
+    n = types.SimpleNamespace
+    return n(MODEL=n(
+        SEM_SEG_HEAD=n(IN_FEATURES=["res2", "res3", "res4", "res5"], CONVS_DIM=256, MASK_DIM=256, NORM="GN",
+                       TRANSFORMER_ENC_LAYERS=6, DEFORMABLE_TRANSFORMER_ENCODER_IN_FEATURES=["res3", "res4", "res5"],
+                       COMMON_STRIDE=4, NUM_CLASSES=num_classes, PIXEL_DECODER_NAME="MSDeformAttnPixelDecoder"),
+        MASK_FORMER=n(DROPOUT=0.0, NHEADS=8, HIDDEN_DIM=256, NUM_OBJECT_QUERIES=num_queries, DIM_FEEDFORWARD=2048,
+                      DEC_LAYERS=10, PRE_NORM=False, ENFORCE_INPUT_PROJ=False,
+                      TRANSFORMER_DECODER_NAME="MultiScaleMaskedTransformerDecoder")))
+
+
+class MaskFormerR50(nn.Module):
+    def __init__(self, cfg=None):
+        super().__init__()
+        cfg = cfg or default_cfg()
+        self.backbone = ResNet50()
+        self.pixel_decoder = MSDeformAttnPixelDecoder(cfg, self.backbone.output_shape())
+        self.predictor = MultiScaleMaskedTransformerDecoder(cfg, cfg.MODEL.SEM_SEG_HEAD.CONVS_DIM, True)
+        self.register_buffer("pixel_mean", torch.tensor(PIXEL_MEAN).view(-1, 1, 1), False)
+        self.register_buffer("pixel_std", torch.tensor(PIXEL_STD).view(-1, 1, 1), False)
+
+    def forward(self, images):
+        x = (images - self.pixel_mean) / self.pixel_std
+        features = self.backbone(x)
+        mask_features, _, multi_scale = self.pixel_decoder.forward_features(features)
+        return self.predictor(multi_scale, mask_features)
+
+
+def surrogate_loss(out):
+    """Sum over the 10 heads of mean(pred_logits) + mean(pred_masks)."""
+    heads = [out] + list(out["aux_outputs"])
+    return sum(h["pred_logits"].float().mean() + h["pred_masks"].float().mean() for h in heads)
+
+
+def make_optimizer(model):
+    return torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.05, foreach=True)
+
+
+def train_step(model, opt, images, amp_dtype=torch.bfloat16, clip=0.01):
+    opt.zero_grad(set_to_none=True)
+    with torch.autocast(device_type=images.device.type, dtype=amp_dtype, enabled=amp_dtype is not None):
+        out = model(images)
+        loss = surrogate_loss(out)
+    loss.backward()
+    torch.nn.utils.clip_grad_norm_(model.parameters(), clip, foreach=True)
+    opt.step()
+    return loss.detach()

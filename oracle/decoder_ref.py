@@ -1,5 +1,8 @@
-"""Test-only torch restatements of the decoder ops' reference semantics, used to exercise the bm2f_amd
-decoder modules on CPU (patched in place of the HIP ops) and as the GPU kernels' checkers.
+"""TEST INFRASTRUCTURE ONLY — torch restatements of the decoder ops' reference semantics.
+
+Used as the GPU kernels' checkers (tests/), to exercise the bm2f_amd decoder modules on CPU (patched in
+place of the HIP ops), and by bench.py's cpu_baseline leg (the reference's CPU path).  Pinned by the
+reference's golden decoder outputs (tests/golden/decoder.npz, video_decoder.npz: bit-exact masks).
 
 * ref_attn_bool: F.interpolate(bilinear, align_corners=False) -> sigmoid -> < 0.5 in the logits' dtype,
   then the fully-masked-row fix (mask2former_transformer_decoder.py:446-449, :400).

@@ -1,13 +1,13 @@
 """Decoder HIP kernels on the GPU: attention-mask bits (bit-exact vs torch's own GPU interpolate +
 sigmoid + threshold in the same dtype, i.e. the reference's ops on the same device) and masked
-attention fwd/bwd vs an fp32 restatement of nn.MultiheadAttention's math (tests/torch_ref_ops.py)."""
+attention fwd/bwd vs an fp32 restatement of nn.MultiheadAttention's math (oracle/decoder_ref.py)."""
 import math
 
 import numpy as np
 import pytest
 import torch
 
-from torch_ref_ops import pack_bits, ref_attn_bool, ref_masked_attention, unpack_bits
+from oracle.decoder_ref import pack_bits, ref_attn_bool, ref_masked_attention, unpack_bits
 
 pytestmark = pytest.mark.gpu
 
@@ -53,8 +53,10 @@ def _attn_case(device, B, Lq, Lk, H, dtype, density, seed):
     k = torch.randn(B, Lk, C, device=device, generator=g).to(dtype)
     v = torch.randn(B, Lk, C, device=device, generator=g).to(dtype)
     blocked = torch.rand(B, Lq, Lk, device=device, generator=g) < density
-    blocked[:, 0, 1:] = True      # only the first key open
-    blocked[:, 1, :-1] = True     # only the last key open
+    blocked[:, 0] = True          # only the first key open
+    blocked[:, 0, 0] = False
+    blocked[:, 1] = True          # only the last key open
+    blocked[:, 1, -1] = False
     blocked[:, 2] = False
     return q, k, v, blocked
 

@@ -43,7 +43,7 @@ def test_pixdec_forward_backward_cpu():
 @pytest.mark.parametrize("fixture,video", [("decoder.npz", False), ("video_decoder.npz", True)])
 def test_decoder_forward_backward_cpu(fixture, video):
     from module_cases import run_decoder
-    from torch_ref_ops import torch_decoder_ops, unpack_bits
+    from oracle.decoder_ref import torch_decoder_ops, unpack_bits
     d = build_video_decoder() if video else build_decoder()
     with torch_decoder_ops():
         g, x, mf, logits, masks, captured = run_decoder(d, torch.device("cpu"), fixture, video)

@@ -4,7 +4,7 @@ import pytest
 import torch
 
 from module_cases import build_decoder, build_pixdec, build_video_decoder, rel_err, run_decoder, run_pixdec
-from torch_ref_ops import unpack_bits
+from oracle.decoder_ref import unpack_bits
 
 pytestmark = pytest.mark.gpu
 
