@@ -1,0 +1,208 @@
+#!/usr/bin/env python
+"""Benchmark: images/sec of the Mask2Former R50 training step (fwd + bwd + AdamW) on synthetic
+1024x1024 batches, 16 images per GPU (BASELINE.json config 2; configs 3 at --gpus 8 under torchrun).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 16] [--res 1024] [--amp bf16|fp16|none]
+
+For N > 1 the driver launches one process per GPU with torch.distributed.run; gradients are all-reduced
+by DDP over RCCL (backend "nccl"), the only exchange on this path.  Rank 0 prints ONE
+JSON line.  Besides the contract fields it reports:
+  roofline      the MSDA backward kernel (the hot path's dominant hand-written kernel): algorithmic
+                bytes per launch (115.60 MB per 1024^2 image) / its mean duration,
+                measured with HIP events on the launch stream over the timed region, vs the 8 TB/s
+                HBM peak; traffic = PMC-measured HBM bytes per launch from profiles/, when committed.
+  cpu_baseline  the reference's CPU path (oracle/cpu_path.py: the same model with the reference's
+                ms_deform_attn_core_pytorch and MultiheadAttention math) on a bounded sample, rank 0, N=1.
+  kernels       mean per-launch time of each bm2f kernel family over the timed region.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")  # no exhaustive conv search on a fresh box
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "images/sec fwd+bwd, R50 100-query 1024² bs16, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+class KernelTimer:
+    """HIP events around the native calls of a few ops, on the stream they launch on."""
+
+    def __init__(self):
+        self.enabled = False
+        self.events = {}
+
+    def wrap(self, mod, name, key):
+        fn = getattr(mod, name)
+        timer = self
+
+        def wrapped(*args, **kwargs):
+            if not timer.enabled:
+                return fn(*args, **kwargs)
+            s = torch.cuda.Event(enable_timing=True)
+            e = torch.cuda.Event(enable_timing=True)
+            s.record()
+            out = fn(*args, **kwargs)
+            e.record()
+            timer.events.setdefault(key, []).append((s, e))
+            return out
+
+        setattr(mod, name, wrapped)
+
+    def summary(self):
+        torch.cuda.synchronize()
+        res = {}
+        for key, evs in self.events.items():
+            ms = [s.elapsed_time(e) for s, e in evs]
+            res[key] = {"calls": len(ms), "mean_ms": sum(ms) / len(ms), "total_ms": sum(ms)}
+        return res
+
+
+def msda_bwd_bytes(n_images, res, M=8, D=32, L=3, P=4):
+    S = sum((res // s) ** 2 for s in (32, 16, 8))
+    f = 4
+    value = n_images * S * M * D * f
+    loc = n_images * S * M * L * P * 2 * f
+    attn = n_images * S * M * L * P * f
+    return 2 * value + 2 * loc + 2 * attn + value  # reads v,loc,attn,gout; writes gv,gloc,gattn
+
+
+def load_traffic():
+    path = os.path.join(ROOT, "profiles", "msda_bwd_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--queries", type=int, default=100)
+    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16", "none"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+
+    from bm2f_amd import decoder_ops, msda
+    from bm2f_amd.bench_model import MaskFormerR50, default_cfg, make_optimizer, train_step
+
+    timer = KernelTimer()
+    timer.wrap(msda, "ms_deform_attn_backward", "msda_bwd")
+    timer.wrap(msda, "ms_deform_attn_forward", "msda_fwd")
+    timer.wrap(decoder_ops, "attn_mask_bits", "attn_mask_bits")
+
+    torch.manual_seed(0)
+    model = MaskFormerR50(default_cfg(num_queries=args.queries)).to(device)
+    if world > 1:
+        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False,
+                                                          gradient_as_bucket_view=True, bucket_cap_mb=64)
+    opt = make_optimizer(model)
+    g = torch.Generator(device=device).manual_seed(1000 + rank)
+    images = torch.randn(args.batch, 3, args.res, args.res, device=device, generator=g) * 57.0 + 117.0
+    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "none": None}[args.amp]
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    t0 = time.perf_counter()
+    for i in range(args.warmup):
+        train_step(model, opt, images, amp)
+        torch.cuda.synchronize()
+        log(f"warmup {i + 1}/{args.warmup} done ({time.perf_counter() - t0:.1f}s)")
+
+    barrier()
+    torch.cuda.synchronize()
+    timer.enabled = True
+    start = time.perf_counter()
+    last = start
+    for i in range(args.steps):
+        train_step(model, opt, images, amp)
+        if time.perf_counter() - last > 30:
+            log(f"step {i + 1}/{args.steps}")
+            last = time.perf_counter()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - start
+    timer.enabled = False
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    kern = timer.summary()
+    log(f"timed {args.steps} steps in {elapsed:.3f}s")
+
+    if rank == 0:
+        images_total = world * args.batch * args.steps
+        value = images_total / elapsed
+        bwd = kern.get("msda_bwd")
+        roof = None
+        if bwd:
+            nbytes = msda_bwd_bytes(args.batch, args.res)
+            achieved = nbytes / (bwd["mean_ms"] * 1e-3) / 1e9
+            tr = load_traffic()
+            roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": (tr or {}).get("hbm_bytes_per_launch") if tr else None,
+                    "kernel": "MSDA backward (m2f_msda_bwd_f32)", "algorithmic_bytes_per_launch": nbytes,
+                    "mean_launch_ms": round(bwd["mean_ms"], 4)}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle.cpu_path import time_cpu_step
+            log("cpu baseline ...")
+            sec, threads = time_cpu_step(res=args.res, images=1, steps=args.cpu_steps)
+            cpu = {"value": round(1.0 / sec, 4), "unit": "images/s", "cores": threads, "kind": "port",
+                   "sample": f"1 image {args.res}x{args.res} fwd+bwd (no optimizer), fp32, best of {args.cpu_steps} "
+                             "steps: same model with the reference's CPU MSDA (ms_deform_attn_core_pytorch) and "
+                             "MultiheadAttention math (oracle/cpu_path.py)"}
+        line = {
+            "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.amp if amp is not None else "fp32",
+            "data": "synthetic (randn images, random-init weights)",
+            "config": {"workload": "config 2: Mask2Former R50 COCO-panoptic, 100 queries, 1024x1024, "
+                                   f"{args.batch} images/GPU, fwd+bwd+AdamW; pixel decoder + MSDA in fp32 "
+                                   f"(as the reference forces), backbone/decoder under AMP {args.amp}",
+                       "model": "maskformer2_R50", "global_batch": world * args.batch,
+                       "seq_len": sum((args.res // s) ** 2 for s in (32, 16, 8)), "queries": args.queries,
+                       "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu,
+            "kernels": {k: {"calls_per_step": v["calls"] / args.steps, "mean_ms": round(v["mean_ms"], 4)}
+                        for k, v in kern.items()},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
