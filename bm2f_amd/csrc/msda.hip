@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace m2f {
 std::string& last_error() {
@@ -164,6 +165,7 @@ __global__ void __launch_bounds__(BS) msda_bwd_generic(
 
 struct Corners {
   int64_t o1, o2, o3, o4;     // element offsets of the 4 corner rows (clamped to valid rows)
+  int h0, w0;                 // top-left corner (may be -1; meaningful when ok)
   float w1, w2, w3, w4;       // bilinear weights
   float hy, ly, hx, lx;       // 1-lh, lh, 1-lw, lw
   bool c1, c2, c3, c4;        // corner inside the level
@@ -178,6 +180,7 @@ __device__ __forceinline__ Corners make_corners(float locx, float locy, int H, i
   const float hs = k.ok ? h : -2.f, ws = k.ok ? w : -2.f;   // invalid point: every corner outside
   const float fh = floorf(hs), fw = floorf(ws);
   const int h0 = static_cast<int>(fh), w0 = static_cast<int>(fw);
+  k.h0 = h0; k.w0 = w0;
   k.ly = hs - fh; k.lx = ws - fw;
   k.hy = 1.f - k.ly; k.hx = 1.f - k.lx;
   k.w1 = k.hy * k.hx; k.w2 = k.hy * k.lx; k.w3 = k.ly * k.hx; k.w4 = k.ly * k.lx;
@@ -310,6 +313,238 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 }
 
 // ------------------------------------------------------------------------------------------------
+// fp32 backward, spatially tiled: encoder self-attention (Lq == S, query i = pyramid position i).
+//
+// Workgroup = (spatial tile, head m, image n).  A tile is the same normalised rectangle on every level
+// (level l's tile ty spans rows [ty*H_l/nty, (ty+1)*H_l/nty)), so its queries at every level sample the
+// same neighbourhood.  Phase 0 takes the bounding box of the corners the tile's samples touch per level;
+// the window = that box clipped to the tile +- halo (halo shrunk until all windows fit the LDS budget).
+// Phase 2 accumulates grad_value corner rows into the LDS windows with ds_add_f32 (lane groups of a
+// half-wave rotate their float4 component so the 4 groups hit disjoint banks); corners outside the
+// windows go straight to HBM atomics.  Phase 3 adds every non-zero window element to HBM with
+// row-contiguous atomics (32 lanes = one 128 B row).  grad_loc / grad_attn are owned per (q, m) and
+// written once.  Results do not depend on where the windows land, only the atomic traffic does.
+// ------------------------------------------------------------------------------------------------
+constexpr int kTileMaxL = 4;
+
+struct TileGeom {
+  int L;
+  int H[kTileMaxL], W[kTileMaxL], start[kTileMaxL];
+  int nty, ntx;   // tile grid shared by all levels
+  int max_rows;   // LDS window budget (rows of 32 floats)
+  int max_halo;   // windows never extend more than this many pixels past the tile
+};
+
+__device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
+
+__device__ __forceinline__ float pick4(const f4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+
+template <int P>
+__global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
+    const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn,
+    const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
+    float* __restrict__ gloc, float* __restrict__ gattn) {
+  constexpr int D = 32;
+  extern __shared__ __attribute__((aligned(16))) float win[];
+  __shared__ int s_bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
+  __shared__ int s_wy0[kTileMaxL], s_wx0[kTileMaxL], s_wh[kTileMaxL], s_ww[kTileMaxL];
+  __shared__ int s_woff[kTileMaxL + 1];
+  __shared__ int s_qc[kTileMaxL + 1];  // prefix sums of per-level query counts
+  __shared__ int s_qy0[kTileMaxL], s_qx0[kTileMaxL], s_qw[kTileMaxL];
+
+  const int tile = blockIdx.x, m = blockIdx.y, n = blockIdx.z;
+  const int ty = tile / geo.ntx, tx = tile - ty * geo.ntx;
+  const int L = geo.L;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwaves = blockDim.x >> 6;
+  const int j = lane & 7, gq = lane >> 3;
+  const int64_t rs = static_cast<int64_t>(M) * D;
+
+  if (tid < L) {
+    const int l = tid;
+    const int y0 = tile_lo(ty, geo.H[l], geo.nty), y1 = tile_lo(ty + 1, geo.H[l], geo.nty);
+    const int x0 = tile_lo(tx, geo.W[l], geo.ntx), x1 = tile_lo(tx + 1, geo.W[l], geo.ntx);
+    s_qy0[l] = y0;
+    s_qx0[l] = x0;
+    s_qw[l] = x1 - x0;
+    s_qc[l + 1] = (y1 - y0) * (x1 - x0);
+    s_bb[l][0] = 0x7fffffff; s_bb[l][1] = -1; s_bb[l][2] = 0x7fffffff; s_bb[l][3] = -1;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    s_qc[0] = 0;
+    for (int l = 0; l < L; ++l) s_qc[l + 1] += s_qc[l];
+  }
+  __syncthreads();
+  const int Qt = s_qc[L];
+
+  // ---- phase 0: bounding boxes of the touched corners -------------------------------------------
+  {
+    int bmin_y[kTileMaxL], bmax_y[kTileMaxL], bmin_x[kTileMaxL], bmax_x[kTileMaxL];
+#pragma unroll
+    for (int l = 0; l < kTileMaxL; ++l) { bmin_y[l] = 0x7fffffff; bmax_y[l] = -1; bmin_x[l] = 0x7fffffff; bmax_x[l] = -1; }
+    for (int base = wid * 8; base < Qt; base += nwaves * 8) {
+      const int qi = base + gq;
+      if (qi < Qt) {
+        int lq = 0;
+        while (qi >= s_qc[lq + 1]) ++lq;
+        const int r = qi - s_qc[lq];
+        const int q = geo.start[lq] + (s_qy0[lq] + r / s_qw[lq]) * geo.W[lq] + s_qx0[lq] + r % s_qw[lq];
+        const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
+        for (int k = j; k < L * P; k += 8) {
+          const int l = k / P;
+          const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (pair * L * P + k));
+          const int H = geo.H[l], W = geo.W[l];
+          const float h = xy.y * H - 0.5f, w = xy.x * W - 0.5f;
+          if (h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W)) {
+            const int h0 = static_cast<int>(floorf(h)), w0 = static_cast<int>(floorf(w));
+            const int ylo = max(h0, 0), yhi = min(h0 + 1, H - 1), xlo = max(w0, 0), xhi = min(w0 + 1, W - 1);
+#pragma unroll
+            for (int ll = 0; ll < kTileMaxL; ++ll)
+              if (ll == l) {
+                bmin_y[ll] = min(bmin_y[ll], ylo); bmax_y[ll] = max(bmax_y[ll], yhi);
+                bmin_x[ll] = min(bmin_x[ll], xlo); bmax_x[ll] = max(bmax_x[ll], xhi);
+              }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int l = 0; l < kTileMaxL; ++l) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        bmin_y[l] = min(bmin_y[l], __shfl_xor(bmin_y[l], o)); bmax_y[l] = max(bmax_y[l], __shfl_xor(bmax_y[l], o));
+        bmin_x[l] = min(bmin_x[l], __shfl_xor(bmin_x[l], o)); bmax_x[l] = max(bmax_x[l], __shfl_xor(bmax_x[l], o));
+      }
+      if (lane == 0 && l < L) {
+        atomicMin(&s_bb[l][0], bmin_y[l]); atomicMax(&s_bb[l][1], bmax_y[l]);
+        atomicMin(&s_bb[l][2], bmin_x[l]); atomicMax(&s_bb[l][3], bmax_x[l]);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- window choice ----------------------------------------------------------------------------
+  if (tid == 0) {
+    for (int halo = geo.max_halo; halo >= 0; --halo) {
+      int total = 0;
+      for (int l = 0; l < L; ++l) {
+        const int H = geo.H[l], W = geo.W[l];
+        const int ry0 = max(tile_lo(ty, H, geo.nty) - halo, 0), ry1 = min(tile_lo(ty + 1, H, geo.nty) - 1 + halo, H - 1);
+        const int rx0 = max(tile_lo(tx, W, geo.ntx) - halo, 0), rx1 = min(tile_lo(tx + 1, W, geo.ntx) - 1 + halo, W - 1);
+        const int wy0 = max(ry0, s_bb[l][0]), wy1 = min(ry1, s_bb[l][1]);
+        const int wx0 = max(rx0, s_bb[l][2]), wx1 = min(rx1, s_bb[l][3]);
+        const int wh = wy1 >= wy0 ? wy1 - wy0 + 1 : 0, ww = wx1 >= wx0 ? wx1 - wx0 + 1 : 0;
+        s_wy0[l] = wy0; s_wx0[l] = wx0;
+        s_wh[l] = (wh && ww) ? wh : 0; s_ww[l] = (wh && ww) ? ww : 0;
+        s_woff[l] = total;
+        total += s_wh[l] * s_ww[l];
+      }
+      s_woff[L] = total;
+      if (total <= geo.max_rows) break;
+      if (halo == 0) {  // cannot happen when the budget covers a tile's own footprint; stay correct anyway
+        for (int l = 0; l <= L; ++l) s_woff[l] = 0;
+        for (int l = 0; l < L; ++l) { s_wh[l] = 0; s_ww[l] = 0; }
+      }
+    }
+  }
+  __syncthreads();
+  const int rows_total = s_woff[L];
+  {
+    f4* w4 = reinterpret_cast<f4*>(win);
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    for (int i = tid; i < rows_total * (D / 4); i += blockDim.x) w4[i] = z;
+  }
+  __syncthreads();
+
+  // ---- phase 2: gradients; grad_value into the windows --------------------------------------------
+  for (int base = wid * 8; base < Qt; base += nwaves * 8) {
+    const int qi = base + gq;
+    if (qi >= Qt) continue;  // whole lane group (same qi) idles together
+    int lq = 0;
+    while (qi >= s_qc[lq + 1]) ++lq;
+    const int r = qi - s_qc[lq];
+    const int q = geo.start[lq] + (s_qy0[lq] + r / s_qw[lq]) * geo.W[lq] + s_qx0[lq] + r % s_qw[lq];
+    const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
+    const f4 g = ld4(gout + pair * D + 4 * j);
+    const f4 z = {0.f, 0.f, 0.f, 0.f};
+    for (int l = 0; l < L; ++l) {
+      const int H = geo.H[l], W = geo.W[l];
+      const int64_t lbase = ((static_cast<int64_t>(n) * S + geo.start[l]) * M + m) * D + 4 * j;
+      const int wy0 = s_wy0[l], wx0 = s_wx0[l], wh = s_wh[l], ww = s_ww[l], woff = s_woff[l];
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        const int64_t kk = (pair * L + l) * P + p;
+        const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * kk);
+        const float a = attn[kk];
+        const Corners k = make_corners(xy.x, xy.y, H, W, lbase, rs);
+        f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
+        v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
+        const f4 tg = g * a;
+        const f4 val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
+        const f4 gw = -k.hy * v1 + k.hy * v2 - k.ly * v3 + k.ly * v4;
+        const f4 gh = -k.hx * v1 - k.lx * v2 + k.hx * v3 + k.lx * v4;
+        const f4 ta = g * val, tx2 = gw * tg, ty2 = gh * tg;
+        float pa = ta.x + ta.y + ta.z + ta.w;
+        float px = tx2.x + tx2.y + tx2.z + tx2.w;
+        float py = ty2.x + ty2.y + ty2.z + ty2.w;
+#pragma unroll
+        for (int o = 4; o > 0; o >>= 1) {
+          pa += __shfl_xor(pa, o);
+          px += __shfl_xor(px, o);
+          py += __shfl_xor(py, o);
+        }
+        if (j == 0) {
+          gattn[kk] = k.ok ? pa : 0.f;
+          *reinterpret_cast<float2*>(gloc + 2 * kk) = k.ok ? make_float2(W * px, H * py) : make_float2(0.f, 0.f);
+        }
+        if (k.ok) {
+          const int dy = k.h0 - wy0, dx = k.w0 - wx0;
+          const bool iny0 = dy >= 0 && dy < wh, iny1 = dy + 1 >= 0 && dy + 1 < wh;
+          const bool inx0 = dx >= 0 && dx < ww, inx1 = dx + 1 >= 0 && dx + 1 < ww;
+          const int rbase = woff + dy * ww + dx;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const bool valid = c == 0 ? k.c1 : (c == 1 ? k.c2 : (c == 2 ? k.c3 : k.c4));
+            if (!valid) continue;
+            const float wc = c == 0 ? k.w1 : (c == 1 ? k.w2 : (c == 2 ? k.w3 : k.w4));
+            const bool inside = (c < 2 ? iny0 : iny1) && ((c & 1) ? inx1 : inx0);
+            const f4 contrib = wc * tg;
+            if (inside) {
+              float* row = win + (rbase + (c >> 1) * ww + (c & 1)) * D + 4 * j;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int comp = (e + gq) & 3;
+                atomicAdd(row + comp, pick4(contrib, comp));
+              }
+            } else {
+              const int64_t o = c == 0 ? k.o1 : (c == 1 ? k.o2 : (c == 2 ? k.o3 : k.o4));
+              atomicAdd(gvalue + o, contrib.x); atomicAdd(gvalue + o + 1, contrib.y);
+              atomicAdd(gvalue + o + 2, contrib.z); atomicAdd(gvalue + o + 3, contrib.w);
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 3: flush the windows ----------------------------------------------------------------
+  for (int idx = tid; idx < rows_total * D; idx += blockDim.x) {
+    const float v = win[idx];
+    if (v == 0.f) continue;
+    const int row = idx >> 5, ch = idx & 31;
+    int l = 0;
+    while (row >= s_woff[l + 1]) ++l;
+    const int rr = row - s_woff[l];
+    const int y = s_wy0[l] + rr / s_ww[l], x = s_wx0[l] + rr % s_ww[l];
+    const int64_t o = ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D + ch;
+    atomicAdd(gvalue + o, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------------
 
@@ -388,11 +623,56 @@ int fwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
   return m2f::check_launch(fn);
 }
 
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
+// Tiled backward when the queries are the flattened pyramid (Lq == S) and the host knows the shapes.
+bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,
+                      const int64_t* host_shapes, float* gv, float* gl, float* ga, hipStream_t st) {
+  if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
+  if (env_int("M2F_MSDA_BWD_TILED", 1) == 0) return false;
+  TileGeom geo{};
+  geo.L = d.L;
+  int64_t total = 0;
+  int fi = 0;
+  for (int l = 0; l < d.L; ++l) {
+    geo.H[l] = static_cast<int>(host_shapes[2 * l]);
+    geo.W[l] = static_cast<int>(host_shapes[2 * l + 1]);
+    geo.start[l] = static_cast<int>(total);
+    total += static_cast<int64_t>(geo.H[l]) * geo.W[l];
+    if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
+  }
+  if (total != d.S) return false;
+  const int tile = env_int("M2F_MSDA_TILE", 16);
+  geo.nty = (geo.H[fi] + tile - 1) / tile;
+  geo.ntx = (geo.W[fi] + tile - 1) / tile;
+  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 1152);
+  geo.max_halo = env_int("M2F_MSDA_HALO", 8);
+  // the budget must hold every level's share of one tile (halo 0)
+  int own = 0;
+  for (int l = 0; l < d.L; ++l) {
+    const int th = (geo.H[l] + geo.nty - 1) / geo.nty + 1, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx + 1;
+    own += th * tw;
+  }
+  if (own > geo.max_rows) return false;
+  const size_t lds = static_cast<size_t>(geo.max_rows) * 32 * sizeof(float);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<4>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
+    attr = true;
+  }
+  const dim3 grid(geo.nty * geo.ntx, d.M, d.N);
+  msda_bwd_f32_tiled<4><<<grid, 512, lds, st>>>(value, loc, attn, gout, geo, d.S, d.M, gv, gl, ga);
+  return true;
+}
+
 template <typename T>
 int bwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_t* lsi, const T* loc,
              const T* attn, const T* gout, const Dims& d, int im2col_step, const int64_t* host_shapes, T* gv,
              T* gl, T* ga, hipStream_t st) {
-  (void)host_shapes;
   int rc = check_dims(fn, value, shapes, lsi, loc, attn, d, im2col_step);
   if (rc) return rc;
   if (!gout || !gv || !gl || !ga) return m2f::fail(M2F_EINVAL, "%s: null gradient pointer", fn);
@@ -402,11 +682,14 @@ int bwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
   bool done = false;
   if constexpr (std::is_same<T, float>::value) {
     if (fast_f32_ok(d, value, loc, gout) && m2f::aligned(gv, 16) && m2f::aligned(gl, 8)) {
-      if (d.D == 16) launch_bwd_vec<16>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
+      if (launch_bwd_tiled(value, loc, attn, gout, d, host_shapes, gv, gl, ga, st)) done = true;
+      else if (d.D == 16) launch_bwd_vec<16>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
       else if (d.D == 32) launch_bwd_vec<32>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
       else launch_bwd_vec<64>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
       done = true;
     }
+  } else {
+    (void)host_shapes;
   }
   if (!done) {
     const int64_t npairs = d.npairs();

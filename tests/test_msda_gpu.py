@@ -157,3 +157,50 @@ def test_full_size_properties(device):
     # <grad_attn, a> == <grad_out, out> (the forward is linear in attn too)
     rhs_a = (ga.double() * a.double()).sum()
     assert abs((lhs - rhs_a) / lhs).item() < 1e-4
+
+
+def _pyramid_case(shapes, N, M, far_frac, seed):
+    """Encoder-like inputs: query i = pyramid position i, samples near the reference point plus a
+    fraction far away (exercising the out-of-window path of the tiled backward)."""
+    gen = torch.Generator().manual_seed(seed)
+    st = torch.tensor(shapes, dtype=torch.int64)
+    lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
+    S = int(st.prod(1).sum())
+    L, P, D = len(shapes), 4, 32
+    refs = []
+    for h, w in shapes:
+        ys, xs = torch.meshgrid(torch.linspace(0.5, h - 0.5, h), torch.linspace(0.5, w - 0.5, w), indexing="ij")
+        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
+    ref = torch.cat(refs, 0)
+    norm = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32)
+    off = torch.randn(N, S, M, L, P, 2, generator=gen) * 2.0
+    loc = ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]
+    far = torch.rand(N, S, M, L, P, 1, generator=gen) < far_frac
+    loc = torch.where(far, torch.rand(N, S, M, L, P, 2, generator=gen) * 1.2 - 0.1, loc)
+    value = torch.randn(N, S, M, D, generator=gen)
+    attn = torch.rand(N, S, M, L, P, generator=gen)
+    gout = torch.randn(N, S, M * D, generator=gen)
+    return value, st, lsi, loc.contiguous(), attn, gout
+
+
+@pytest.mark.parametrize("tile,rows,halo", [(16, 1152, 8), (8, 480, 8), (4, 64, 2), (8, 200, 0)])
+def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo):
+    from bm2f_amd import msda
+    monkeypatch.setenv("M2F_MSDA_TILE", str(tile))
+    monkeypatch.setenv("M2F_MSDA_WIN_ROWS", str(rows))
+    monkeypatch.setenv("M2F_MSDA_HALO", str(halo))
+    shapes = [(6, 10), (12, 20), (24, 40)]   # non-square, tiles not dividing every level evenly
+    value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 2, 8, 0.05, tile + rows)
+    dst = msda.attach_host_shapes(st.to(device), shapes)
+    gv, gl, ga = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
+                                             attn.to(device), gout.to(device), 64)
+    wv, wl, wa = msda_ref.msda_backward(value.double(), st, lsi, loc.double(), attn.double(), gout.double())
+    _close(gv.cpu(), wv)
+    _close(ga.cpu(), wa)
+    _close(gl.cpu(), wl, atol_frac=1e-4)
+    # identical to the untiled kernel up to summation order
+    monkeypatch.setenv("M2F_MSDA_BWD_TILED", "0")
+    gv2, gl2, ga2 = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
+                                                attn.to(device), gout.to(device), 64)
+    torch.testing.assert_close(gv, gv2, rtol=1e-5, atol=1e-5)
+    assert torch.equal(ga, ga2) and torch.equal(gl, gl2)
