@@ -319,10 +319,13 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // (level l's tile ty spans rows [ty*H_l/nty, (ty+1)*H_l/nty)), so its queries at every level sample the
 // same neighbourhood.  Phase 0 takes the bounding box of the corners the tile's samples touch per level;
 // the window = that box clipped to the tile +- halo (halo shrunk until all windows fit the LDS budget).
-// Phase 2 accumulates grad_value corner rows into the LDS windows with ds_add_f32 (lane groups of a
-// half-wave rotate their float4 component so the 4 groups hit disjoint banks); corners outside the
-// windows go straight to HBM atomics.  Phase 3 adds every non-zero window element to HBM with
-// row-contiguous atomics (32 lanes = one 128 B row).  grad_loc / grad_attn are owned per (q, m) and
+// Phase 2 accumulates grad_value corner rows into the LDS windows as exact fixed point: every
+// contribution w*g*a is bounded by B = max|g| * max|a| over the workgroup (phase 0), scaled by 2^e with
+// 2^e * B * (contributions per element <= Qt*L*P) < 2^62 (no int64 overflow) and added with ds_add_u64.
+// gfx950's ds_add_f32 runs at ~190 cycles per wave-instruction, ds_add_u64 at ~30 (tools/ubench), and
+// the integer sum is order-independent.  Corners outside the windows go straight to HBM atomics.
+// Phase 3 converts every non-zero element back (x 2^-e) and adds it to HBM with row-contiguous atomics
+// (32 lanes = one 128 B row).  A workgroup whose bound is 0 / non-finite uses direct atomics only.  grad_loc / grad_attn are owned per (q, m) and
 // written once.  Results do not depend on where the windows land, only the atomic traffic does.
 // ------------------------------------------------------------------------------------------------
 constexpr int kTileMaxL = 4;
@@ -333,6 +336,7 @@ struct TileGeom {
   int nty, ntx;   // tile grid shared by all levels
   int max_rows;   // LDS window budget (rows of 32 floats)
   int max_halo;   // windows never extend more than this many pixels past the tile
+  int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no LDS adds, 2 no flush, 4 no spill atomics
 };
 
 __device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
@@ -342,13 +346,16 @@ __device__ __forceinline__ float pick4(const f4& v, int c) {
 }
 
 template <int P>
-__global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
+__global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
     float* __restrict__ gloc, float* __restrict__ gattn) {
   constexpr int D = 32;
-  extern __shared__ __attribute__((aligned(16))) float win[];
+  extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
   __shared__ int s_bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
+  __shared__ unsigned int s_gmax, s_amax;  // max |grad_out|, max |attn| (float bits, non-negative)
+  __shared__ float s_scale;
+  __shared__ double s_unscale;
   __shared__ int s_wy0[kTileMaxL], s_wx0[kTileMaxL], s_wh[kTileMaxL], s_ww[kTileMaxL];
   __shared__ int s_woff[kTileMaxL + 1];
   __shared__ int s_qc[kTileMaxL + 1];  // prefix sums of per-level query counts
@@ -371,6 +378,7 @@ __global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
     s_qc[l + 1] = (y1 - y0) * (x1 - x0);
     s_bb[l][0] = 0x7fffffff; s_bb[l][1] = -1; s_bb[l][2] = 0x7fffffff; s_bb[l][3] = -1;
   }
+  if (tid == 0) { s_gmax = 0u; s_amax = 0u; }
   __syncthreads();
   if (tid == 0) {
     s_qc[0] = 0;
@@ -384,6 +392,7 @@ __global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
     int bmin_y[kTileMaxL], bmax_y[kTileMaxL], bmin_x[kTileMaxL], bmax_x[kTileMaxL];
 #pragma unroll
     for (int l = 0; l < kTileMaxL; ++l) { bmin_y[l] = 0x7fffffff; bmax_y[l] = -1; bmin_x[l] = 0x7fffffff; bmax_x[l] = -1; }
+    float gmax = 0.f, amax = 0.f;
     for (int base = wid * 8; base < Qt; base += nwaves * 8) {
       const int qi = base + gq;
       if (qi < Qt) {
@@ -392,8 +401,11 @@ __global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
         const int r = qi - s_qc[lq];
         const int q = geo.start[lq] + (s_qy0[lq] + r / s_qw[lq]) * geo.W[lq] + s_qx0[lq] + r % s_qw[lq];
         const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
+        const f4 gv4 = ld4(gout + pair * D + 4 * j);
+        gmax = fmaxf(gmax, fmaxf(fmaxf(fabsf(gv4.x), fabsf(gv4.y)), fmaxf(fabsf(gv4.z), fabsf(gv4.w))));
         for (int k = j; k < L * P; k += 8) {
           const int l = k / P;
+          amax = fmaxf(amax, fabsf(attn[pair * L * P + k]));
           const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (pair * L * P + k));
           const int H = geo.H[l], W = geo.W[l];
           const float h = xy.y * H - 0.5f, w = xy.x * W - 0.5f;
@@ -422,12 +434,31 @@ __global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
         atomicMin(&s_bb[l][2], bmin_x[l]); atomicMax(&s_bb[l][3], bmax_x[l]);
       }
     }
+    // NaN compares false in fmaxf chains; record it explicitly so the workgroup falls back to atomics
+    if (gmax != gmax) gmax = INFINITY;
+    if (amax != amax) amax = INFINITY;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      gmax = fmaxf(gmax, __shfl_xor(gmax, o));
+      amax = fmaxf(amax, __shfl_xor(amax, o));
+    }
+    if (lane == 0) {
+      atomicMax(&s_gmax, __float_as_uint(gmax));
+      atomicMax(&s_amax, __float_as_uint(amax));
+    }
   }
   __syncthreads();
 
   // ---- window choice ----------------------------------------------------------------------------
   if (tid == 0) {
-    for (int halo = geo.max_halo; halo >= 0; --halo) {
+    const float bound = __uint_as_float(s_gmax) * __uint_as_float(s_amax);
+    const bool use_lds = bound > 1e-30f && bound < 1e30f;  // else: direct atomics (zeros, inf or NaN)
+    // at most Qt*L*P contributions reach one element: keep their sum below 2^62
+    const int cnt_bits = 32 - __clz(max(Qt * L * P, 1)) + 1;
+    const int e = use_lds ? 62 - cnt_bits - static_cast<int>(ceilf(log2f(bound))) : 0;
+    s_scale = use_lds ? ldexpf(1.f, e) : 0.f;
+    s_unscale = use_lds ? ldexp(1.0, -e) : 0.0;
+    for (int halo = use_lds ? geo.max_halo : -1; halo >= 0; --halo) {
       int total = 0;
       for (int l = 0; l < L; ++l) {
         const int H = geo.H[l], W = geo.W[l];
@@ -448,14 +479,15 @@ __global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
         for (int l = 0; l < L; ++l) { s_wh[l] = 0; s_ww[l] = 0; }
       }
     }
+    if (!use_lds) {
+      for (int l = 0; l <= L; ++l) s_woff[l] = 0;
+      for (int l = 0; l < L; ++l) { s_wh[l] = 0; s_ww[l] = 0; s_wy0[l] = 0; s_wx0[l] = 0; }
+    }
   }
   __syncthreads();
   const int rows_total = s_woff[L];
-  {
-    f4* w4 = reinterpret_cast<f4*>(win);
-    const f4 z = {0.f, 0.f, 0.f, 0.f};
-    for (int i = tid; i < rows_total * (D / 4); i += blockDim.x) w4[i] = z;
-  }
+  const float fscale = s_scale;
+  for (int i = tid; i < rows_total * D; i += blockDim.x) win[i] = 0ull;
   __syncthreads();
 
   // ---- phase 2: gradients; grad_value into the windows --------------------------------------------
@@ -512,13 +544,16 @@ __global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
             const bool inside = (c < 2 ? iny0 : iny1) && ((c & 1) ? inx1 : inx0);
             const f4 contrib = wc * tg;
             if (inside) {
-              float* row = win + (rbase + (c >> 1) * ww + (c & 1)) * D + 4 * j;
+              if (geo.ablate & 1) continue;
+              unsigned long long* row = win + (rbase + (c >> 1) * ww + (c & 1)) * D + 4 * j;
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
-                const int comp = (e + gq) & 3;
-                atomicAdd(row + comp, pick4(contrib, comp));
+                const int comp = (e + gq) & 3;  // the 4 lane groups of a half-wave hit disjoint banks
+                const long long fx = __float2ll_rn(pick4(contrib, comp) * fscale);
+                atomicAdd(row + comp, static_cast<unsigned long long>(fx));
               }
             } else {
+              if (geo.ablate & 4) continue;
               const int64_t o = c == 0 ? k.o1 : (c == 1 ? k.o2 : (c == 2 ? k.o3 : k.o4));
               atomicAdd(gvalue + o, contrib.x); atomicAdd(gvalue + o + 1, contrib.y);
               atomicAdd(gvalue + o + 2, contrib.z); atomicAdd(gvalue + o + 3, contrib.w);
@@ -531,9 +566,12 @@ __global__ void __launch_bounds__(512) msda_bwd_f32_tiled(
   __syncthreads();
 
   // ---- phase 3: flush the windows ----------------------------------------------------------------
-  for (int idx = tid; idx < rows_total * D; idx += blockDim.x) {
-    const float v = win[idx];
-    if (v == 0.f) continue;
+  const int flush_end = (geo.ablate & 2) ? 0 : rows_total * D;
+  const double unscale = s_unscale;
+  for (int idx = tid; idx < flush_end; idx += blockDim.x) {
+    const long long fx = static_cast<long long>(win[idx]);
+    if (fx == 0) continue;
+    const float v = static_cast<float>(static_cast<double>(fx) * unscale);
     const int row = idx >> 5, ch = idx & 31;
     int l = 0;
     while (row >= s_woff[l + 1]) ++l;
@@ -645,11 +683,13 @@ bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, c
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   if (total != d.S) return false;
-  const int tile = env_int("M2F_MSDA_TILE", 16);
+  const int tile = env_int("M2F_MSDA_TILE", 8);
+  const int threads = env_int("M2F_MSDA_THREADS", 1024);
   geo.nty = (geo.H[fi] + tile - 1) / tile;
   geo.ntx = (geo.W[fi] + tile - 1) / tile;
-  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 1152);
+  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 576);
   geo.max_halo = env_int("M2F_MSDA_HALO", 8);
+  geo.ablate = env_int("M2F_MSDA_ABLATE", 0);
   // the budget must hold every level's share of one tile (halo 0)
   int own = 0;
   for (int l = 0; l < d.L; ++l) {
@@ -657,7 +697,8 @@ bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, c
     own += th * tw;
   }
   if (own > geo.max_rows) return false;
-  const size_t lds = static_cast<size_t>(geo.max_rows) * 32 * sizeof(float);
+  const size_t lds = static_cast<size_t>(geo.max_rows) * 32 * sizeof(unsigned long long);
+  if (lds > 150 * 1024 || (threads != 256 && threads != 512 && threads != 1024)) return false;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<4>),
@@ -665,7 +706,7 @@ bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, c
     attr = true;
   }
   const dim3 grid(geo.nty * geo.ntx, d.M, d.N);
-  msda_bwd_f32_tiled<4><<<grid, 512, lds, st>>>(value, loc, attn, gout, geo, d.S, d.M, gv, gl, ga);
+  msda_bwd_f32_tiled<4><<<grid, threads, lds, st>>>(value, loc, attn, gout, geo, d.S, d.M, gv, gl, ga);
   return true;
 }
 

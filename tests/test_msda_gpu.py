@@ -183,12 +183,14 @@ def _pyramid_case(shapes, N, M, far_frac, seed):
     return value, st, lsi, loc.contiguous(), attn, gout
 
 
-@pytest.mark.parametrize("tile,rows,halo", [(16, 1152, 8), (8, 480, 8), (4, 64, 2), (8, 200, 0)])
-def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo):
+@pytest.mark.parametrize("tile,rows,halo,threads", [(16, 576, 8, 1024), (8, 480, 8, 512), (4, 64, 2, 256),
+                                                     (8, 200, 0, 1024)])
+def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, threads):
     from bm2f_amd import msda
     monkeypatch.setenv("M2F_MSDA_TILE", str(tile))
     monkeypatch.setenv("M2F_MSDA_WIN_ROWS", str(rows))
     monkeypatch.setenv("M2F_MSDA_HALO", str(halo))
+    monkeypatch.setenv("M2F_MSDA_THREADS", str(threads))
     shapes = [(6, 10), (12, 20), (24, 40)]   # non-square, tiles not dividing every level evenly
     value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 2, 8, 0.05, tile + rows)
     dst = msda.attach_host_shapes(st.to(device), shapes)
@@ -204,3 +206,21 @@ def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo):
                                                 attn.to(device), gout.to(device), 64)
     torch.testing.assert_close(gv, gv2, rtol=1e-5, atol=1e-5)
     assert torch.equal(ga, ga2) and torch.equal(gl, gl2)
+
+
+def test_tiled_backward_nonfinite_and_zero_grads(device):
+    """A workgroup whose grad bound is 0 or non-finite must fall back to plain atomics: NaN/inf in
+    grad_output propagate into grad_value exactly as the reference's atomics would."""
+    from bm2f_amd import msda
+    shapes = [(4, 4), (8, 8), (16, 16)]
+    value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 1, 8, 0.0, 7)
+    gout[:, :16] = 0.0
+    gout[0, 100, 5] = float("nan")
+    dst = msda.attach_host_shapes(st.to(device), shapes)
+    gv, gl, ga = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
+                                             attn.to(device), gout.to(device), 64)
+    wv, wl, wa = msda_ref.msda_backward(value.double(), st, lsi, loc.double(), attn.double(), gout.double())
+    got, want = gv.cpu().double().numpy(), wv
+    assert np.array_equal(np.isnan(got), np.isnan(want))
+    fin = np.isfinite(want)
+    np.testing.assert_allclose(got[fin], want[fin], rtol=1e-3, atol=1e-5 * np.abs(want[fin]).max())

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bm2f_amd import msda  # noqa: E402
 
 
-def make_inputs(N, shapes, M=8, D=32, P=4, stress=False, device="cuda", seed=0):
+def make_inputs(N, shapes, M=8, D=32, P=4, stress=False, device="cuda", seed=0, noise=1.0):
     g = torch.Generator(device=device).manual_seed(seed)
     st = torch.tensor(shapes, dtype=torch.int64, device=device)
     msda.attach_host_shapes(st, shapes)
@@ -39,7 +39,7 @@ def make_inputs(N, shapes, M=8, D=32, P=4, stress=False, device="cuda", seed=0):
         grid = grid / grid.abs().max(-1, keepdim=True)[0]
         off = grid.view(M, 1, 1, 2) * torch.arange(1, P + 1, device=device).view(1, 1, P, 1)
         off = off.expand(M, L, P, 2)
-        off = off[None, None] + torch.randn(N, S, M, L, P, 2, device=device, generator=g)
+        off = off[None, None] + noise * torch.randn(N, S, M, L, P, 2, device=device, generator=g)
         norm = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32, device=device)
         loc = ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]
     attn = torch.rand(N, S, M, L, P, device=device, generator=g)
@@ -68,18 +68,21 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--stress", action="store_true")
     ap.add_argument("--no-host-shapes", action="store_true")
+    ap.add_argument("--noise", type=float, default=1.0, help="px std of the offsets around the init rays")
+    ap.add_argument("--bwd-only", action="store_true")
     a = ap.parse_args()
     r = a.res
     shapes = [(r // 32, r // 32), (r // 16, r // 16), (r // 8, r // 8)]
-    v, st, lsi, loc, attn, gout = make_inputs(a.n, shapes, stress=a.stress)
+    v, st, lsi, loc, attn, gout = make_inputs(a.n, shapes, stress=a.stress, noise=a.noise)
     if a.no_host_shapes:
         delattr(st, "_bm2f_host_shapes")
     per_img = (r / 1024) ** 2
     fwd_bytes = 68.81e6 * per_img * a.n
     bwd_bytes = 115.60e6 * per_img * a.n
-    tf = timeit(lambda: msda.ms_deform_attn_forward(v, st, lsi, loc, attn, 64), a.iters)
+    tf = 0.0 if a.bwd_only else timeit(lambda: msda.ms_deform_attn_forward(v, st, lsi, loc, attn, 64), a.iters)
     tb = timeit(lambda: msda.ms_deform_attn_backward(v, st, lsi, loc, attn, gout, 64), a.iters)
-    print(f"N={a.n} res={r} stress={a.stress}: fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
+    tf = tf or float("nan")
+    print(f"N={a.n} res={r} stress={a.stress} noise={a.noise} env={ {k: v for k, v in os.environ.items() if k.startswith('M2F_')} }: fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
           f"bwd {tb:.3f} ms ({bwd_bytes / tb / 1e6:.0f} GB/s alg)")
 
 
