@@ -341,6 +341,15 @@ struct TileGeom {
 
 __device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
 
+// Sum over each aligned group of 8 lanes with DPP moves (VALU, no LDS crossbar): xor 1, xor 2 within
+// quads, then row_half_mirror (lane i <-> 7-i) pairs the two quads.
+__device__ __forceinline__ float sum8_dpp(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  return v;
+}
+
 __device__ __forceinline__ float pick4(const f4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }
@@ -402,10 +411,14 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
         const int q = geo.start[lq] + (s_qy0[lq] + r / s_qw[lq]) * geo.W[lq] + s_qx0[lq] + r % s_qw[lq];
         const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
         const f4 gv4 = ld4(gout + pair * D + 4 * j);
-        gmax = fmaxf(gmax, fmaxf(fmaxf(fabsf(gv4.x), fabsf(gv4.y)), fmaxf(fabsf(gv4.z), fabsf(gv4.w))));
+        const float gm = fmaxf(fmaxf(fabsf(gv4.x), fabsf(gv4.y)), fmaxf(fabsf(gv4.z), fabsf(gv4.w)));
+        // fmaxf drops NaN: fold non-finite values in as +inf so the workgroup takes the atomic path
+        const bool gbad = !(isfinite(gv4.x) && isfinite(gv4.y) && isfinite(gv4.z) && isfinite(gv4.w));
+        gmax = gbad ? INFINITY : fmaxf(gmax, gm);
         for (int k = j; k < L * P; k += 8) {
           const int l = k / P;
-          amax = fmaxf(amax, fabsf(attn[pair * L * P + k]));
+          const float av = attn[pair * L * P + k];
+          amax = isfinite(av) ? fmaxf(amax, fabsf(av)) : INFINITY;
           const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (pair * L * P + k));
           const int H = geo.H[l], W = geo.W[l];
           const float h = xy.y * H - 0.5f, w = xy.x * W - 0.5f;
@@ -434,9 +447,6 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
         atomicMin(&s_bb[l][2], bmin_x[l]); atomicMax(&s_bb[l][3], bmax_x[l]);
       }
     }
-    // NaN compares false in fmaxf chains; record it explicitly so the workgroup falls back to atomics
-    if (gmax != gmax) gmax = INFINITY;
-    if (amax != amax) amax = INFINITY;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       gmax = fmaxf(gmax, __shfl_xor(gmax, o));
@@ -505,6 +515,8 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
       const int H = geo.H[l], W = geo.W[l];
       const int64_t lbase = ((static_cast<int64_t>(n) * S + geo.start[l]) * M + m) * D + 4 * j;
       const int wy0 = s_wy0[l], wx0 = s_wx0[l], wh = s_wh[l], ww = s_ww[l], woff = s_woff[l];
+      float st_a = 0.f, st_l = 0.f;
+      static_assert(P <= 4, "one lane per grad_loc component: 2P <= 8");
 #pragma unroll
       for (int p = 0; p < P; ++p) {
         const int64_t kk = (pair * L + l) * P + p;
@@ -518,19 +530,13 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
         const f4 gw = -k.hy * v1 + k.hy * v2 - k.ly * v3 + k.ly * v4;
         const f4 gh = -k.hx * v1 - k.lx * v2 + k.hx * v3 + k.lx * v4;
         const f4 ta = g * val, tx2 = gw * tg, ty2 = gh * tg;
-        float pa = ta.x + ta.y + ta.z + ta.w;
-        float px = tx2.x + tx2.y + tx2.z + tx2.w;
-        float py = ty2.x + ty2.y + ty2.z + ty2.w;
-#pragma unroll
-        for (int o = 4; o > 0; o >>= 1) {
-          pa += __shfl_xor(pa, o);
-          px += __shfl_xor(px, o);
-          py += __shfl_xor(py, o);
-        }
-        if (j == 0) {
-          gattn[kk] = k.ok ? pa : 0.f;
-          *reinterpret_cast<float2*>(gloc + 2 * kk) = k.ok ? make_float2(W * px, H * py) : make_float2(0.f, 0.f);
-        }
+        const float pa = sum8_dpp(ta.x + ta.y + ta.z + ta.w);
+        const float px = sum8_dpp(tx2.x + tx2.y + tx2.z + tx2.w);
+        const float py = sum8_dpp(ty2.x + ty2.y + ty2.z + ty2.w);
+        // every lane of the group holds the sums: lane p stores grad_attn of point p, lanes 2p, 2p+1
+        // store its grad_loc pair -- one store instruction per level instead of 3 per point
+        if (j == p) st_a = k.ok ? pa : 0.f;
+        if ((j >> 1) == p) st_l = k.ok ? ((j & 1) ? H * py : W * px) : 0.f;
         if (k.ok) {
           const int dy = k.h0 - wy0, dx = k.w0 - wx0;
           const bool iny0 = dy >= 0 && dy < wh, iny1 = dy + 1 >= 0 && dy + 1 < wh;
@@ -561,6 +567,9 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
           }
         }
       }
+      const int64_t kl = (pair * L + l) * P;
+      if (j < P) gattn[kl + j] = st_a;
+      if (j < 2 * P) gloc[2 * kl + j] = st_l;
     }
   }
   __syncthreads();
@@ -683,7 +692,7 @@ bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, c
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   if (total != d.S) return false;
-  const int tile = env_int("M2F_MSDA_TILE", 8);
+  const int tile = env_int("M2F_MSDA_TILE", 12);
   const int threads = env_int("M2F_MSDA_THREADS", 1024);
   geo.nty = (geo.H[fi] + tile - 1) / tile;
   geo.ntx = (geo.W[fi] + tile - 1) / tile;
