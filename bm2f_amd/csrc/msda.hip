@@ -18,6 +18,7 @@
 //     HBM once with row-contiguous atomics; samples falling outside the window take the direct path.
 //   * fp64 and channel counts the fast path does not cover use straightforward generic kernels.
 #include "common.h"
+#include "msda_device.h"
 
 #include <algorithm>
 #include <cmath>
@@ -35,7 +36,7 @@ extern "C" int m2f_abi_version(void) { return 1; }
 
 namespace {
 
-using f4 = float __attribute__((ext_vector_type(4)));
+using namespace m2f_msda;
 
 constexpr int kMaxLevels = 16;
 
@@ -158,47 +159,6 @@ __global__ void __launch_bounds__(BS) msda_bwd_generic(
     }
   }
 }
-
-// ------------------------------------------------------------------------------------------------
-// fp32 fast path: G = D/4 lanes per (n,q,m) pair, float4 per lane.
-// ------------------------------------------------------------------------------------------------
-
-struct Corners {
-  int64_t o1, o2, o3, o4;     // element offsets of the 4 corner rows (clamped to valid rows)
-  int h0, w0;                 // top-left corner (may be -1; meaningful when ok)
-  float w1, w2, w3, w4;       // bilinear weights
-  float hy, ly, hx, lx;       // 1-lh, lh, 1-lw, lw
-  bool c1, c2, c3, c4;        // corner inside the level
-  bool ok;                    // sample inside (-1,H)x(-1,W)
-};
-
-__device__ __forceinline__ Corners make_corners(float locx, float locy, int H, int W, int64_t lbase, int64_t rs) {
-  Corners k;
-  const float h = locy * H - 0.5f;
-  const float w = locx * W - 0.5f;
-  k.ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
-  const float hs = k.ok ? h : -2.f, ws = k.ok ? w : -2.f;   // invalid point: every corner outside
-  const float fh = floorf(hs), fw = floorf(ws);
-  const int h0 = static_cast<int>(fh), w0 = static_cast<int>(fw);
-  k.h0 = h0; k.w0 = w0;
-  k.ly = hs - fh; k.lx = ws - fw;
-  k.hy = 1.f - k.ly; k.hx = 1.f - k.lx;
-  k.w1 = k.hy * k.hx; k.w2 = k.hy * k.lx; k.w3 = k.ly * k.hx; k.w4 = k.ly * k.lx;
-  k.c1 = h0 >= 0 && w0 >= 0;
-  k.c2 = h0 >= 0 && w0 + 1 <= W - 1;
-  k.c3 = h0 + 1 <= H - 1 && w0 >= 0;
-  k.c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
-  // clamp every corner into the level so the (masked) loads never leave it, valid point or not
-  const int y0 = min(max(h0, 0), H - 1), y1 = min(max(h0 + 1, 0), H - 1);
-  const int x0 = min(max(w0, 0), W - 1), x1 = min(max(w0 + 1, 0), W - 1);
-  k.o1 = lbase + (static_cast<int64_t>(y0) * W + x0) * rs;
-  k.o2 = lbase + (static_cast<int64_t>(y0) * W + x1) * rs;
-  k.o3 = lbase + (static_cast<int64_t>(y1) * W + x0) * rs;
-  k.o4 = lbase + (static_cast<int64_t>(y1) * W + x1) * rs;
-  return k;
-}
-
-__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
 template <int D, int PT>
 __global__ void __launch_bounds__(256) msda_fwd_f32_vec(
@@ -325,78 +285,76 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // gfx950's ds_add_f32 runs at ~190 cycles per wave-instruction, ds_add_u64 at ~30 (tools/ubench), and
 // the integer sum is order-independent.  Corners outside the windows go straight to HBM atomics.
 // Phase 3 converts every non-zero element back (x 2^-e) and adds it to HBM with row-contiguous atomics
-// (32 lanes = one 128 B row).  A workgroup whose bound is 0 / non-finite uses direct atomics only.  grad_loc / grad_attn are owned per (q, m) and
-// written once.  Results do not depend on where the windows land, only the atomic traffic does.
+// (32 lanes = one 128 B row).  A workgroup whose bound is 0 / non-finite uses direct atomics only.
+// grad_loc / grad_attn are owned per (q, m) and written once.  Results do not depend on where the
+// windows land, only the atomic traffic does.
+//
+// FUSED = true is the same kernel for the fused front end (see msda_fused_fwd): the samples come from the
+// raw projection (offsets | logits) and the reference points, and the outputs are the gradients w.r.t.
+// that projection: d offset = sum_c dval/dloc * g * a / (W, H) * (W, H) (the level scale cancels) and
+// d logit = a * (d attn - sum_k a_k d attn_k) (softmax backward over the L*P logits of the pair).
 // ------------------------------------------------------------------------------------------------
-constexpr int kTileMaxL = 4;
-
-struct TileGeom {
-  int L;
-  int H[kTileMaxL], W[kTileMaxL], start[kTileMaxL];
-  int nty, ntx;   // tile grid shared by all levels
-  int max_rows;   // LDS window budget (rows of 32 floats)
-  int max_halo;   // windows never extend more than this many pixels past the tile
-  int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no LDS adds, 2 no flush, 4 no spill atomics
+struct TileState {
+  int bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
+  unsigned int gmax, amax;
+  float scale;
+  double unscale;
+  int wy0[kTileMaxL], wx0[kTileMaxL], wh[kTileMaxL], ww[kTileMaxL], woff[kTileMaxL + 1];
+  int qc[kTileMaxL + 1], qy0[kTileMaxL], qx0[kTileMaxL], qw[kTileMaxL];
 };
 
-__device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
+// Fused-front-end inputs (raw projection + reference points).
+struct FrontEnd {
+  const float* proj;   // (N, Lq, ld): offsets (M, L, P, 2) then logits (M, L*P)
+  int ld;
+  const float* ref;    // (N or broadcast, Lq, L, 2) [x, y]
+  int64_t ref_bs;      // batch stride of ref in elements (0 = broadcast)
+};
 
-// Sum over each aligned group of 8 lanes with DPP moves (VALU, no LDS crossbar): xor 1, xor 2 within
-// quads, then row_half_mirror (lane i <-> 7-i) pairs the two quads.
-__device__ __forceinline__ float sum8_dpp(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
-  return v;
+__device__ __forceinline__ int tile_query(const TileState& ts, const TileGeom& geo, int qi) {
+  int lq = 0;
+  while (qi >= ts.qc[lq + 1]) ++lq;
+  const int r = qi - ts.qc[lq];
+  return geo.start[lq] + (ts.qy0[lq] + r / ts.qw[lq]) * geo.W[lq] + ts.qx0[lq] + r % ts.qw[lq];
 }
 
-__device__ __forceinline__ float pick4(const f4& v, int c) {
-  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
-}
-
-template <int P>
+template <int P, int LT, bool FUSED>
 __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
-    const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn,
+    const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
     float* __restrict__ gloc, float* __restrict__ gattn) {
   constexpr int D = 32;
   extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
-  __shared__ int s_bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
-  __shared__ unsigned int s_gmax, s_amax;  // max |grad_out|, max |attn| (float bits, non-negative)
-  __shared__ float s_scale;
-  __shared__ double s_unscale;
-  __shared__ int s_wy0[kTileMaxL], s_wx0[kTileMaxL], s_wh[kTileMaxL], s_ww[kTileMaxL];
-  __shared__ int s_woff[kTileMaxL + 1];
-  __shared__ int s_qc[kTileMaxL + 1];  // prefix sums of per-level query counts
-  __shared__ int s_qy0[kTileMaxL], s_qx0[kTileMaxL], s_qw[kTileMaxL];
+  __shared__ TileState ts;
 
   const int tile = blockIdx.x, m = blockIdx.y, n = blockIdx.z;
   const int ty = tile / geo.ntx, tx = tile - ty * geo.ntx;
-  const int L = geo.L;
+  const int L = LT > 0 ? LT : geo.L;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwaves = blockDim.x >> 6;
   const int j = lane & 7, gq = lane >> 3;
   const int64_t rs = static_cast<int64_t>(M) * D;
+  const int MLP2 = M * L * P * 2;  // fused: column of the first logit in a projection row
 
   if (tid < L) {
     const int l = tid;
     const int y0 = tile_lo(ty, geo.H[l], geo.nty), y1 = tile_lo(ty + 1, geo.H[l], geo.nty);
     const int x0 = tile_lo(tx, geo.W[l], geo.ntx), x1 = tile_lo(tx + 1, geo.W[l], geo.ntx);
-    s_qy0[l] = y0;
-    s_qx0[l] = x0;
-    s_qw[l] = x1 - x0;
-    s_qc[l + 1] = (y1 - y0) * (x1 - x0);
-    s_bb[l][0] = 0x7fffffff; s_bb[l][1] = -1; s_bb[l][2] = 0x7fffffff; s_bb[l][3] = -1;
+    ts.qy0[l] = y0;
+    ts.qx0[l] = x0;
+    ts.qw[l] = x1 - x0;
+    ts.qc[l + 1] = (y1 - y0) * (x1 - x0);
+    ts.bb[l][0] = 0x7fffffff; ts.bb[l][1] = -1; ts.bb[l][2] = 0x7fffffff; ts.bb[l][3] = -1;
   }
-  if (tid == 0) { s_gmax = 0u; s_amax = 0u; }
+  if (tid == 0) { ts.gmax = 0u; ts.amax = 0u; }
   __syncthreads();
   if (tid == 0) {
-    s_qc[0] = 0;
-    for (int l = 0; l < L; ++l) s_qc[l + 1] += s_qc[l];
+    ts.qc[0] = 0;
+    for (int l = 0; l < L; ++l) ts.qc[l + 1] += ts.qc[l];
   }
   __syncthreads();
-  const int Qt = s_qc[L];
+  const int Qt = ts.qc[L];
 
-  // ---- phase 0: bounding boxes of the touched corners -------------------------------------------
+  // ---- phase 0: bounding boxes of the touched corners, and the contribution bound ------------------
   {
     int bmin_y[kTileMaxL], bmax_y[kTileMaxL], bmin_x[kTileMaxL], bmax_x[kTileMaxL];
 #pragma unroll
@@ -405,23 +363,35 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
     for (int base = wid * 8; base < Qt; base += nwaves * 8) {
       const int qi = base + gq;
       if (qi < Qt) {
-        int lq = 0;
-        while (qi >= s_qc[lq + 1]) ++lq;
-        const int r = qi - s_qc[lq];
-        const int q = geo.start[lq] + (s_qy0[lq] + r / s_qw[lq]) * geo.W[lq] + s_qx0[lq] + r % s_qw[lq];
+        const int q = tile_query(ts, geo, qi);
         const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
         const f4 gv4 = ld4(gout + pair * D + 4 * j);
         const float gm = fmaxf(fmaxf(fabsf(gv4.x), fabsf(gv4.y)), fmaxf(fabsf(gv4.z), fabsf(gv4.w)));
         // fmaxf drops NaN: fold non-finite values in as +inf so the workgroup takes the atomic path
         const bool gbad = !(isfinite(gv4.x) && isfinite(gv4.y) && isfinite(gv4.z) && isfinite(gv4.w));
         gmax = gbad ? INFINITY : fmaxf(gmax, gm);
+        const float* prow = FUSED ? fe.proj + (static_cast<int64_t>(n) * S + q) * fe.ld : nullptr;
+        const float* rrow = FUSED ? fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * L * 2 : nullptr;
         for (int k = j; k < L * P; k += 8) {
           const int l = k / P;
-          const float av = attn[pair * L * P + k];
-          amax = isfinite(av) ? fmaxf(amax, fabsf(av)) : INFINITY;
-          const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (pair * L * P + k));
+          float lx, ly;
+          if constexpr (FUSED) {
+            // softmax weights are in [0, 1]: the bound only needs the logits to be finite
+            const float lg = prow[MLP2 + m * L * P + k];
+            amax = isfinite(lg) ? fmaxf(amax, 1.f) : INFINITY;
+            const float2 off = *reinterpret_cast<const float2*>(prow + (m * L * P + k) * 2);
+            const float2 rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
+            lx = rf.x + off.x / static_cast<float>(geo.W[l]);
+            ly = rf.y + off.y / static_cast<float>(geo.H[l]);
+          } else {
+            const float av = attn[pair * L * P + k];
+            amax = isfinite(av) ? fmaxf(amax, fabsf(av)) : INFINITY;
+            const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (pair * L * P + k));
+            lx = xy.x;
+            ly = xy.y;
+          }
           const int H = geo.H[l], W = geo.W[l];
-          const float h = xy.y * H - 0.5f, w = xy.x * W - 0.5f;
+          const float h = ly * H - 0.5f, w = lx * W - 0.5f;
           if (h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W)) {
             const int h0 = static_cast<int>(floorf(h)), w0 = static_cast<int>(floorf(w));
             const int ylo = max(h0, 0), yhi = min(h0 + 1, H - 1), xlo = max(w0, 0), xhi = min(w0 + 1, W - 1);
@@ -443,8 +413,8 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
         bmin_x[l] = min(bmin_x[l], __shfl_xor(bmin_x[l], o)); bmax_x[l] = max(bmax_x[l], __shfl_xor(bmax_x[l], o));
       }
       if (lane == 0 && l < L) {
-        atomicMin(&s_bb[l][0], bmin_y[l]); atomicMax(&s_bb[l][1], bmax_y[l]);
-        atomicMin(&s_bb[l][2], bmin_x[l]); atomicMax(&s_bb[l][3], bmax_x[l]);
+        atomicMin(&ts.bb[l][0], bmin_y[l]); atomicMax(&ts.bb[l][1], bmax_y[l]);
+        atomicMin(&ts.bb[l][2], bmin_x[l]); atomicMax(&ts.bb[l][3], bmax_x[l]);
       }
     }
 #pragma unroll
@@ -453,76 +423,101 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
       amax = fmaxf(amax, __shfl_xor(amax, o));
     }
     if (lane == 0) {
-      atomicMax(&s_gmax, __float_as_uint(gmax));
-      atomicMax(&s_amax, __float_as_uint(amax));
+      atomicMax(&ts.gmax, __float_as_uint(gmax));
+      atomicMax(&ts.amax, __float_as_uint(amax));
     }
   }
   __syncthreads();
 
   // ---- window choice ----------------------------------------------------------------------------
   if (tid == 0) {
-    const float bound = __uint_as_float(s_gmax) * __uint_as_float(s_amax);
+    const float bound = __uint_as_float(ts.gmax) * __uint_as_float(ts.amax);
     const bool use_lds = bound > 1e-30f && bound < 1e30f;  // else: direct atomics (zeros, inf or NaN)
     // at most Qt*L*P contributions reach one element: keep their sum below 2^62
     const int cnt_bits = 32 - __clz(max(Qt * L * P, 1)) + 1;
     const int e = use_lds ? 62 - cnt_bits - static_cast<int>(ceilf(log2f(bound))) : 0;
-    s_scale = use_lds ? ldexpf(1.f, e) : 0.f;
-    s_unscale = use_lds ? ldexp(1.0, -e) : 0.0;
+    ts.scale = use_lds ? ldexpf(1.f, e) : 0.f;
+    ts.unscale = use_lds ? ldexp(1.0, -e) : 0.0;
     for (int halo = use_lds ? geo.max_halo : -1; halo >= 0; --halo) {
       int total = 0;
       for (int l = 0; l < L; ++l) {
         const int H = geo.H[l], W = geo.W[l];
         const int ry0 = max(tile_lo(ty, H, geo.nty) - halo, 0), ry1 = min(tile_lo(ty + 1, H, geo.nty) - 1 + halo, H - 1);
         const int rx0 = max(tile_lo(tx, W, geo.ntx) - halo, 0), rx1 = min(tile_lo(tx + 1, W, geo.ntx) - 1 + halo, W - 1);
-        const int wy0 = max(ry0, s_bb[l][0]), wy1 = min(ry1, s_bb[l][1]);
-        const int wx0 = max(rx0, s_bb[l][2]), wx1 = min(rx1, s_bb[l][3]);
+        const int wy0 = max(ry0, ts.bb[l][0]), wy1 = min(ry1, ts.bb[l][1]);
+        const int wx0 = max(rx0, ts.bb[l][2]), wx1 = min(rx1, ts.bb[l][3]);
         const int wh = wy1 >= wy0 ? wy1 - wy0 + 1 : 0, ww = wx1 >= wx0 ? wx1 - wx0 + 1 : 0;
-        s_wy0[l] = wy0; s_wx0[l] = wx0;
-        s_wh[l] = (wh && ww) ? wh : 0; s_ww[l] = (wh && ww) ? ww : 0;
-        s_woff[l] = total;
-        total += s_wh[l] * s_ww[l];
+        ts.wy0[l] = wy0; ts.wx0[l] = wx0;
+        ts.wh[l] = (wh && ww) ? wh : 0; ts.ww[l] = (wh && ww) ? ww : 0;
+        ts.woff[l] = total;
+        total += ts.wh[l] * ts.ww[l];
       }
-      s_woff[L] = total;
+      ts.woff[L] = total;
       if (total <= geo.max_rows) break;
       if (halo == 0) {  // cannot happen when the budget covers a tile's own footprint; stay correct anyway
-        for (int l = 0; l <= L; ++l) s_woff[l] = 0;
-        for (int l = 0; l < L; ++l) { s_wh[l] = 0; s_ww[l] = 0; }
+        for (int l = 0; l <= L; ++l) ts.woff[l] = 0;
+        for (int l = 0; l < L; ++l) { ts.wh[l] = 0; ts.ww[l] = 0; }
       }
     }
     if (!use_lds) {
-      for (int l = 0; l <= L; ++l) s_woff[l] = 0;
-      for (int l = 0; l < L; ++l) { s_wh[l] = 0; s_ww[l] = 0; s_wy0[l] = 0; s_wx0[l] = 0; }
+      for (int l = 0; l <= L; ++l) ts.woff[l] = 0;
+      for (int l = 0; l < L; ++l) { ts.wh[l] = 0; ts.ww[l] = 0; ts.wy0[l] = 0; ts.wx0[l] = 0; }
     }
   }
   __syncthreads();
-  const int rows_total = s_woff[L];
-  const float fscale = s_scale;
+  const int rows_total = ts.woff[L];
+  const float fscale = ts.scale;
   for (int i = tid; i < rows_total * D; i += blockDim.x) win[i] = 0ull;
   __syncthreads();
 
   // ---- phase 2: gradients; grad_value into the windows --------------------------------------------
+  constexpr int LPS = (LT > 0 ? LT : 1) * P;  // fused path: per-pair arrays, statically indexed
   for (int base = wid * 8; base < Qt; base += nwaves * 8) {
     const int qi = base + gq;
     if (qi >= Qt) continue;  // whole lane group (same qi) idles together
-    int lq = 0;
-    while (qi >= s_qc[lq + 1]) ++lq;
-    const int r = qi - s_qc[lq];
-    const int q = geo.start[lq] + (s_qy0[lq] + r / s_qw[lq]) * geo.W[lq] + s_qx0[lq] + r % s_qw[lq];
+    const int q = tile_query(ts, geo, qi);
     const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
     const f4 g = ld4(gout + pair * D + 4 * j);
     const f4 z = {0.f, 0.f, 0.f, 0.f};
+    // fused: softmax statistics of the pair (every lane), this lane's two grad_attn values, and
+    // sum_k a_k dA_k; a_k itself is recomputed per point (fewer live registers than keeping all L*P)
+    float smx = 0.f, sinv = 0.f, myga0 = 0.f, myga1 = 0.f, dot = 0.f;
+    const float* prow = FUSED ? fe.proj + (static_cast<int64_t>(n) * S + q) * fe.ld : nullptr;
+    const float* rrow = FUSED ? fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * (LT > 0 ? LT : 1) * 2 : nullptr;
+    const float* lgt = FUSED ? prow + MLP2 + m * LPS : nullptr;
+    if constexpr (FUSED) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < LPS; ++k) mx = fmaxf(mx, lgt[k]);
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < LPS; ++k) sum += expf(lgt[k] - mx);
+      smx = mx;
+      sinv = 1.f / sum;
+    }
+#pragma unroll 1
     for (int l = 0; l < L; ++l) {
       const int H = geo.H[l], W = geo.W[l];
       const int64_t lbase = ((static_cast<int64_t>(n) * S + geo.start[l]) * M + m) * D + 4 * j;
-      const int wy0 = s_wy0[l], wx0 = s_wx0[l], wh = s_wh[l], ww = s_ww[l], woff = s_woff[l];
+      const int wy0 = ts.wy0[l], wx0 = ts.wx0[l], wh = ts.wh[l], ww = ts.ww[l], woff = ts.woff[l];
       float st_a = 0.f, st_l = 0.f;
       static_assert(P <= 4, "one lane per grad_loc component: 2P <= 8");
+      float2 rf = make_float2(0.f, 0.f);
+      if constexpr (FUSED) rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
 #pragma unroll
       for (int p = 0; p < P; ++p) {
         const int64_t kk = (pair * L + l) * P + p;
-        const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * kk);
-        const float a = attn[kk];
-        const Corners k = make_corners(xy.x, xy.y, H, W, lbase, rs);
+        float sx, sy, a;
+        if constexpr (FUSED) {
+          const float2 off = *reinterpret_cast<const float2*>(prow + (m * LT * P + l * P + p) * 2);
+          sx = rf.x + off.x / static_cast<float>(W);
+          sy = rf.y + off.y / static_cast<float>(H);
+          a = expf(lgt[l * P + p] - smx) * sinv;
+        } else {
+          const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * kk);
+          sx = xy.x; sy = xy.y; a = attn[kk];
+        }
+        const Corners k = make_corners(sx, sy, H, W, lbase, rs);
         f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
         v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
         const f4 tg = g * a;
@@ -534,9 +529,19 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
         const float px = sum8_dpp(tx2.x + tx2.y + tx2.z + tx2.w);
         const float py = sum8_dpp(ty2.x + ty2.y + ty2.z + ty2.w);
         // every lane of the group holds the sums: lane p stores grad_attn of point p, lanes 2p, 2p+1
-        // store its grad_loc pair -- one store instruction per level instead of 3 per point
-        if (j == p) st_a = k.ok ? pa : 0.f;
-        if ((j >> 1) == p) st_l = k.ok ? ((j & 1) ? H * py : W * px) : 0.f;
+        // store its grad_loc pair -- one store instruction per level instead of 3 per point.
+        // Fused: d offset = d loc / (W, H) = (px, py) exactly (loc = ref + off / (W, H)).
+        if constexpr (FUSED) {
+          const int kp = l * P + p;
+          const float gak = k.ok ? pa : 0.f;
+          dot += a * gak;
+          if (kp == j) myga0 = gak;
+          if (kp == j + 8) myga1 = gak;
+          if ((j >> 1) == p) st_l = k.ok ? ((j & 1) ? py : px) : 0.f;
+        } else {
+          if (j == p) st_a = k.ok ? pa : 0.f;
+          if ((j >> 1) == p) st_l = k.ok ? ((j & 1) ? H * py : W * px) : 0.f;
+        }
         if (k.ok) {
           const int dy = k.h0 - wy0, dx = k.w0 - wx0;
           const bool iny0 = dy >= 0 && dy < wh, iny1 = dy + 1 >= 0 && dy + 1 < wh;
@@ -555,8 +560,8 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const int comp = (e + gq) & 3;  // the 4 lane groups of a half-wave hit disjoint banks
-                const long long fx = __float2ll_rn(pick4(contrib, comp) * fscale);
-                atomicAdd(row + comp, static_cast<unsigned long long>(fx));
+                const long long fxp = __float2ll_rn(pick4(contrib, comp) * fscale);
+                atomicAdd(row + comp, static_cast<unsigned long long>(fxp));
               }
             } else {
               if (geo.ablate & 4) continue;
@@ -567,28 +572,91 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
           }
         }
       }
-      const int64_t kl = (pair * L + l) * P;
-      if (j < P) gattn[kl + j] = st_a;
-      if (j < 2 * P) gloc[2 * kl + j] = st_l;
+      if constexpr (FUSED) {
+        // gproj row: offsets (M, L, P, 2) -> this level's 2P values are contiguous
+        if (j < 2 * P) gloc[(static_cast<int64_t>(n) * S + q) * (MLP2 + MLP2 / 2) + (m * LT + l) * P * 2 + j] = st_l;
+      } else {
+        const int64_t kl = (pair * L + l) * P;
+        if (j < P) gattn[kl + j] = st_a;
+        if (j < 2 * P) gloc[2 * kl + j] = st_l;
+      }
+    }
+    if constexpr (FUSED) {
+      // softmax backward over the pair's L*P logits: d logit_k = a_k (d a_k - sum_i a_i d a_i)
+      float* gl = gloc + (static_cast<int64_t>(n) * S + q) * (MLP2 + MLP2 / 2) + MLP2 + m * LPS;
+      static_assert(LPS <= 16, "two logits per lane of the 8-lane group");
+      if (j < LPS) gl[j] = expf(lgt[j] - smx) * sinv * (myga0 - dot);
+      if (j + 8 < LPS) gl[j + 8] = expf(lgt[j + 8] - smx) * sinv * (myga1 - dot);
     }
   }
   __syncthreads();
 
   // ---- phase 3: flush the windows ----------------------------------------------------------------
   const int flush_end = (geo.ablate & 2) ? 0 : rows_total * D;
-  const double unscale = s_unscale;
+  const double unscale = ts.unscale;
   for (int idx = tid; idx < flush_end; idx += blockDim.x) {
-    const long long fx = static_cast<long long>(win[idx]);
-    if (fx == 0) continue;
-    const float v = static_cast<float>(static_cast<double>(fx) * unscale);
+    const long long fxp = static_cast<long long>(win[idx]);
+    if (fxp == 0) continue;
+    const float v = static_cast<float>(static_cast<double>(fxp) * unscale);
     const int row = idx >> 5, ch = idx & 31;
     int l = 0;
-    while (row >= s_woff[l + 1]) ++l;
-    const int rr = row - s_woff[l];
-    const int y = s_wy0[l] + rr / s_ww[l], x = s_wx0[l] + rr % s_ww[l];
+    while (row >= ts.woff[l + 1]) ++l;
+    const int rr = row - ts.woff[l];
+    const int y = ts.wy0[l] + rr / ts.ww[l], x = ts.wx0[l] + rr % ts.ww[l];
     const int64_t o = ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D + ch;
     atomicAdd(gvalue + o, v);
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused front end, forward: the MSDA forward reading the raw projection (offsets | logits) and the
+// reference points instead of materialised sampling_locations / attention_weights.  Per pair the 8-lane
+// group computes softmax over the L*P logits and loc = ref + offset / (W_l, H_l) exactly as the
+// reference module does (ms_deform_attn.py:102-109), then samples as msda_fwd_f32_vec.
+// ------------------------------------------------------------------------------------------------
+template <int LT>
+__global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ value, FrontEnd fe, TileGeom geo,
+                                                      int64_t npairs, int S, int M, int Lq, float* __restrict__ out) {
+  constexpr int D = 32, G = 8, P = 4, LP = LT * P;
+  const int64_t pair = static_cast<int64_t>(blockIdx.x) * (256 / G) + threadIdx.x / G;
+  if (pair >= npairs) return;
+  const int j = threadIdx.x % G;
+  const int m = static_cast<int>(pair % M);
+  const int64_t nq = pair / M;
+  const int64_t n = nq / Lq;
+  const int q = static_cast<int>(nq - n * Lq);
+  const int64_t rs = static_cast<int64_t>(M) * D;
+  const float* prow = fe.proj + nq * fe.ld;
+  const float* rrow = fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * LT * 2;
+  const float* lg = prow + M * LP * 2 + m * LP;
+  float a[LP];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < LP; ++k) { a[k] = lg[k]; mx = fmaxf(mx, a[k]); }
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < LP; ++k) { a[k] = expf(a[k] - mx); sum += a[k]; }
+  const float inv = 1.f / sum;
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  f4 acc = z;
+#pragma unroll
+  for (int l = 0; l < LT; ++l) {
+    const int H = geo.H[l], W = geo.W[l];
+    const int64_t lbase = ((n * S + geo.start[l]) * M + m) * D + 4 * j;
+    const float2 rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const float2 off = *reinterpret_cast<const float2*>(prow + (m * LP + l * P + p) * 2);
+      const float sx = rf.x + off.x / static_cast<float>(W);
+      const float sy = rf.y + off.y / static_cast<float>(H);
+      const Corners k = make_corners(sx, sy, H, W, lbase, rs);
+      f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
+      v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
+      const f4 val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
+      acc += k.ok ? val * (a[l * P + p] * inv) : z;
+    }
+  }
+  *reinterpret_cast<f4*>(out + pair * D + 4 * j) = acc;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -675,25 +743,25 @@ int env_int(const char* name, int dflt) {
   return (v && *v) ? atoi(v) : dflt;
 }
 
-// Tiled backward when the queries are the flattened pyramid (Lq == S) and the host knows the shapes.
-bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,
-                      const int64_t* host_shapes, float* gv, float* gl, float* ga, hipStream_t st) {
+// Tile geometry for the tiled backward; false when the configuration does not qualify (then the
+// caller uses the untiled kernels).  Lq == S: the queries are the flattened pyramid.
+bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds, int& threads) {
   if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
-  if (env_int("M2F_MSDA_BWD_TILED", 1) == 0) return false;
-  TileGeom geo{};
+  geo = TileGeom{};
   geo.L = d.L;
   int64_t total = 0;
   int fi = 0;
   for (int l = 0; l < d.L; ++l) {
     geo.H[l] = static_cast<int>(host_shapes[2 * l]);
     geo.W[l] = static_cast<int>(host_shapes[2 * l + 1]);
+    if (geo.H[l] <= 0 || geo.W[l] <= 0) return false;
     geo.start[l] = static_cast<int>(total);
     total += static_cast<int64_t>(geo.H[l]) * geo.W[l];
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   if (total != d.S) return false;
   const int tile = env_int("M2F_MSDA_TILE", 12);
-  const int threads = env_int("M2F_MSDA_THREADS", 1024);
+  threads = env_int("M2F_MSDA_THREADS", 1024);
   geo.nty = (geo.H[fi] + tile - 1) / tile;
   geo.ntx = (geo.W[fi] + tile - 1) / tile;
   geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 576);
@@ -706,16 +774,32 @@ bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, c
     own += th * tw;
   }
   if (own > geo.max_rows) return false;
-  const size_t lds = static_cast<size_t>(geo.max_rows) * 32 * sizeof(unsigned long long);
-  if (lds > 150 * 1024 || (threads != 256 && threads != 512 && threads != 1024)) return false;
-  static bool attr = false;
+  lds = static_cast<size_t>(geo.max_rows) * 32 * sizeof(unsigned long long);
+  return lds <= 150 * 1024 && (threads == 256 || threads == 512 || threads == 1024);
+}
+
+template <int P, int LT, bool FUSED>
+void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                  const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
+                  hipStream_t st) {
+  static bool attr = false;  // one flag per instantiation
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<4>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<P, LT, FUSED>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     attr = true;
   }
   const dim3 grid(geo.nty * geo.ntx, d.M, d.N);
-  msda_bwd_f32_tiled<4><<<grid, threads, lds, st>>>(value, loc, attn, gout, geo, d.S, d.M, gv, gl, ga);
+  msda_bwd_f32_tiled<P, LT, FUSED><<<grid, threads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+}
+
+bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,
+                      const int64_t* host_shapes, float* gv, float* gl, float* ga, hipStream_t st) {
+  if (env_int("M2F_MSDA_BWD_TILED", 1) == 0) return false;
+  TileGeom geo;
+  size_t lds;
+  int threads;
+  if (!make_tile_geom(d, host_shapes, geo, lds, threads)) return false;
+  launch_tiled<4, 0, false>(value, loc, attn, FrontEnd{}, gout, geo, lds, threads, d, gv, gl, ga, st);
   return true;
 }
 
@@ -799,4 +883,90 @@ extern "C" int m2f_msda_bwd_f64(const double* value, const int64_t* spatial_shap
   return bwd_impl<double>("m2f_msda_bwd_f64", value, spatial_shapes, level_start_index, sampling_loc,
                           attn_weight, grad_output, d, im2col_step, host_spatial_shapes, grad_value,
                           grad_sampling_loc, grad_attn_weight, static_cast<hipStream_t>(stream));
+}
+
+// ------------------------------------------------------------------------------------------------
+// Fused front end C ABI
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+int fused_check(const char* fn, const float* value, const float* proj, int ld, const float* ref,
+                const int64_t* host_shapes, const Dims& d, TileGeom& geo) {
+  if (!value || !proj || !ref || !host_shapes) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (d.N <= 0 || d.S <= 0 || d.M <= 0 || d.Lq <= 0) return m2f::fail(M2F_EINVAL, "%s: non-positive size", fn);
+  if (d.D != 32 || d.P != 4 || d.L < 1 || d.L > kTileMaxL)
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs channels 32, points 4, 1..4 levels (got D=%d P=%d L=%d)", fn,
+                     d.D, d.P, d.L);
+  if (ld < d.M * d.L * d.P * 3 || (ld & 1))
+    return m2f::fail(M2F_EINVAL, "%s: projection row stride %d (need even, >= %d)", fn, ld, d.M * d.L * d.P * 3);
+  if (!m2f::aligned(value, 16) || !m2f::aligned(proj, 8) || !m2f::aligned(ref, 8))
+    return m2f::fail(M2F_EINVAL, "%s: misaligned input", fn);
+  geo = TileGeom{};
+  geo.L = d.L;
+  int64_t total = 0;
+  for (int l = 0; l < d.L; ++l) {
+    geo.H[l] = static_cast<int>(host_shapes[2 * l]);
+    geo.W[l] = static_cast<int>(host_shapes[2 * l + 1]);
+    if (geo.H[l] <= 0 || geo.W[l] <= 0) return m2f::fail(M2F_EINVAL, "%s: bad level shape", fn);
+    geo.start[l] = static_cast<int>(total);
+    total += static_cast<int64_t>(geo.H[l]) * geo.W[l];
+  }
+  if (total != d.S) return m2f::fail(M2F_EINVAL, "%s: sum of H*W (%lld) != spatial_size (%d)", fn,
+                                     static_cast<long long>(total), d.S);
+  return M2F_OK;
+}
+
+}  // namespace
+
+extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+                                      int64_t ref_batch_stride, const int64_t* host_spatial_shapes, int batch,
+                                      int spatial_size, int num_heads, int channels, int num_levels,
+                                      int num_query, int num_point, float* output, void* stream) {
+  const char* fn = "m2f_msda_fused_fwd_f32";
+  const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
+  TileGeom geo;
+  int rc = fused_check(fn, value, proj, proj_ld, ref, host_spatial_shapes, d, geo);
+  if (rc) return rc;
+  if (!output || !m2f::aligned(output, 16)) return m2f::fail(M2F_EINVAL, "%s: bad output", fn);
+  const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = m2f::ceil_div(d.npairs(), 32);
+  switch (d.L) {
+    case 1: msda_fused_fwd<1><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output); break;
+    case 2: msda_fused_fwd<2><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output); break;
+    case 3: msda_fused_fwd<3><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output); break;
+    default: msda_fused_fwd<4><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output); break;
+  }
+  return m2f::check_launch(fn);
+}
+
+extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+                                      int64_t ref_batch_stride, const int64_t* host_spatial_shapes,
+                                      const float* grad_output, int batch, int spatial_size, int num_heads,
+                                      int channels, int num_levels, int num_query, int num_point,
+                                      float* grad_value, float* grad_proj, void* stream) {
+  const char* fn = "m2f_msda_fused_bwd_f32";
+  const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
+  TileGeom geo0;
+  int rc = fused_check(fn, value, proj, proj_ld, ref, host_spatial_shapes, d, geo0);
+  if (rc) return rc;
+  if (!grad_output || !grad_value || !grad_proj || !m2f::aligned(grad_output, 16) || !m2f::aligned(grad_value, 16))
+    return m2f::fail(M2F_EINVAL, "%s: bad gradient pointer", fn);
+  TileGeom geo;
+  size_t lds;
+  int threads;
+  if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout (num_query == spatial_size)", fn);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const size_t gv_bytes = static_cast<size_t>(d.N) * d.S * d.M * d.D * sizeof(float);
+  hipError_t e = hipMemsetAsync(grad_value, 0, gv_bytes, st);
+  if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
+  const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
+  switch (d.L) {
+    case 1: launch_tiled<4, 1, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st); break;
+    case 2: launch_tiled<4, 2, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st); break;
+    case 3: launch_tiled<4, 3, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st); break;
+    default: launch_tiled<4, 4, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st); break;
+  }
+  return m2f::check_launch(fn);
 }

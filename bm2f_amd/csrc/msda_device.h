@@ -1,0 +1,79 @@
+// Device helpers shared by the MSDA kernels (msda.hip, msda_fused.hip).  Header-only, internal.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace m2f_msda {
+
+using f4 = float __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------
+// fp32 fast path: G = D/4 lanes per (n,q,m) pair, float4 per lane.
+// ------------------------------------------------------------------------------------------------
+
+struct Corners {
+  int64_t o1, o2, o3, o4;     // element offsets of the 4 corner rows (clamped to valid rows)
+  int h0, w0;                 // top-left corner (may be -1; meaningful when ok)
+  float w1, w2, w3, w4;       // bilinear weights
+  float hy, ly, hx, lx;       // 1-lh, lh, 1-lw, lw
+  bool c1, c2, c3, c4;        // corner inside the level
+  bool ok;                    // sample inside (-1,H)x(-1,W)
+};
+
+__device__ __forceinline__ Corners make_corners(float locx, float locy, int H, int W, int64_t lbase, int64_t rs) {
+  Corners k;
+  const float h = locy * H - 0.5f;
+  const float w = locx * W - 0.5f;
+  k.ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
+  const float hs = k.ok ? h : -2.f, ws = k.ok ? w : -2.f;   // invalid point: every corner outside
+  const float fh = floorf(hs), fw = floorf(ws);
+  const int h0 = static_cast<int>(fh), w0 = static_cast<int>(fw);
+  k.h0 = h0; k.w0 = w0;
+  k.ly = hs - fh; k.lx = ws - fw;
+  k.hy = 1.f - k.ly; k.hx = 1.f - k.lx;
+  k.w1 = k.hy * k.hx; k.w2 = k.hy * k.lx; k.w3 = k.ly * k.hx; k.w4 = k.ly * k.lx;
+  k.c1 = h0 >= 0 && w0 >= 0;
+  k.c2 = h0 >= 0 && w0 + 1 <= W - 1;
+  k.c3 = h0 + 1 <= H - 1 && w0 >= 0;
+  k.c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
+  // clamp every corner into the level so the (masked) loads never leave it, valid point or not
+  const int y0 = min(max(h0, 0), H - 1), y1 = min(max(h0 + 1, 0), H - 1);
+  const int x0 = min(max(w0, 0), W - 1), x1 = min(max(w0 + 1, 0), W - 1);
+  k.o1 = lbase + (static_cast<int64_t>(y0) * W + x0) * rs;
+  k.o2 = lbase + (static_cast<int64_t>(y0) * W + x1) * rs;
+  k.o3 = lbase + (static_cast<int64_t>(y1) * W + x0) * rs;
+  k.o4 = lbase + (static_cast<int64_t>(y1) * W + x1) * rs;
+  return k;
+}
+
+__device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
+
+constexpr int kTileMaxL = 4;
+
+struct TileGeom {
+  int L;
+  int H[kTileMaxL], W[kTileMaxL], start[kTileMaxL];
+  int nty, ntx;   // tile grid shared by all levels
+  int max_rows;   // LDS window budget (rows of 32 floats)
+  int max_halo;   // windows never extend more than this many pixels past the tile
+  int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no LDS adds, 2 no flush, 4 no spill atomics
+};
+
+__device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
+
+// Sum over each aligned group of 8 lanes with DPP moves (VALU, no LDS crossbar): xor 1, xor 2 within
+// quads, then row_half_mirror (lane i <-> 7-i) pairs the two quads.
+__device__ __forceinline__ float sum8_dpp(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  return v;
+}
+
+__device__ __forceinline__ float pick4(const f4& v, int c) {
+  return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
+}
+
+
+}  // namespace m2f_msda

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 import warnings
 from typing import Optional, Sequence, Tuple
 
@@ -33,6 +34,7 @@ __all__ = [
     "ms_deform_attn_forward",
     "ms_deform_attn_backward",
     "MSDeformAttnFunction",
+    "MSDeformAttnFusedFunction",
     "MSDeformAttn",
     "attach_host_shapes",
 ]
@@ -163,6 +165,53 @@ class MSDeformAttnFunction(Function):
         return grad_value, None, None, grad_loc, grad_attn, None
 
 
+class MSDeformAttnFusedFunction(Function):
+    """MSDA with the sampling front end fused into the kernels (encoder layout only).
+
+    Inputs: value (N, S, M, 32) fp32; proj (N, S, M*L*P*3) = [sampling offsets (M, L, P, 2) | attention
+    logits (M, L*P)], the raw output of the two projections of ms_deform_attn.py:102-103; ref (N, S, L, 2)
+    reference points.  Computes softmax and loc = ref + offset / (W, H) in-kernel (ms_deform_attn.py:104-109)
+    instead of materialising sampling_locations / attention_weights; the backward returns d value and
+    d proj directly (reference points are constants of the encoder and get no gradient).
+    """
+
+    @staticmethod
+    def forward(ctx, value, proj, ref, host_shapes, n_points):
+        N, S, M, D = value.shape
+        L = len(host_shapes)
+        if ref.stride(-1) != 1 or ref.stride(-2) != 2 or ref.stride(-3) != 2 * L:
+            ref = ref.contiguous()
+        if proj.stride(-1) != 1 or proj.stride(0) != proj.shape[1] * proj.stride(1):
+            proj = proj.contiguous()
+        hs = _host_shape_buffer(host_shapes)
+        out = torch.empty((N, S, M * D), dtype=value.dtype, device=value.device)
+        _native.call("m2f_msda_fused_fwd_f32", _ptr(value), _ptr(proj), proj.stride(1), _ptr(ref), ref.stride(0),
+                     ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, S, n_points, _ptr(out), _stream(value.device))
+        ctx.save_for_backward(value, proj, ref)
+        ctx.meta = (tuple(host_shapes), n_points)
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_out):
+        value, proj, ref = ctx.saved_tensors
+        host_shapes, n_points = ctx.meta
+        N, S, M, D = value.shape
+        L = len(host_shapes)
+        grad_out = grad_out.contiguous()
+        hs = _host_shape_buffer(host_shapes)
+        grad_value = torch.empty_like(value)
+        grad_proj = torch.empty((N, S, M * L * n_points * 3), dtype=proj.dtype, device=proj.device)
+        _native.call("m2f_msda_fused_bwd_f32", _ptr(value), _ptr(proj), proj.stride(1), _ptr(ref), ref.stride(0),
+                     ctypes.cast(hs, ctypes.c_void_p), _ptr(grad_out), N, S, M, D, L, S, n_points, _ptr(grad_value),
+                     _ptr(grad_proj), _stream(value.device))
+        return grad_value, grad_proj, None, None, None
+
+
+def _fused_enabled():
+    return os.environ.get("M2F_MSDA_FUSED", "1") != "0"
+
+
 def _is_power_of_2(n):
     if (not isinstance(n, int)) or (n < 0):
         raise ValueError("invalid input for _is_power_of_2: {} (type: {})".format(n, type(n)))
@@ -230,10 +279,28 @@ class MSDeformAttn(nn.Module):
                 reference_points.shape[-1]))
         return loc, attn
 
+    def _fusable(self, query, reference_points, input_flatten, input_spatial_shapes, input_padding_mask):
+        hs = _host_shapes(input_spatial_shapes)
+        return (_fused_enabled() and hs is not None and input_padding_mask is None and query.is_cuda
+                and query.dtype == torch.float32 and input_flatten.dtype == torch.float32
+                and self.d_model // self.n_heads == 32 and self.n_points == 4 and 1 <= self.n_levels <= 4
+                and len(hs) == self.n_levels and query.shape[1] == input_flatten.shape[1]
+                and reference_points.shape[-1] == 2 and not reference_points.requires_grad
+                and not torch.is_autocast_enabled("cuda"))
+
     def forward(self, query, reference_points, input_flatten, input_spatial_shapes, input_level_start_index,
                 input_padding_mask=None):
         N, Len_q, _ = query.shape
         N, Len_in, _ = input_flatten.shape
+        if self._fusable(query, reference_points, input_flatten, input_spatial_shapes, input_padding_mask):
+            # one GEMM for both sampling projections; softmax + locations happen inside the MSDA kernels
+            value = self.value_proj(input_flatten).view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
+            w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)
+            b = torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0)
+            proj = torch.nn.functional.linear(query, w, b)
+            out = MSDeformAttnFusedFunction.apply(value, proj, reference_points,
+                                                  _host_shapes(input_spatial_shapes), self.n_points)
+            return self.output_proj(out)
         value = self.value_proj(input_flatten)
         if input_padding_mask is not None:
             value = value.masked_fill(input_padding_mask[..., None], float(0))

@@ -89,6 +89,28 @@ int m2f_msda_bwd_f64(const double* value, const int64_t* spatial_shapes, const i
                      const int64_t* host_spatial_shapes,
                      double* grad_value, double* grad_sampling_loc, double* grad_attn_weight, void* stream);
 
+/* MSDA with the sampling front end fused in (encoder layout: num_query == spatial_size, the queries
+ * being the flattened pyramid; channels 32, points 4, 1..4 levels).  Replaces the chain
+ * sampling_offsets / attention_weights Linear -> softmax -> ref + offset / (W, H) -> ms_deform_attn
+ * (ops/modules/ms_deform_attn.py:102-117) after the two projections, so sampling_loc / attn_weight are
+ * never materialised:
+ *   proj  (N, Lq, proj_ld) fp32: columns [0, M*L*P*2) are the offsets (M, L, P, 2), the next M*L*P the
+ *         attention logits (M, L*P) -- the concatenated output of the two Linear layers;
+ *   ref   reference points (N, Lq, L, 2) [x, y], batch stride ref_batch_stride elements (0 = broadcast);
+ *   host_spatial_shapes (L*2 int64, host, required).
+ * The backward writes grad_value (zeroed + accumulated) and grad_proj (N, Lq, M*L*P*3) contiguous:
+ * d offsets and d logits (the softmax backward applied in-kernel).  Reference points get no gradient. */
+int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+                           int64_t ref_batch_stride, const int64_t* host_spatial_shapes, int batch,
+                           int spatial_size, int num_heads, int channels, int num_levels, int num_query,
+                           int num_point, float* output, void* stream);
+
+int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+                           int64_t ref_batch_stride, const int64_t* host_spatial_shapes,
+                           const float* grad_output, int batch, int spatial_size, int num_heads, int channels,
+                           int num_levels, int num_query, int num_point, float* grad_value, float* grad_proj,
+                           void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Masked-attention decoder (mask2former_transformer_decoder.py).
  *

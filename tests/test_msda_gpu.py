@@ -225,3 +225,40 @@ def test_tiled_backward_nonfinite_and_zero_grads(device):
     assert np.array_equal(np.isnan(got), np.isnan(want))
     fin = np.isfinite(want)
     np.testing.assert_allclose(got[fin], want[fin], rtol=1e-3, atol=1e-5 * np.abs(want[fin]).max())
+
+
+@pytest.mark.parametrize("shapes", [[(4, 4), (8, 8), (16, 16)], [(6, 10), (12, 20), (24, 40)], [(5, 7), (10, 13)]])
+def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
+    """MSDeformAttn with the fused front end == the reference-structured path (Linear -> softmax -> loc ->
+    MSDA), outputs and every gradient, on an encoder-shaped call."""
+    from bm2f_amd.msda import MSDeformAttn, attach_host_shapes
+    torch.manual_seed(0)
+    L = len(shapes)
+    m = MSDeformAttn(256, L, 8, 4).to(device)
+    with torch.no_grad():  # make the offsets/logits non-trivial
+        m.sampling_offsets.weight.normal_(0, 0.02)
+        m.attention_weights.weight.normal_(0, 0.05)
+    st = torch.tensor(shapes, dtype=torch.int64, device=device)
+    attach_host_shapes(st, shapes)
+    lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
+    S = int(st.prod(1).sum())
+    N = 2
+    refs = []
+    for h, w in shapes:
+        ys, xs = torch.meshgrid(torch.linspace(0.5, h - 0.5, h), torch.linspace(0.5, w - 0.5, w), indexing="ij")
+        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
+    ref = torch.cat(refs, 0).to(device)[None, :, None, :].expand(N, S, L, 2)
+    src = torch.randn(N, S, 256, device=device)
+    pos = torch.randn(N, S, 256, device=device)
+    outs, grads = [], []
+    for fused in ("1", "0"):
+        monkeypatch.setenv("M2F_MSDA_FUSED", fused)
+        m.zero_grad()
+        x = src.clone().requires_grad_()
+        out = m(x + pos, ref, x, st, lsi)
+        out.backward(torch.ones_like(out) * 0.01 + out.detach() * 0.1)
+        outs.append(out.detach())
+        grads.append([x.grad] + [p.grad.clone() for p in m.parameters()])
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5)
+    for a, b in zip(grads[0], grads[1]):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * max(b.abs().max().item(), 1e-6))
