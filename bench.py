@@ -41,28 +41,35 @@ def log(msg):
 
 
 class KernelTimer:
-    """HIP events around the native calls of a few ops, on the stream they launch on."""
+    """HIP events around every libbm2f entry point, recorded on torch's current stream -- the stream the
+    C ABI launches on -- so each pair brackets exactly that call's kernels (and its memset)."""
+
+    KEYS = {"m2f_msda_fused_bwd_f32": "msda_bwd", "m2f_msda_bwd_f32": "msda_bwd",
+            "m2f_msda_fused_fwd_f32": "msda_fwd", "m2f_msda_fwd_f32": "msda_fwd",
+            "m2f_attn_mask_bits": "attn_mask_bits", "m2f_masked_attn_fwd": "masked_attn_fwd",
+            "m2f_masked_attn_bwd": "masked_attn_bwd"}
 
     def __init__(self):
         self.enabled = False
         self.events = {}
 
-    def wrap(self, mod, name, key):
-        fn = getattr(mod, name)
+    def install(self, native):
+        fn = native.call
         timer = self
 
-        def wrapped(*args, **kwargs):
-            if not timer.enabled:
-                return fn(*args, **kwargs)
+        def wrapped(name, *args):
+            key = timer.KEYS.get(name)
+            if not timer.enabled or key is None:
+                return fn(name, *args)
             s = torch.cuda.Event(enable_timing=True)
             e = torch.cuda.Event(enable_timing=True)
             s.record()
-            out = fn(*args, **kwargs)
+            out = fn(name, *args)
             e.record()
             timer.events.setdefault(key, []).append((s, e))
             return out
 
-        setattr(mod, name, wrapped)
+        native.call = wrapped
 
     def summary(self):
         torch.cuda.synchronize()
@@ -112,19 +119,16 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
 
-    from bm2f_amd import decoder_ops, msda
-    from bm2f_amd.bench_model import MaskFormerR50, default_cfg, make_optimizer, train_step
+    from bm2f_amd import _native
+    from bm2f_amd.bench_model import MaskFormerR50, default_cfg, make_optimizer, train_step, wrap_ddp
 
     timer = KernelTimer()
-    timer.wrap(msda, "ms_deform_attn_backward", "msda_bwd")
-    timer.wrap(msda, "ms_deform_attn_forward", "msda_fwd")
-    timer.wrap(decoder_ops, "attn_mask_bits", "attn_mask_bits")
+    timer.install(_native)
 
     torch.manual_seed(0)
     model = MaskFormerR50(default_cfg(num_queries=args.queries)).to(device)
     if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local], broadcast_buffers=False,
-                                                          gradient_as_bucket_view=True, bucket_cap_mb=64)
+        model = wrap_ddp(model, device)
     opt = make_optimizer(model)
     g = torch.Generator(device=device).manual_seed(1000 + rank)
     images = torch.randn(args.batch, 3, args.res, args.res, device=device, generator=g) * 57.0 + 117.0
@@ -173,7 +177,8 @@ def main():
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": (tr or {}).get("hbm_bytes_per_launch") if tr else None,
-                    "kernel": "MSDA backward (m2f_msda_bwd_f32)", "algorithmic_bytes_per_launch": nbytes,
+                    "kernel": "MSDA backward (m2f_msda_fused_bwd_f32: tiled, LDS fixed-point grad_value)",
+                    "algorithmic_bytes_per_launch": nbytes,
                     "mean_launch_ms": round(bwd["mean_ms"], 4)}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:

@@ -102,21 +102,49 @@ def default_cfg(num_queries=100, num_classes=133):
                       TRANSFORMER_DECODER_NAME="MultiScaleMaskedTransformerDecoder")))
 
 
+class MaskFormerHead(nn.Module):
+    """The reference's head glue (meta_arch/mask_former_head.py:115-132) for the
+    "multi_scale_pixel_decoder" configuration: pixel decoder -> masked-attention decoder."""
+
+    def __init__(self, cfg, input_shape):
+        super().__init__()
+        self.pixel_decoder = MSDeformAttnPixelDecoder(cfg, input_shape)
+        self.predictor = MultiScaleMaskedTransformerDecoder(cfg, cfg.MODEL.SEM_SEG_HEAD.CONVS_DIM, True)
+
+    def forward(self, features, mask=None):
+        mask_features, _, multi_scale = self.pixel_decoder.forward_features(features)
+        return self.predictor(multi_scale, mask_features, mask)
+
+
 class MaskFormerR50(nn.Module):
     def __init__(self, cfg=None):
         super().__init__()
         cfg = cfg or default_cfg()
         self.backbone = ResNet50()
-        self.pixel_decoder = MSDeformAttnPixelDecoder(cfg, self.backbone.output_shape())
-        self.predictor = MultiScaleMaskedTransformerDecoder(cfg, cfg.MODEL.SEM_SEG_HEAD.CONVS_DIM, True)
+        self.sem_seg_head = MaskFormerHead(cfg, self.backbone.output_shape())
         self.register_buffer("pixel_mean", torch.tensor(PIXEL_MEAN).view(-1, 1, 1), False)
         self.register_buffer("pixel_std", torch.tensor(PIXEL_STD).view(-1, 1, 1), False)
 
+    @property
+    def pixel_decoder(self):
+        return self.sem_seg_head.pixel_decoder
+
+    @property
+    def predictor(self):
+        return self.sem_seg_head.predictor
+
     def forward(self, images):
         x = (images - self.pixel_mean) / self.pixel_std
-        features = self.backbone(x)
-        mask_features, _, multi_scale = self.pixel_decoder.forward_features(features)
-        return self.predictor(multi_scale, mask_features)
+        return self.sem_seg_head(self.backbone(x))
+
+
+def wrap_ddp(model, device=None):
+    """Data parallel over the image batch: DDP's bucketed gradient all-reduce (RCCL on ROCm, gloo on
+    CPU) overlapped with the backward -- the path's only cross-GPU exchange."""
+    kw = dict(broadcast_buffers=False, gradient_as_bucket_view=True, bucket_cap_mb=64)
+    if device is not None and device.type == "cuda":
+        kw["device_ids"] = [device.index]
+    return torch.nn.parallel.DistributedDataParallel(model, **kw)
 
 
 def surrogate_loss(out):

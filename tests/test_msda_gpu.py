@@ -205,8 +205,9 @@ def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, threads
     gv2, gl2, ga2 = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
                                                 attn.to(device), gout.to(device), 64)
     torch.testing.assert_close(gv, gv2, rtol=1e-5, atol=1e-5)
-    torch.testing.assert_close(ga, ga2, rtol=1e-5, atol=1e-6)   # channel sums in another order
-    torch.testing.assert_close(gl, gl2, rtol=1e-5, atol=1e-5)
+    # channel sums in another order (DPP tree vs shuffle tree)
+    torch.testing.assert_close(ga, ga2, rtol=1e-4, atol=1e-6 * ga2.abs().max().item())
+    torch.testing.assert_close(gl, gl2, rtol=1e-4, atol=1e-6 * gl2.abs().max().item())
 
 
 def test_tiled_backward_nonfinite_and_zero_grads(device):
