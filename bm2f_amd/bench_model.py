@@ -11,6 +11,7 @@ function, one op fewer per conv).  Optimizer: AdamW + full-model grad-norm clipp
 """
 from __future__ import annotations
 
+import os
 import types
 
 import torch
@@ -116,11 +117,18 @@ class MaskFormerHead(nn.Module):
         return self.predictor(multi_scale, mask_features, mask)
 
 
+def _channels_last_default():
+    return os.environ.get("M2F_CHANNELS_LAST", "0") == "1"
+
+
 class MaskFormerR50(nn.Module):
-    def __init__(self, cfg=None):
+    def __init__(self, cfg=None, channels_last=None):
         super().__init__()
         cfg = cfg or default_cfg()
+        self.channels_last = _channels_last_default() if channels_last is None else channels_last
         self.backbone = ResNet50()
+        if self.channels_last:   # MIOpen's NHWC kernels without the NCHW<->NHWC transposes around each conv
+            self.backbone.to(memory_format=torch.channels_last)
         self.sem_seg_head = MaskFormerHead(cfg, self.backbone.output_shape())
         self.register_buffer("pixel_mean", torch.tensor(PIXEL_MEAN).view(-1, 1, 1), False)
         self.register_buffer("pixel_std", torch.tensor(PIXEL_STD).view(-1, 1, 1), False)
@@ -135,6 +143,8 @@ class MaskFormerR50(nn.Module):
 
     def forward(self, images):
         x = (images - self.pixel_mean) / self.pixel_std
+        if self.channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
         return self.sem_seg_head(self.backbone(x))
 
 
