@@ -4,14 +4,14 @@ Mirrors the reference's training forward (maskformer_model.py:258-320, mask_form
 with the criterion replaced by the sum of means of every head's outputs (the
 Hungarian matcher / weak-supervision losses are outside the hot path).  The backbone is
 detectron2's R50 as configured by the reference (Base-COCO-*.yaml: depth 50, STRIDE_IN_1X1 False,
-FrozenBN, FREEZE_AT 0, res2..res5), written here in plain PyTorch (MIOpen convs, channels-last) since
+FrozenBN, FREEZE_AT 0, res2..res5), written here in plain PyTorch (MIOpen convs, NCHW: channels-last measured 20x slower in the
+backward under MIOPEN_FIND_MODE=FAST) since
 detectron2 / torchvision are absent; FrozenBN is folded into the conv weights on the fly (same
 function, one op fewer per conv).  Optimizer: AdamW + full-model grad-norm clipping
 (train_net.py:185-263, SOLVER: BASE_LR 1e-4, WEIGHT_DECAY 0.05, CLIP_VALUE 0.01).
 """
 from __future__ import annotations
 
-import os
 import types
 
 import torch
@@ -117,18 +117,11 @@ class MaskFormerHead(nn.Module):
         return self.predictor(multi_scale, mask_features, mask)
 
 
-def _channels_last_default():
-    return os.environ.get("M2F_CHANNELS_LAST", "0") == "1"
-
-
 class MaskFormerR50(nn.Module):
-    def __init__(self, cfg=None, channels_last=None):
+    def __init__(self, cfg=None):
         super().__init__()
         cfg = cfg or default_cfg()
-        self.channels_last = _channels_last_default() if channels_last is None else channels_last
         self.backbone = ResNet50()
-        if self.channels_last:   # MIOpen's NHWC kernels without the NCHW<->NHWC transposes around each conv
-            self.backbone.to(memory_format=torch.channels_last)
         self.sem_seg_head = MaskFormerHead(cfg, self.backbone.output_shape())
         self.register_buffer("pixel_mean", torch.tensor(PIXEL_MEAN).view(-1, 1, 1), False)
         self.register_buffer("pixel_std", torch.tensor(PIXEL_STD).view(-1, 1, 1), False)
@@ -143,8 +136,6 @@ class MaskFormerR50(nn.Module):
 
     def forward(self, images):
         x = (images - self.pixel_mean) / self.pixel_std
-        if self.channels_last:
-            x = x.contiguous(memory_format=torch.channels_last)
         return self.sem_seg_head(self.backbone(x))
 
 

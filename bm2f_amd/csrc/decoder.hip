@@ -17,6 +17,7 @@
 #include "common.h"
 
 #include <cmath>
+#include <cstdlib>
 
 namespace {
 
@@ -426,9 +427,11 @@ __global__ void __launch_bounds__(256) mattn_combine_kernel(const float* __restr
 // grid (B*H, nchunks), 256 threads.  Per 64-key block wave w owns key tile w: dK^T and dV^T stay in
 // registers; S = Q K^T is computed with the query on rows so that P and dS (C layout) are directly
 // the B operands of dV^T += dO^T P and dK^T += Q^T dS; dQ^T += K^T dS^T needs dS^T, transposed
-// through a per-wave 16x16 LDS scratch, and is summed over the workgroup's waves with LDS float
-// atomics, then over chunks by a reduce pass (deterministic across chunks).
-template <typename T>
+// through a per-wave 16x16 LDS scratch.  With NTR > 0 (Lq <= 16 * NTR) each wave keeps its dQ^T in
+// registers over the whole chunk and the four waves are summed through LDS once at the end; with
+// NTR == 0 (more queries) each tile's dQ^T goes to LDS float atomics (~190 cycles per wave-instruction
+// on gfx950, the reason for the register path).  Chunks are summed by a reduce pass (deterministic).
+template <typename T, int NTR>
 __global__ void __launch_bounds__(256) mattn_bwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
     const T* __restrict__ out, const T* __restrict__ dout, const float* __restrict__ lse2, int Lq, int Lk, int H,
@@ -484,6 +487,9 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
   }
 
   float* myscr = scr + w * 16 * 17;
+  f4 dqacc[NTR > 0 ? NTR : 1][2];
+#pragma unroll
+  for (int qt = 0; qt < (NTR > 0 ? NTR : 1); ++qt) dqacc[qt][0] = dqacc[qt][1] = f4{0.f, 0.f, 0.f, 0.f};
   for (int kb0 = key_begin; kb0 < key_end; kb0 += 64) {
     __syncthreads();  // previous block's images fully consumed (and the prologue staged)
     f4 kreg[2], vreg[2];
@@ -527,7 +533,8 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
     const int word_sel = koff >> 5, bit = koff & 31;
     const bool key_ok = koff < kvalid;
 
-    for (int qt = 0; qt < NT; ++qt) {
+    // one 16-query tile against this wave's 16 keys; dQ^T contributions accumulate into dqt
+    auto tile = [&](const int qt, f4* dqt) {
       f4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
       if constexpr (k16) {
 #pragma unroll
@@ -583,7 +590,6 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) dst4[j] = myscr[r * 17 + 4 * g + j];  // dS^T[key = 4g+j][q = r]
       __builtin_amdgcn_wave_barrier();
-      f4 dqt[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
       if constexpr (k16) {
         const s4 sb = pack4<T>(dst4[0], dst4[1], dst4[2], dst4[3]);
 #pragma unroll
@@ -599,11 +605,22 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
             dqt[dt] = mma32(Elt<T>::to_f(Ks[(16 * w + 4 * g + i) * RS + dt * 16 + r]), dst4[i], dqt[dt]);
         }
       }
-      // lane holds dQ^T[d = dt*16 + 4g + i][q = qt*16 + r]
+    };
+    if constexpr (NTR > 0) {
+      // dQ stays in registers across every key block of the chunk (Lqp <= 16 * NTR)
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
+      for (int qt = 0; qt < NTR; ++qt)
+        if (qt < NT) tile(qt, dqacc[qt]);
+    } else {
+      for (int qt = 0; qt < NT; ++qt) {
+        f4 dqt[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
+        tile(qt, dqt);
+        // lane holds dQ^T[d = dt*16 + 4g + i][q = qt*16 + r]
 #pragma unroll
-        for (int i = 0; i < 4; ++i) atomicAdd(&dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i], dqt[dt][i]);
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(&dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i], dqt[dt][i]);
+      }
     }
     // write dK, dV for this key tile: lane holds [d = dt*16 + 4g + i][key = koff]
     if (key_ok) {
@@ -618,6 +635,24 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
         } else {
           *reinterpret_cast<f4*>(dk + krow + dt * 16 + 4 * g) = kk;
           *reinterpret_cast<f4*>(dv + krow + dt * 16 + 4 * g) = vv;
+        }
+      }
+    }
+  }
+  if constexpr (NTR > 0) {
+    // sum the four waves' register dQ^T into dqa, one wave at a time (plain LDS read-modify-write)
+    // lane holds dQ^T[d = dt*16 + 4g + i][q = qt*16 + r]
+    for (int ww = 0; ww < 4; ++ww) {
+      __syncthreads();
+      if (w == ww) {
+#pragma unroll
+        for (int qt = 0; qt < NTR; ++qt) {
+          if (qt < NT) {
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i] += dqacc[qt][dt][i];
+          }
         }
       }
     }
@@ -752,15 +787,22 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   const int Lqp = (Lq + 15) / 16 * 16;
   const size_t lds = bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T));
   if (lds > 160 * 1024) return m2f::fail(M2F_EUNSUPPORTED, "%s: %zu B of LDS", fn, lds);
-  static bool attr_set[3] = {false, false, false};
+  // register dQ accumulation up to 128 queries (the decoders' 100 / 200-frame-shared cases use it)
+  static const bool reg_dq = [] {
+    const char* e = std::getenv("M2F_MATTN_DQ_ATOMIC");
+    return !(e && e[0] == '1');
+  }();
+  auto kern = (reg_dq && Lqp <= 128) ? &mattn_bwd_kernel<T, 8> : &mattn_bwd_kernel<T, 0>;
+  static bool attr_set[3][2] = {{false, false}, {false, false}, {false, false}};
   const int ai = std::is_same<T, float>::value ? 0 : (std::is_same<T, __bf16>::value ? 1 : 2);
-  if (!attr_set[ai]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mattn_bwd_kernel<T>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set[ai] = true;
+  const int ki = kern == &mattn_bwd_kernel<T, 8> ? 1 : 0;
+  if (!attr_set[ai][ki]) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    attr_set[ai][ki] = true;
   }
   const dim3 grid(B * H, nch);
-  mattn_bwd_kernel<T><<<grid, 256, lds, st>>>(
+  kern<<<grid, 256, lds, st>>>(
       static_cast<const T*>(q), static_cast<const T*>(k), static_cast<const T*>(v), bits, static_cast<const T*>(out),
       static_cast<const T*>(dout), lse2, Lq, Lk, H, qs, kvs, nw, scale * kLog2e, scale, chunk, Lqp,
       static_cast<T*>(dq), static_cast<T*>(dk), static_cast<T*>(dv), ws);

@@ -62,7 +62,8 @@ def _attn_case(device, B, Lq, Lk, H, dtype, density, seed):
 
 
 @pytest.mark.parametrize("dt,tol", [("f32", 2e-5), ("bf16", 2e-2), ("f16", 4e-3)])
-@pytest.mark.parametrize("B,Lq,Lk", [(2, 100, 1024), (2, 100, 64), (1, 37, 4096 + 17), (3, 200, 300)])
+@pytest.mark.parametrize("B,Lq,Lk", [(2, 100, 1024), (2, 100, 64), (1, 37, 4096 + 17), (3, 200, 300),
+                                     (1, 128, 700), (1, 129, 700)])
 def test_masked_attention(device, dt, tol, B, Lq, Lk):
     from bm2f_amd import decoder_ops
     H = 8

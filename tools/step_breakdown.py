@@ -40,8 +40,6 @@ def main():
         mark("start")
         with torch.autocast("cuda", dtype=amp, enabled=amp is not None):
             xx = (x - model.pixel_mean) / model.pixel_std
-            if model.channels_last:
-                xx = xx.contiguous(memory_format=torch.channels_last)
             feats = model.backbone(xx)
             mark("backbone_fwd")
             mf, _, ms = model.pixel_decoder.forward_features(feats)
