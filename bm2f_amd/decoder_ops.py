@@ -8,6 +8,9 @@
 * :class:`MaskEinsum` — ``einsum("bqc,bchw->bqhw")`` (:442) with the low-precision copy of the mask
   features cast once per decoder forward (the reference re-casts the 1 GB fp32 map on every one of its 10
   calls under AMP); its gradient is returned in the features' dtype, as the reference's cast would.
+* :class:`MaskFeatureFold` — the same einsum for all of a decoder's heads, with the gradient w.r.t. the
+  shared mask features summed by ONE batched GEMM over the stacked heads (K = heads x queries) in the
+  backward, instead of one GEMM + cast + 1 GB fp32 accumulation per head.
 """
 from __future__ import annotations
 
@@ -168,3 +171,97 @@ def mask_einsum(embed, feats, feats_lp=None):
     if feats_lp is None:
         feats_lp = feats
     return MaskEinsum.apply(embed, feats, feats_lp)
+
+
+class _FoldGate(Function):
+    """Identity gate between the mask features and every folded einsum.  Its output is an empty token
+    the einsums take as an input, so autograd runs this backward only after every einsum's backward
+    has run (each stashes its embed and incoming gradient on the fold); it then returns
+    d feats = sum_i E_i^T G_i as one GEMM with fp32 accumulation over K = sum_i Q_i."""
+
+    @staticmethod
+    def forward(ctx, feats, state):
+        ctx.state = state          # not the fold itself: the fold holds this node's output (no cycle)
+        ctx.feats_meta = (feats.shape, feats.dtype)
+        return feats.new_empty(0)
+
+    @staticmethod
+    def backward(ctx, _token_grad):
+        state = ctx.state
+        items, state.items = state.items, []
+        if not items:
+            return None, None
+        shape, dtype = ctx.feats_meta
+        e = items[0][0] if len(items) == 1 else torch.cat([it[0] for it in items], dim=1)   # (B, K, C)
+        g = items[0][1] if len(items) == 1 else torch.cat([it[1] for it in items], dim=1)   # (B, K, N)
+        del items
+        et = e.transpose(1, 2)
+        if g.is_cuda and g.dtype != dtype:
+            df = torch.bmm(et, g, out_dtype=dtype)      # fp32 accumulate, one rounding to the feats' dtype
+        else:
+            df = torch.bmm(et, g).to(dtype)
+        return state.to_feats(df, shape), None
+
+
+class _FoldState:
+    __slots__ = ("items", "to_feats")
+
+    def __init__(self, to_feats):
+        self.items = []
+        self.to_feats = to_feats
+
+
+class _FoldedMaskEinsum(Function):
+    @staticmethod
+    def forward(ctx, embed, token, fold):
+        f = fold.feats_lp                                    # (B, C, N) low-precision copy
+        e = embed.to(f.dtype)
+        out = torch.bmm(e, f)
+        ctx.fold = fold
+        ctx.edtype = embed.dtype
+        ctx.save_for_backward(e)
+        return out.view(fold.out_shape(e.shape[1]))
+
+    @staticmethod
+    def backward(ctx, grad):
+        (e,) = ctx.saved_tensors
+        fold = ctx.fold
+        f = fold.feats_lp
+        B, C, N = f.shape
+        g = grad.to(f.dtype).reshape(B, -1, N)
+        de = torch.bmm(g, f.transpose(1, 2)).to(ctx.edtype) if ctx.needs_input_grad[0] else None
+        tok = None
+        if ctx.needs_input_grad[1]:
+            fold.state.items.append((e, g))
+            tok = g.new_empty(0)
+        return de, tok, None
+
+
+class MaskFeatureFold:
+    """All mask einsums of one decoder forward against one mask-feature map.
+
+    ``feats``     the features as the model holds them (e.g. fp32 (B, C, H, W)); gets the gradient.
+    ``feats_lp``  (B, C, N) copy in the einsum's compute dtype (``feats`` itself when no autocast).
+    ``out_tail``  trailing output dims after (B, Q): (H, W) for images, (T, H, W) for video.
+    ``to_feats``  maps the (B, C, N) gradient back to ``feats``' shape.
+    """
+
+    def __init__(self, feats, feats_lp, out_tail, to_feats):
+        self.feats_lp = feats_lp
+        self.state = _FoldState(to_feats)
+        self._tail = tuple(out_tail)
+        track = feats.requires_grad and torch.is_grad_enabled()
+        self.token = _FoldGate.apply(feats, self.state) if track else None
+
+    def out_shape(self, q):
+        return (self.feats_lp.shape[0], q) + self._tail
+
+    def __call__(self, embed):
+        return _FoldedMaskEinsum.apply(embed, self.token, self)
+
+
+def image_mask_fold(mask_features, mask_features_lp=None):
+    """Fold for ``einsum("bqc,bchw->bqhw")`` (mask2former_transformer_decoder.py:442)."""
+    lp = mask_features if mask_features_lp is None else mask_features_lp
+    B, C, H, W = lp.shape
+    return MaskFeatureFold(mask_features, lp.detach().reshape(B, C, H * W), (H, W), lambda df, shape: df.view(shape))

@@ -22,6 +22,7 @@ from torch.nn import functional as F
 from torch.nn.init import normal_
 
 from .msda import MSDeformAttn, attach_host_shapes
+from .norm_ops import add_layernorm
 from .position_encoding import PositionEmbeddingSine
 from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill, configurable, get_norm
 
@@ -59,14 +60,20 @@ class MSDeformAttnTransformerEncoderLayer(nn.Module):
     def with_pos_embed(tensor, pos):
         return tensor if pos is None else tensor + pos
 
+    def _add_norm(self, src, src2, dropout, norm):
+        # residual + LayerNorm in one kernel when the dropout is an identity (p = 0, as configured, or eval)
+        if dropout.p == 0.0 or not self.training:
+            return add_layernorm(src, src2, norm)
+        return norm(src + dropout(src2))
+
     def forward_ffn(self, src):
         src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
-        return self.norm2(src + self.dropout3(src2))
+        return self._add_norm(src, src2, self.dropout3, self.norm2)
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, padding_mask=None):
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, spatial_shapes,
                               level_start_index, padding_mask)
-        src = self.norm1(src + self.dropout1(src2))
+        src = self._add_norm(src, src2, self.dropout1, self.norm1)
         return self.forward_ffn(src)
 
 

@@ -270,11 +270,12 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         bs = src[0].shape[0]
         query_embed = self.query_embed.weight.unsqueeze(0).expand(bs, -1, -1)
         output = self.query_feat.weight.unsqueeze(0).repeat(bs, 1, 1)
-        mf_lp = self._lowp_features(mask_features)
+        # every head's einsum against one fold: the features' gradient is one GEMM over all heads
+        fold = decoder_ops.image_mask_fold(mask_features, self._lowp_features(mask_features))
 
         predictions_class, predictions_mask = [], []
         outputs_class, outputs_mask, attn_mask = self.forward_prediction_heads(
-            output, mask_features, size_list[0], mf_lp)
+            output, mask_features, size_list[0], fold)
         predictions_class.append(outputs_class)
         predictions_mask.append(outputs_mask)
 
@@ -288,7 +289,7 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
             output = self.transformer_ffn_layers[i](output)
             last = i == self.num_layers - 1
             outputs_class, outputs_mask, attn_mask = self.forward_prediction_heads(
-                output, mask_features, size_list[(i + 1) % self.num_feature_levels], mf_lp, need_mask=not last)
+                output, mask_features, size_list[(i + 1) % self.num_feature_levels], fold, need_mask=not last)
             predictions_class.append(outputs_class)
             predictions_mask.append(outputs_mask)
 
@@ -300,13 +301,15 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
                                               predictions_mask),
         }
 
-    def forward_prediction_heads(self, output, mask_features, attn_mask_target_size, mask_features_lp=None,
-                                 need_mask=True):
-        """output (B, Q, C) -> class logits (B, Q, K+1), mask logits (B, Q, H, W), attention bits."""
+    def forward_prediction_heads(self, output, mask_features, attn_mask_target_size, fold=None, need_mask=True):
+        """output (B, Q, C) -> class logits (B, Q, K+1), mask logits (B, Q, H, W), attention bits.
+        ``fold`` is the forward's :class:`~bm2f_amd.decoder_ops.MaskFeatureFold` (one is made if absent)."""
         decoder_output = self.decoder_norm(output)
         outputs_class = self.class_embed(decoder_output)
         mask_embed = self.mask_embed(decoder_output)
-        outputs_mask = decoder_ops.mask_einsum(mask_embed, mask_features, mask_features_lp)
+        if fold is None:
+            fold = decoder_ops.image_mask_fold(mask_features, self._lowp_features(mask_features))
+        outputs_mask = fold(mask_embed)
         attn_mask = decoder_ops.attn_mask_bits(outputs_mask, attn_mask_target_size) if need_mask else None
         return outputs_class, outputs_mask, attn_mask
 

@@ -9,38 +9,11 @@ from __future__ import annotations
 
 import torch
 from torch import nn
-from torch.autograd import Function
 
 from . import decoder_ops
 from .position_encoding import PositionEmbeddingSine3D
 from .registry import TRANSFORMER_DECODER_REGISTRY, configurable
 from .transformer_decoder import MultiScaleMaskedTransformerDecoder
-
-
-class _VideoMaskEinsum(Function):
-    """out[b,q,t,h,w] = sum_c e[b,q,c] f[b,t,c,h,w]; f_lp is a (B, C, T*H*W) precast copy."""
-
-    @staticmethod
-    def forward(ctx, embed, feats, feats_lp):
-        B, T, C, H, W = feats.shape
-        e = embed.to(feats_lp.dtype)
-        out = torch.bmm(e, feats_lp).view(B, e.shape[1], T, H, W)
-        ctx.save_for_backward(e, feats_lp)
-        ctx.meta = (embed.dtype, feats.dtype, T, H, W)
-        return out
-
-    @staticmethod
-    def backward(ctx, grad):
-        e, f = ctx.saved_tensors
-        edt, fdt, T, H, W = ctx.meta
-        B, C, N = f.shape
-        g = grad.to(f.dtype).reshape(B, -1, N)
-        de = df = None
-        if ctx.needs_input_grad[0]:
-            de = torch.bmm(g, f.transpose(1, 2)).to(edt)
-        if ctx.needs_input_grad[1]:
-            df = torch.bmm(e.transpose(1, 2), g).view(B, C, T, H, W).transpose(1, 2).to(fdt)
-        return de, df, None
 
 
 @TRANSFORMER_DECODER_REGISTRY.register()
@@ -87,10 +60,14 @@ class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder
 
         query_embed = self.query_embed.weight.unsqueeze(0).expand(bs, -1, -1)
         output = self.query_feat.weight.unsqueeze(0).repeat(bs, 1, 1)
-        mf_lp = self._lowp_features(mask_features).transpose(1, 2).reshape(bs, c_m, t * h_m * w_m)
+        mf_lp = self._lowp_features(mask_features).detach().transpose(1, 2).reshape(bs, c_m, t * h_m * w_m)
+        # (B, C, T*H*W) gradient -> (B, T, C, H, W)
+        fold = decoder_ops.MaskFeatureFold(
+            mask_features, mf_lp, (t, h_m, w_m),
+            lambda df, shape: df.view(shape[0], shape[2], shape[1], shape[3], shape[4]).transpose(1, 2))
 
         predictions_class, predictions_mask = [], []
-        outputs_class, outputs_mask, attn_mask = self._heads(output, mask_features, mf_lp, size_list[0])
+        outputs_class, outputs_mask, attn_mask = self._heads(output, fold, size_list[0])
         predictions_class.append(outputs_class)
         predictions_mask.append(outputs_mask)
         for i in range(self.num_layers):
@@ -102,7 +79,7 @@ class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder
                                                                query_pos=query_embed)
             output = self.transformer_ffn_layers[i](output)
             outputs_class, outputs_mask, attn_mask = self._heads(
-                output, mask_features, mf_lp, size_list[(i + 1) % self.num_feature_levels],
+                output, fold, size_list[(i + 1) % self.num_feature_levels],
                 need_mask=i < self.num_layers - 1)
             predictions_class.append(outputs_class)
             predictions_mask.append(outputs_mask)
@@ -114,10 +91,10 @@ class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder
                                               predictions_mask),
         }
 
-    def _heads(self, output, mask_features, mf_lp, size, need_mask=True):
+    def _heads(self, output, fold, size, need_mask=True):
         decoder_output = self.decoder_norm(output)
         outputs_class = self.class_embed(decoder_output)
         mask_embed = self.mask_embed(decoder_output)
-        outputs_mask = _VideoMaskEinsum.apply(mask_embed, mask_features, mf_lp)  # (b, q, t, h, w)
+        outputs_mask = fold(mask_embed)  # (b, q, t, h, w): einsum "bqc,btchw->bqthw" (:449)
         attn_mask = decoder_ops.attn_mask_bits(outputs_mask, size) if need_mask else None
         return outputs_class, outputs_mask, attn_mask

@@ -18,7 +18,8 @@
  *                              fully-masked-row fix (:400)
  *   m2f_masked_attn_*       <- the attention core of nn.MultiheadAttention(attn_mask=bool) used by
  *                              CrossAttentionLayer.forward_post (mask2former_transformer_decoder.py:98-110)
- *   m2f_mask_einsum_*       <- torch.einsum("bqc,bchw->bqhw") (mask2former_transformer_decoder.py:442)
+ *   m2f_add_layernorm_*     <- norm1(src + dropout1(src2)) / norm2(src + dropout3(src2)) of
+ *                              MSDeformAttnTransformerEncoderLayer (pixel_decoder/msdeformattn.py:92-131)
  *
  * Preconditions mirrored from the reference (ms_deform_attn_cuda.cu:33-43, :55-57, :98-124):
  *   batch % min(batch, im2col_step) == 0, else M2F_EINVAL.  All tensors contiguous (checked by the
@@ -147,6 +148,23 @@ int m2f_masked_attn_bwd(int dtype, const void* q, const void* k, const void* v, 
                         int num_queries, int num_keys, int num_heads, int head_dim, int q_row_stride,
                         int kv_row_stride, int mask_words, float scale, void* grad_q, void* grad_k,
                         void* grad_v, void* workspace, int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Residual add + LayerNorm over the last dimension (fp32), the encoder layer's post-norm:
+ *   y = (x - mean) * rstd * gamma + beta,  x = a + b (b may be NULL: plain LayerNorm),
+ *   mean / rstd per row (rows,), rstd = 1 / sqrt(var + eps) with the biased variance.
+ * a, b, y, grad_* are (rows, C) row-major, 16-byte aligned; C % 4 == 0 and C <= 1024.
+ * The backward recomputes x from a and b and returns grad_x (the gradient of both a and b);
+ * grad_gamma / grad_beta (may be NULL) are reduced in a fixed order (deterministic) through a
+ * caller-provided workspace of m2f_add_layernorm_workspace() bytes. */
+int m2f_add_layernorm_workspace(int64_t rows, int C, int64_t* workspace_bytes);
+int m2f_add_layernorm_fwd_f32(const float* a, const float* b, const float* gamma, const float* beta,
+                              int64_t rows, int C, float eps, float* y, float* mean, float* rstd,
+                              void* stream);
+int m2f_add_layernorm_bwd_f32(const float* grad_y, const float* a, const float* b, const float* gamma,
+                              const float* mean, const float* rstd, int64_t rows, int C, float* grad_x,
+                              float* grad_gamma, float* grad_beta, void* workspace,
+                              int64_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }
