@@ -28,7 +28,7 @@ from torch.autograd import Function
 from torch.autograd.function import once_differentiable
 from torch.nn.init import constant_, xavier_uniform_
 
-from . import _native
+from . import _native, linear_ops
 
 __all__ = [
     "ms_deform_attn_forward",
@@ -294,13 +294,16 @@ class MSDeformAttn(nn.Module):
         N, Len_in, _ = input_flatten.shape
         if self._fusable(query, reference_points, input_flatten, input_spatial_shapes, input_padding_mask):
             # one GEMM for both sampling projections; softmax + locations happen inside the MSDA kernels
-            value = self.value_proj(input_flatten).view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
+            # fp32 linears on the MFMA GEMMs (linear_ops): bias in the epilogue, bias gradient in the
+            # weight-gradient GEMM
+            value = linear_ops.linear(input_flatten, self.value_proj).view(
+                N, Len_in, self.n_heads, self.d_model // self.n_heads)
             w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)
             b = torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0)
-            proj = torch.nn.functional.linear(query, w, b)
+            proj = linear_ops.linear_wb(query, w, b)
             out = MSDeformAttnFusedFunction.apply(value, proj, reference_points,
                                                   _host_shapes(input_spatial_shapes), self.n_points)
-            return self.output_proj(out)
+            return linear_ops.linear(out, self.output_proj)
         value = self.value_proj(input_flatten)
         if input_padding_mask is not None:
             value = value.masked_fill(input_padding_mask[..., None], float(0))

@@ -22,6 +22,7 @@ from torch.nn import functional as F
 from torch.nn.init import normal_
 
 from .msda import MSDeformAttn, attach_host_shapes
+from . import linear_ops
 from .norm_ops import add_layernorm
 from .position_encoding import PositionEmbeddingSine
 from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill, configurable, get_norm
@@ -67,7 +68,10 @@ class MSDeformAttnTransformerEncoderLayer(nn.Module):
         return norm(src + dropout(src2))
 
     def forward_ffn(self, src):
-        src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
+        if self.activation is F.relu and (self.dropout2.p == 0.0 or not self.training):
+            src2 = linear_ops.ffn(src, self.linear1, self.linear2)   # bias+ReLU / ReLU mask fused in the GEMMs
+        else:
+            src2 = self.linear2(self.dropout2(self.activation(self.linear1(src))))
         return self._add_norm(src, src2, self.dropout3, self.norm2)
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, padding_mask=None):

@@ -18,6 +18,9 @@
  *                              fully-masked-row fix (:400)
  *   m2f_masked_attn_*       <- the attention core of nn.MultiheadAttention(attn_mask=bool) used by
  *                              CrossAttentionLayer.forward_post (mask2former_transformer_decoder.py:98-110)
+ *   m2f_gemm_f32_*          <- the nn.Linear layers of MSDeformAttnTransformerEncoderLayer (value_proj /
+ *                              sampling_offsets+attention_weights / output_proj, ms_deform_attn.py:59-62;
+ *                              linear1 / linear2 + ReLU, msdeformattn.py:101-106) in fp32 (:314,320)
  *   m2f_add_layernorm_*     <- norm1(src + dropout1(src2)) / norm2(src + dropout3(src2)) of
  *                              MSDeformAttnTransformerEncoderLayer (pixel_decoder/msdeformattn.py:92-131)
  *
@@ -165,6 +168,24 @@ int m2f_add_layernorm_bwd_f32(const float* grad_y, const float* a, const float* 
                               const float* mean, const float* rstd, int64_t rows, int C, float* grad_x,
                               float* grad_gamma, float* grad_beta, void* workspace,
                               int64_t workspace_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Exact-fp32 GEMMs on the f32 MFMA (row-major; lda/ldb/ldc/ldm are row pitches in elements).
+ *
+ * m2f_gemm_f32_nt:  C[M,N] = A[M,K] . B[N,K]^T  (+ bias[N] if bias) then ReLU if relu, or
+ *                   C *= (mask[M,N] > 0) if mask (ReLU backward through the saved activation).
+ *   K, lda, ldb multiples of 4; A, B 16-byte aligned.  Forward of nn.Linear is B = weight;
+ *   its input gradient is B = weight^T (the caller transposes the weight).
+ * m2f_gemm_f32_tn:  C[N1,N2] = A[M,N1]^T . B[M,N2] and, if colsum, colsum[N1] = sum_m A[m,:]
+ *   (weight and bias gradients of nn.Linear: A = grad_out, B = input).  Rows are split over
+ *   workgroups; the fp32 partial slabs are summed in a fixed order (deterministic) through a
+ *   workspace of m2f_gemm_f32_tn_workspace() bytes.  N1, N2, lda, ldb multiples of 4. */
+int m2f_gemm_f32_nt(const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias, int relu,
+                    const float* mask, int64_t ldm, float* C, int64_t ldc, int M, int N, int K, void* stream);
+int m2f_gemm_f32_tn_workspace(int M, int N1, int N2, int64_t* workspace_bytes);
+int m2f_gemm_f32_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                    float* colsum, int M, int N1, int N2, void* workspace, int64_t workspace_bytes,
+                    void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,109 @@
+"""fp32 MFMA GEMMs (csrc/gemm.hip) and the encoder's linear / FFN autograd nodes (linear_ops.py) against
+fp64 torch references of nn.Linear / linear2(relu(linear1(x))) (msdeformattn.py:101-106,
+ms_deform_attn.py:59-62)."""
+import pytest
+import torch
+from torch import nn
+
+from bm2f_amd import linear_ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4, 4), (37, 256, 256), (1000, 288, 256), (129, 1024, 256), (300, 256, 1024),
+                                   (5000, 96, 36), (77, 132, 260)])
+@pytest.mark.parametrize("epi", ["none", "bias", "relu", "bias_relu", "mask", "bias_mask"])
+def test_gemm_nt_vs_fp64(device, M, N, K, epi):
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn(M, K, generator=g).to(device)
+    b = torch.randn(N, K, generator=g).to(device)
+    bias = torch.randn(N, generator=g).to(device) if "bias" in epi else None
+    mask = torch.randn(M, N, generator=g).to(device) if "mask" in epi else None
+    out = linear_ops.gemm_nt(a, b, bias, relu="relu" in epi, mask=mask)
+    ref = a.double() @ b.double().t()
+    if bias is not None:
+        ref = ref + bias.double()
+    if "relu" in epi:
+        ref = ref.clamp_min(0)
+    if mask is not None:
+        ref = torch.where(mask.double() > 0, ref, torch.zeros_like(ref))
+    assert _rel(out, ref) < 2e-6
+
+
+@pytest.mark.parametrize("M,N1,N2", [(1, 4, 4), (31, 256, 256), (4097, 288, 256), (10000, 1024, 256),
+                                     (777, 256, 1024), (33, 132, 8)])
+def test_gemm_tn_vs_fp64(device, M, N1, N2):
+    g = torch.Generator(device="cpu").manual_seed(M * 3 + N1)
+    a = torch.randn(M, N1, generator=g).to(device)
+    b = torch.randn(M, N2, generator=g).to(device)
+    c, cs = linear_ops.gemm_tn(a, b, colsum=True)
+    assert _rel(c, a.double().t() @ b.double()) < 2e-6
+    assert _rel(cs, a.double().sum(0)) < 2e-6
+    c2, cs2 = linear_ops.gemm_tn(a, b, colsum=True)     # fixed-order slab reduce: bitwise repeatable
+    assert torch.equal(c, c2) and torch.equal(cs, cs2)
+
+
+def test_gemm_tn_zero_rows(device):
+    a = torch.empty(0, 8, device=device)
+    b = torch.empty(0, 4, device=device)
+    c, cs = linear_ops.gemm_tn(a, b, colsum=True)
+    assert torch.equal(c, torch.zeros(8, 4, device=device)) and torch.equal(cs, torch.zeros(8, device=device))
+
+
+@pytest.mark.parametrize("shape,cin,cout,relu", [((2, 333, 256), 256, 256, False), ((2, 333, 256), 256, 288, False),
+                                                 ((700, 256), 256, 1024, True), ((3, 50, 1024), 1024, 256, False)])
+def test_linear_autograd_vs_fp64(device, shape, cin, cout, relu):
+    torch.manual_seed(cin + cout)
+    lin = nn.Linear(cin, cout).to(device)
+    x = torch.randn(*shape, device=device, requires_grad=True)
+    y = linear_ops.linear(x, lin, relu=relu)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    xd = x.detach().double().requires_grad_(True)
+    wd = lin.weight.detach().double().requires_grad_(True)
+    bd = lin.bias.detach().double().requires_grad_(True)
+    yd = torch.nn.functional.linear(xd, wd, bd)
+    if relu:
+        yd = yd.clamp_min(0)
+    yd.backward(gy.double())
+    assert _rel(y, yd) < 2e-6
+    assert _rel(x.grad, xd.grad) < 2e-6
+    assert _rel(lin.weight.grad, wd.grad) < 2e-6
+    assert _rel(lin.bias.grad, bd.grad) < 2e-6
+
+
+def test_ffn_autograd_vs_fp64(device):
+    # fp64 reference on the fp32 forward's ReLU pattern: a pre-activation within an ulp of 0 can take the
+    # other branch in fp64, and one flipped unit moves a whole row of grad_h (~1e-3 of the norm here)
+    torch.manual_seed(5)
+    l1, l2 = nn.Linear(256, 1024).to(device), nn.Linear(1024, 256).to(device)
+    x = torch.randn(3, 1111, 256, device=device, requires_grad=True)
+    y = linear_ops.ffn(x, l1, l2)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    x2 = x.detach().reshape(-1, 256)
+    on = linear_ops.gemm_nt(x2, l1.weight.detach(), l1.bias.detach(), relu=True) > 0
+    X, W1, B1, W2 = x2.double(), l1.weight.detach().double(), l1.bias.detach().double(), l2.weight.detach().double()
+    G = gy.reshape(-1, 256).double()
+    H = torch.where(on, X @ W1.t() + B1, torch.zeros((), dtype=torch.float64, device=device))
+    GH = torch.where(on, G @ W2, torch.zeros((), dtype=torch.float64, device=device))
+    assert _rel(y.reshape(-1, 256), H @ W2.t() + l2.bias.detach().double()) < 2e-6
+    want = {"x": GH @ W1, "w1": GH.t() @ X, "b1": GH.sum(0), "w2": G.t() @ H, "b2": G.sum(0)}
+    got = {"x": x.grad.reshape(-1, 256), "w1": l1.weight.grad, "b1": l1.bias.grad, "w2": l2.weight.grad,
+           "b2": l2.bias.grad}
+    errs = {k: _rel(got[k], want[k]) for k in want}
+    assert max(errs.values()) < 2e-6, str(errs)
+
+
+def test_gemm_rejects(device):
+    a = torch.randn(4, 6, device=device)
+    with pytest.raises(RuntimeError, match="multiples of 4"):
+        linear_ops.gemm_nt(a, torch.randn(4, 6, device=device))
+    with pytest.raises(RuntimeError, match="exclusive"):
+        linear_ops.gemm_nt(torch.randn(4, 8, device=device), torch.randn(4, 8, device=device), relu=True,
+                           mask=torch.ones(4, 4, device=device))
