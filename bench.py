@@ -23,11 +23,14 @@ import os
 import sys
 import time
 
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")  # no exhaustive conv search on a fresh box
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+
+from bm2f_amd.miopen_tuning import use_shipped_find_db  # noqa: E402
+
+use_shipped_find_db()  # FAST find mode + the shipped NORMAL-mode find-db (no search on a fresh box)
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402

@@ -11,8 +11,10 @@ import os
 import sys
 import tempfile
 
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bm2f_amd.miopen_tuning import use_shipped_find_db  # noqa: E402
+
+use_shipped_find_db()
 import torch  # noqa: E402
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
@@ -72,6 +74,7 @@ def main():
     ap.add_argument("--rows", type=int, default=45)
     ap.add_argument("--part", default="all")
     ap.add_argument("--attribute", action="store_true")
+    ap.add_argument("--shapes", default="", help="print input shapes of aten ops whose name contains this")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
@@ -91,10 +94,15 @@ def main():
     for _ in range(2):
         step()
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA]) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=bool(a.shapes)) as prof:
         step()
         torch.cuda.synchronize()
     print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=60))
+    if a.shapes:
+        rows = [e for e in prof.key_averages(group_by_input_shape=True) if a.shapes in e.key]
+        rows.sort(key=lambda e: -e.self_device_time_total)
+        for e in rows[:30]:
+            print(f"{e.self_device_time_total / 1e3:8.2f} ms {e.count:4d}  {e.key[:40]:40s} {str(e.input_shapes)[:160]}")
     if a.attribute:
         path = os.path.join(tempfile.gettempdir(), f"op_profile_{os.getpid()}.json")
         prof.export_chrome_trace(path)

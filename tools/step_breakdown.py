@@ -5,8 +5,10 @@ import os
 import sys
 import time
 
-os.environ.setdefault("MIOPEN_FIND_MODE", "FAST")
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bm2f_amd.miopen_tuning import use_shipped_find_db  # noqa: E402
+
+use_shipped_find_db()
 import torch  # noqa: E402
 
 from bm2f_amd.bench_model import MaskFormerR50, make_optimizer, surrogate_loss  # noqa: E402
