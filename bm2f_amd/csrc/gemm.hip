@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -48,7 +49,7 @@ enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4 };
 // NT: block BM x BN, WM x WN waves, each wave TI x TJ MFMA tiles of 32x32; K step 32, LDS double buffer
 // with the next tile's global loads in flight (registers) during the current tile's MFMAs.
 // ---------------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, int DEPTH>
 __global__ void __launch_bounds__(64 * WM * WN) gemm_nt_kernel(const float* __restrict__ A, int64_t lda,
                                                               const float* __restrict__ B, int64_t ldb,
                                                               const float* __restrict__ bias,
@@ -69,31 +70,35 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_nt_kernel(const float* __re
   const int wm = w / WN, wn = w % WN;
   const int li = lane & 31, lh = lane >> 5;
 
-  f4 ra[NA], rb[NB];
-  auto gload = [&](int k0) {
+  // register staging ring of DEPTH tiles (DEPTH 1: the next tile's loads fly during one K step; DEPTH 2:
+  // during two).  Slots are compile-time indices: the K loop is unrolled by DEPTH.
+  f4 ra[DEPTH][NA], rb[DEPTH][NB];
+  auto gload = [&](int k0, auto slot) {
+    constexpr int sl = decltype(slot)::value;
 #pragma unroll
     for (int u = 0; u < NA; ++u) {
       const int idx = tid + u * NT, r = idx >> 3, k = k0 + (idx & 7) * 4;
       const int gm = m0 + r;
-      ra[u] = (gm < M && k < K) ? *reinterpret_cast<const f4*>(A + gm * lda + k) : f4{0.f, 0.f, 0.f, 0.f};
+      ra[sl][u] = (gm < M && k < K) ? *reinterpret_cast<const f4*>(A + gm * lda + k) : f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
       const int idx = tid + u * NT, r = idx >> 3, k = k0 + (idx & 7) * 4;
       const int gn = n0 + r;
-      rb[u] = (gn < N && k < K) ? *reinterpret_cast<const f4*>(B + gn * ldb + k) : f4{0.f, 0.f, 0.f, 0.f};
+      rb[sl][u] = (gn < N && k < K) ? *reinterpret_cast<const f4*>(B + gn * ldb + k) : f4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](int buf, auto slot) {
+    constexpr int sl = decltype(slot)::value;
 #pragma unroll
     for (int u = 0; u < NA; ++u) {
       const int idx = tid + u * NT;
-      *reinterpret_cast<f4*>(&smem[buf][(idx >> 3) * kPitch + (idx & 7) * 4]) = ra[u];
+      *reinterpret_cast<f4*>(&smem[buf][(idx >> 3) * kPitch + (idx & 7) * 4]) = ra[sl][u];
     }
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
       const int idx = tid + u * NT;
-      *reinterpret_cast<f4*>(&smem[buf][(BM + (idx >> 3)) * kPitch + (idx & 7) * 4]) = rb[u];
+      *reinterpret_cast<f4*>(&smem[buf][(BM + (idx >> 3)) * kPitch + (idx & 7) * 4]) = rb[sl][u];
     }
   };
 
@@ -105,13 +110,7 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_nt_kernel(const float* __re
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  const int nk = (K + kBK - 1) / kBK;
-  gload(0);
-  sstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload((kt + 1) * kBK);
+  auto compute = [&](int buf) {
     const float* sa = smem[buf];
     const float* sb = smem[buf] + BM * kPitch;
 #pragma unroll
@@ -130,46 +129,95 @@ __global__ void __launch_bounds__(64 * WM * WN) gemm_nt_kernel(const float* __re
 #pragma unroll
           for (int j = 0; j < TJ; ++j) acc[i][j] = mfma32(fa[i][s], fb[j][s], acc[i][j]);
     }
-    if (kt + 1 < nk) sstore(buf ^ 1);
+  };
+
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, DEPTH - 1>;
+  const int nk = (K + kBK - 1) / kBK;
+  if constexpr (DEPTH == 1) {
+    gload(0, S0{});
+    sstore(0, S0{});
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) gload((kt + 1) * kBK, S0{});
+      compute(buf);
+      if (kt + 1 < nk) sstore(buf ^ 1, S0{});
+      __syncthreads();
+    }
+  } else {
+    // tile t is staged in register slot t & 1 and LDS buffer t & 1
+    gload(0, S0{});
+    if (nk > 1) gload(kBK, S1{});
+    sstore(0, S0{});
+    __syncthreads();
+    auto step = [&](int kt, auto cur, auto nxt) {
+      // cur = slot of tile kt (already in LDS, free for tile kt+2); nxt = slot of tile kt+1
+      if (kt + 2 < nk) gload((kt + 2) * kBK, cur);
+      compute(kt & 1);
+      if (kt + 1 < nk) sstore((kt + 1) & 1, nxt);
+      __syncthreads();
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      step(kt, S0{}, S1{});
+      if (kt + 1 < nk) step(kt + 1, S1{}, S0{});
+    }
   }
 
-  // epilogue: lane holds C[row = (e&3) + 8*(e>>2) + 4*lh][col = li] of each 32x32 tile.  The ReLU-mask
-  // operand of one 32x32 tile is loaded before any of it is applied (16 independent loads in flight).
+  // epilogue through LDS: each wave drops its accumulators into a [BM][BN + 4] fp32 image (lane holds
+  // C[row = (e&3) + 8*(e>>2) + 4*lh][col = li] of each 32x32 tile: 32 consecutive floats per row and
+  // store instruction), then every thread streams whole rows out as float4 with the bias / ReLU / mask
+  // applied -- 4x fewer memory instructions than per-element stores, and the mask read is coalesced.
+  constexpr int CP = BN + 4;
+  static_assert(BM * CP <= 2 * (BM + BN) * kPitch, "C image fits the staging buffers");
+  float* cimg = &smem[0][0];  // the loop ended with a barrier: staging buffers are free
 #pragma unroll
-  for (int j = 0; j < TJ; ++j) {
-    const int col = n0 + wn * TJ * 32 + j * 32 + li;
-    if (col >= N) continue;
-    const float bv = (EPI & kBias) ? bias[col] : 0.f;
+  for (int i = 0; i < TI; ++i)
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
-      const int rbase = m0 + wm * TI * 32 + i * 32 + 4 * lh;
-      float mk[(EPI & kMask) ? 16 : 1];
-      if constexpr ((EPI & kMask) != 0) {
+    for (int j = 0; j < TJ; ++j)
 #pragma unroll
-        for (int e = 0; e < 16; ++e) mk[e] = mask[min(rbase + (e & 3) + 8 * (e >> 2), M - 1) * ldm + col];
+      for (int e = 0; e < 16; ++e)
+        cimg[(wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh) * CP + wn * TJ * 32 + j * 32 + li] = acc[i][j][e];
+  __syncthreads();
+  constexpr int C4 = BN / 4;  // float4 per tile row
+  const bool vec_ok = ((N & 3) == 0) && ((ldc & 3) == 0) && (!(EPI & kMask) || (ldm & 3) == 0);
+  for (int idx = tid; idx < BM * C4; idx += NT) {
+    const int r = idx / C4, c = (idx - r * C4) * 4;
+    const int row = m0 + r, col = n0 + c;
+    if (row >= M || col >= N) continue;
+    f4 v = *reinterpret_cast<const f4*>(&cimg[r * CP + c]);
+    if (vec_ok) {
+      if constexpr ((EPI & kBias) != 0) v += *reinterpret_cast<const f4*>(bias + col);
+      if constexpr ((EPI & kRelu) != 0) {
+        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
       }
+      if constexpr ((EPI & kMask) != 0) {
+        const f4 mk = *reinterpret_cast<const f4*>(mask + row * ldm + col);
+        v.x = mk.x > 0.f ? v.x : 0.f; v.y = mk.y > 0.f ? v.y : 0.f;
+        v.z = mk.z > 0.f ? v.z : 0.f; v.w = mk.w > 0.f ? v.w : 0.f;
+      }
+      *reinterpret_cast<f4*>(C + row * ldc + col) = v;
+    } else {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = rbase + (e & 3) + 8 * (e >> 2);
-        if (row < M) {
-          float v = acc[i][j][e] + bv;
-          if constexpr ((EPI & kRelu) != 0) v = fmaxf(v, 0.f);
-          if constexpr ((EPI & kMask) != 0) v = mk[e] > 0.f ? v : 0.f;
-          C[row * ldc + col] = v;
-        }
+      for (int t = 0; t < 4; ++t) {
+        if (col + t >= N) break;
+        float x = v[t];
+        if constexpr ((EPI & kBias) != 0) x += bias[col + t];
+        if constexpr ((EPI & kRelu) != 0) x = fmaxf(x, 0.f);
+        if constexpr ((EPI & kMask) != 0) x = mask[row * ldm + col + t] > 0.f ? x : 0.f;
+        C[row * ldc + col + t] = x;
       }
     }
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int DEPTH = 1>
 int launch_nt(int epi, const float* A, int64_t lda, const float* B, int64_t ldb, const float* bias,
               const float* mask, int64_t ldm, float* C, int64_t ldc, int M, int N, int K, hipStream_t st) {
   const int64_t nwg = static_cast<int64_t>((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (nwg > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "m2f_gemm_f32_nt: too many tiles");
   const dim3 grid(static_cast<unsigned>(nwg)), block(64 * WM * WN);
-#define M2F_NT(E) gemm_nt_kernel<BM, BN, WM, WN, E><<<grid, block, 0, st>>>(A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K)
+#define M2F_NT(E) gemm_nt_kernel<BM, BN, WM, WN, E, DEPTH><<<grid, block, 0, st>>>(A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K)
   switch (epi) {
     case kNone: M2F_NT(kNone); break;
     case kBias: M2F_NT(kBias); break;
@@ -346,16 +394,15 @@ extern "C" int m2f_gemm_f32_nt(const float* A, int64_t lda, const float* B, int6
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int epi = (bias ? kBias : 0) | (relu ? kRelu : 0) | (mask ? kMask : 0);
   // tile choice: N a multiple of 96 but not 128 (the 288-wide sampling projection) gets 96-wide blocks
-  int cfg = (N % 128 != 0 && N % 96 == 0) ? 4 : 6;
+  int cfg = (N % 128 != 0 && N % 96 == 0) ? 4 : 0;
   if (const char* e = std::getenv("M2F_GEMM_NT_CFG")) cfg = std::atoi(e);
   switch (cfg) {
     case 0: return launch_nt<128, 128, 2, 2>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
-    case 1: return launch_nt<256, 128, 4, 2>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
-    case 2: return launch_nt<128, 256, 2, 4>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
-    case 3: return launch_nt<256, 128, 2, 2>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
     case 4: return launch_nt<128, 96, 4, 1>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
-    case 5: return launch_nt<256, 96, 4, 1>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
     case 6: return launch_nt<128, 128, 4, 1>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
+    case 7: return launch_nt<128, 128, 4, 1, 2>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
+    case 8: return launch_nt<128, 96, 4, 1, 2>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
+    case 9: return launch_nt<128, 128, 2, 2, 2>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
     default: return m2f::fail(M2F_EINVAL, "%s: config %d", fn, cfg);
   }
 }
