@@ -1,0 +1,582 @@
+// fp32 GEMMs on the bf16 matrix cores by exact three-way operand splitting ("x3" GEMMs).
+//
+// The pixel decoder's encoder linears run in fp32 (msdeformattn.py:314,320 force autocast off).  gfx950
+// has no xf32/TF32 and its f32-input MFMA runs at 1/16 of the bf16 rate (MI355X_MICROARCH.md, matrix
+// cores), so the exact-f32 kernels of gemm.hip top out at ~157 TF.  Here every fp32 operand is split
+// into three bf16 planes
+//
+//     x = h + m + l,   h = bf16(x),  m = bf16(x - h),  l = bf16(x - h - m)
+//
+// (each subtraction is exact in fp32; h, m, l carry 8 significant bits each, so x - h - m - l is at most
+// 2^-24 |x|: the split is fp32-exact up to the last bit).  A product is then the six bf16 MFMA terms of
+// order <= 2^-16,
+//
+//     a.b ~ ah.bh + ah.bm + am.bh + ah.bl + am.bm + al.bh
+//
+// dropping am.bl + al.bm + al.bl (<= ~2^-24 |a||b|, the size of one fp32 rounding).  bf16 x bf16 products
+// are exact in fp32 and the MFMA accumulates in fp32, so the result is an fp32-accurate GEMM (error vs an
+// fp64 reference at the level of the exact-f32 MFMA kernels; tests/test_gemm_x3_gpu.py pins it) at
+// 16/6 = 2.7x the f32 MFMA peak.  This is an fp32 GEMM, not a reduced-precision one: no input bit that
+// fp32 keeps is dropped.  Non-finite inputs keep their fp32 meaning (h = x, m = l = 0).
+//
+//   x3_nt:  C[M,N] = A[M,K] . B[N,K]^T  (+ bias[N]) (ReLU | * [mask[M,N] > 0])        forward, dgrad
+//   x3_tn:  C[N1,N2] = A[M,N1]^T . B[M,N2] over M-slabs, reduced in a fixed order;   wgrad (+ bias grad)
+//           optionally colsum[N1] = sum_m A[m,:]
+//
+// Both kernels share one LDS image per stage: for each operand and plane, rows (M/N1 rows for A, N/N2
+// rows for B) of BK = 16 bf16 along k with a 48-byte pitch, so the 32x32x16 operand read of a lane
+// (row l&31, k 8(l>>5) .. +7) is one conflict-free ds_read_b128.  NT stages rows as they lie in memory;
+// TN transposes while splitting (a thread owns one column and 8 consecutive k).  Double-buffered, one
+// barrier per k-step, the next step's global loads in flight during the MFMAs.
+#include "bm2f.h"
+#include "common.h"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+namespace {
+
+using f4 = float __attribute__((ext_vector_type(4)));
+using f16v = float __attribute__((ext_vector_type(16)));
+using bf8 = __bf16 __attribute__((ext_vector_type(8)));
+using bf4 = __bf16 __attribute__((ext_vector_type(4)));
+
+constexpr int kBK = 16;     // k per stage = one 32x32x16 MFMA step
+constexpr int kPitch = 24;  // bf16 per LDS row (48 B): 16 data + 8 pad
+
+__device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ int xcd_remap(int id, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = id % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+}
+
+// x -> (h, m, l); non-finite x keeps h = x (inf / nan propagate as in fp32), m = l = 0
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = static_cast<__bf16>(x);
+  const float r1 = x - static_cast<float>(h);
+  m = static_cast<__bf16>(r1);
+  const float r2 = r1 - static_cast<float>(m);
+  l = static_cast<__bf16>(r2);
+  if (!isfinite(x)) { m = static_cast<__bf16>(0.f); l = static_cast<__bf16>(0.f); }
+}
+
+enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4 };
+
+// One stage's LDS image: [plane][row][kPitch] for ROWS = (A rows + B rows).
+template <int ROWS>
+struct Stage {
+  __bf16 p[3][ROWS * kPitch];
+};
+
+// MFMA core shared by NT and TN: wave (wm, wn) owns TI x TJ tiles of 32x32 at rows wm*TI*32 of the A
+// image and wn*TJ*32 of the B image (B image rows start at BM).
+template <int BM, int TI, int TJ, int ROWS>
+__device__ __forceinline__ void stage_mfma(const Stage<ROWS>& s, int wm, int wn, int li, int lh,
+                                           f16v (&acc)[TI][TJ]) {
+  bf8 fa[3][TI], fb[3][TJ];
+#pragma unroll
+  for (int pl = 0; pl < 3; ++pl) {
+#pragma unroll
+    for (int i = 0; i < TI; ++i)
+      fa[pl][i] = *reinterpret_cast<const bf8*>(&s.p[pl][(wm * TI * 32 + i * 32 + li) * kPitch + lh * 8]);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+      fb[pl][j] = *reinterpret_cast<const bf8*>(&s.p[pl][(BM + wn * TJ * 32 + j * 32 + li) * kPitch + lh * 8]);
+  }
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      f16v c = acc[i][j];
+      c = mfma(fa[2][i], fb[0][j], c);  // al.bh
+      c = mfma(fa[1][i], fb[1][j], c);  // am.bm
+      c = mfma(fa[0][i], fb[2][j], c);  // ah.bl
+      c = mfma(fa[1][i], fb[0][j], c);  // am.bh
+      c = mfma(fa[0][i], fb[1][j], c);  // ah.bm
+      c = mfma(fa[0][i], fb[0][j], c);  // ah.bh
+      acc[i][j] = c;
+    }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// NT: C[M,N] = A[M,K] . B[N,K]^T.
+//
+// B (a weight: <= 1024 x 1024) is split once per call into planes Bs[k16 chunk][plane][NP][16] bf16
+// (x3_presplit; NP = N rounded up to the block width, zero-filled).  Rows are 32 B with the two 16-B
+// halves swapped on rows whose bit 3 is set: with that swizzle the dense image is conflict-free for the
+// 32x32x16 operand read (ds_read_b128 lane groups {0-3,12-15,20-27}, ... cover all 64 banks once), so a
+// chunk is copied to LDS as one linear 16-byte-per-thread stream.
+//
+// A block of NW waves owns NW*32 rows of A and BN columns of C; each wave owns 32 rows.  A wave loads its
+// own A fragments straight from HBM into registers (lane (r, h): row r, k 8h .. 8h+7 of the chunk, two
+// float4), splits them in registers, and multiplies them against the block's B chunk in LDS.  A never
+// touches LDS and is split once.  Pipeline: global loads run two chunks ahead in two register sets (the
+// loop is unrolled by 2 so the sets are static); chunk c+1 is written to the other LDS buffer and split
+// while chunk c's MFMAs drain; one barrier per chunk.
+// Epilogue: each 32x32 accumulator tile goes through a per-wave LDS image and leaves as float4 rows, with
+// the bias / ReLU / ReLU-mask applied on the way (mask reads coalesced like the stores).
+// ---------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int swz(int n) { return (n >> 3) & 1; }  // half swap of B row n
+
+__global__ void __launch_bounds__(256) x3_presplit(const float* __restrict__ B, int64_t ldb, int b_kn, int N, int K,
+                                                   int NP, int nchunks, __bf16* __restrict__ Bs) {
+  const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (t >= static_cast<int64_t>(nchunks) * NP) return;
+  const int c = static_cast<int>(t / NP), n = static_cast<int>(t - static_cast<int64_t>(c) * NP);
+  bf8 pl[3][2];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int k = c * 16 + j;
+    float v = 0.f;
+    if (n < N && k < K) v = b_kn ? B[static_cast<int64_t>(k) * ldb + n] : B[static_cast<int64_t>(n) * ldb + k];
+    __bf16 h, m, l;
+    split3(v, h, m, l);
+    pl[0][j >> 3][j & 7] = h;
+    pl[1][j >> 3][j & 7] = m;
+    pl[2][j >> 3][j & 7] = l;
+  }
+  const int sw = swz(n);
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    bf8* dst = reinterpret_cast<bf8*>(Bs + ((static_cast<int64_t>(c) * 3 + p) * NP + n) * 16);
+    dst[sw] = pl[p][0];
+    dst[sw ^ 1] = pl[p][1];
+  }
+}
+
+template <int BN, int NW, int EPI>
+__global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restrict__ A, int64_t lda,
+                                                       const __bf16* __restrict__ Bs, int NP,
+                                                       const float* __restrict__ bias,
+                                                       const float* __restrict__ mask, int64_t ldm,
+                                                       float* __restrict__ C, int64_t ldc, int M, int N, int K) {
+  constexpr int NT = 64 * NW, BM = 32 * NW, TJ = BN / 32;
+  constexpr int PIECES = 3 * BN * 2;             // 16-byte pieces of one B chunk
+  constexpr int NBL = (PIECES + NT - 1) / NT;    // per thread
+  constexpr int CHUNK = 3 * BN * 16;             // bf16 per LDS chunk image
+  constexpr int EP = 36;                         // epilogue image pitch (floats)
+  constexpr int LDS_B = 2 * CHUNK * 2, LDS_E = NW * 32 * EP * 4;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_B > LDS_E ? LDS_B : LDS_E];
+  __bf16(*sb)[CHUNK] = reinterpret_cast<__bf16(*)[CHUNK]>(smem);
+
+  const int nbn = (N + BN - 1) / BN;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int bm = tile / nbn, bn = tile % nbn;
+  const int m0 = bm * BM, n0 = bn * BN;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int arow = m0 + w * 32 + li;
+  const float* ap = A + static_cast<int64_t>(min(arow, M - 1)) * lda + lh * 8;
+  const bool arow_ok = arow < M;
+  const int nk = (K + kBK - 1) / kBK;
+
+  struct Regs {
+    f4 a[2];
+    bf8 b[NBL];
+  };
+  // branch-free: out-of-range A reads are clamped in-bounds (rows >= M only feed rows never stored; k >= K
+  // is zeroed when the chunk is split, not here, so the load is not waited on early)
+  auto gload = [&](Regs& r, int c) {
+    const int k = c * kBK + lh * 8;
+    const int cc = min(c, nk - 1);
+    r.a[0] = *reinterpret_cast<const f4*>(ap + min(k, K - 4) - lh * 8);
+    r.a[1] = *reinterpret_cast<const f4*>(ap + min(k + 4, K - 4) - lh * 8);
+    const __bf16* bc = Bs + static_cast<int64_t>(cc) * 3 * NP * 16;
+#pragma unroll
+    for (int u = 0; u < NBL; ++u) {
+      const int q = min(tid + u * NT, PIECES - 1);
+      const int p = q / (BN * 2), rem = q - p * BN * 2;
+      r.b[u] = *reinterpret_cast<const bf8*>(bc + (static_cast<int64_t>(p) * NP + n0) * 16 + rem * 8);
+    }
+  };
+  auto bstore = [&](const Regs& r, int buf) {
+#pragma unroll
+    for (int u = 0; u < NBL; ++u) {
+      const int q = tid + u * NT;
+      if (PIECES % NT != 0 && q >= PIECES) continue;
+      *reinterpret_cast<bf8*>(&sb[buf][q * 8]) = r.b[u];
+    }
+  };
+  auto asplit = [&](const Regs& r, int c, bf8 (&fa)[3]) {
+    const int k = c * kBK + lh * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 h, m, l;
+      split3(k + e < K ? r.a[e >> 2][e & 3] : 0.f, h, m, l);
+      fa[0][e] = h; fa[1][e] = m; fa[2][e] = l;
+    }
+  };
+
+  f16v acc[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  // B operand read of tile j: row j*32 + li, half lh (swizzled)
+  const int boff = li * 16 + ((lh ^ swz(li)) * 8);
+  auto chunk_mfma = [&](int buf, const bf8 (&fa)[3]) {
+    const __bf16* base = &sb[buf][0];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int off = j * 32 * 16 + boff;
+      const bf8 bh = *reinterpret_cast<const bf8*>(base + off);
+      const bf8 bmv = *reinterpret_cast<const bf8*>(base + BN * 16 + off);
+      const bf8 bl = *reinterpret_cast<const bf8*>(base + 2 * BN * 16 + off);
+      f16v x = acc[j];
+      x = mfma(fa[2], bh, x);   // al.bh
+      x = mfma(fa[1], bmv, x);  // am.bm
+      x = mfma(fa[0], bl, x);   // ah.bl
+      x = mfma(fa[1], bh, x);   // am.bh
+      x = mfma(fa[0], bmv, x);  // ah.bm
+      x = mfma(fa[0], bh, x);   // ah.bh
+      acc[j] = x;
+    }
+  };
+
+  Regs r0, r1;
+  bf8 fa[3];
+  gload(r0, 0);
+  gload(r1, 1);
+  bstore(r0, 0);
+  asplit(r0, 0, fa);
+  __syncthreads();
+  // iteration c: loads for c+2 into the set chunk c used; chunk c+1 (other set) to LDS + split
+  auto step = [&](int c, Regs& cur, Regs& nxt) {
+    if (c + 2 < nk) gload(cur, c + 2);
+    chunk_mfma(c & 1, fa);
+    if (c + 1 < nk) {
+      bstore(nxt, (c + 1) & 1);
+      asplit(nxt, c + 1, fa);
+    }
+    __syncthreads();
+  };
+  for (int c = 0; c < nk; c += 2) {
+    step(c, r0, r1);
+    if (c + 1 < nk) step(c + 1, r1, r0);
+  }
+
+  // ---- epilogue -----------------------------------------------------------------------------------
+  float* img = reinterpret_cast<float*>(smem) + w * 32 * EP;
+  const int er = lane >> 3, ec = (lane & 7) * 4;  // read-back: 8 rows x 8 float4 per instruction
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+#pragma unroll
+    for (int e = 0; e < 16; ++e) img[((e & 3) + 8 * (e >> 2) + 4 * lh) * EP + li] = acc[j][e];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int col = n0 + j * 32 + ec;
+    f4 bv = {0.f, 0.f, 0.f, 0.f};
+    if constexpr ((EPI & kBias) != 0) {
+      if (col + 3 < N) bv = *reinterpret_cast<const f4*>(bias + col);
+      else
+        for (int t = 0; t < 4; ++t) bv[t] = col + t < N ? bias[col + t] : 0.f;
+    }
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int lr = rr * 8 + er, row = m0 + w * 32 + lr;
+      f4 v = *reinterpret_cast<const f4*>(&img[lr * EP + ec]) + bv;
+      if (row >= M || col >= N) continue;
+      if constexpr ((EPI & kRelu) != 0) {
+        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      }
+      const bool vec = col + 3 < N && ((ldc & 3) == 0) && (!(EPI & kMask) || (ldm & 3) == 0);
+      if (vec) {
+        if constexpr ((EPI & kMask) != 0) {
+          const f4 mk = *reinterpret_cast<const f4*>(mask + static_cast<int64_t>(row) * ldm + col);
+          v.x = mk.x > 0.f ? v.x : 0.f; v.y = mk.y > 0.f ? v.y : 0.f;
+          v.z = mk.z > 0.f ? v.z : 0.f; v.w = mk.w > 0.f ? v.w : 0.f;
+        }
+        *reinterpret_cast<f4*>(C + static_cast<int64_t>(row) * ldc + col) = v;
+      } else {
+        for (int t = 0; t < 4 && col + t < N; ++t) {
+          float x = v[t];
+          if constexpr ((EPI & kMask) != 0) x = mask[static_cast<int64_t>(row) * ldm + col + t] > 0.f ? x : 0.f;
+          C[static_cast<int64_t>(row) * ldc + col + t] = x;
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
+
+template <int BN, int NW>
+int launch_nt(int epi, const float* A, int64_t lda, const __bf16* Bs, int NP, const float* bias, const float* mask,
+              int64_t ldm, float* C, int64_t ldc, int M, int N, int K, hipStream_t st) {
+  constexpr int BM = 32 * NW;
+  const int64_t nwg = static_cast<int64_t>((M + BM - 1) / BM) * ((N + BN - 1) / BN);
+  if (nwg > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "m2f_gemm_f32x3_nt: too many tiles");
+  const dim3 grid(static_cast<unsigned>(nwg)), block(64 * NW);
+#define M2F_X3NT(E) x3_nt_kernel<BN, NW, E><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K)
+  switch (epi) {
+    case kNone: M2F_X3NT(kNone); break;
+    case kBias: M2F_X3NT(kBias); break;
+    case kRelu: M2F_X3NT(kRelu); break;
+    case kBias | kRelu: M2F_X3NT(kBias | kRelu); break;
+    case kMask: M2F_X3NT(kMask); break;
+    case kBias | kMask: M2F_X3NT(kBias | kMask); break;
+    default: return m2f::fail(M2F_EINVAL, "m2f_gemm_f32x3_nt: epilogue %d", epi);
+  }
+#undef M2F_X3NT
+  return m2f::check_launch("m2f_gemm_f32x3_nt");
+}
+
+// padded B width for a block width; every config's NP is a multiple of 384 = lcm(96, 128) so one
+// workspace size serves them all
+int64_t nt_np(int N) { return (N + 383) / 384 * 384; }
+
+int64_t nt_workspace(int N, int K) {
+  const int64_t nchunks = (K + kBK - 1) / kBK;
+  return nchunks * 3 * nt_np(N) * 16 * 2;
+}
+
+// ---------------------------------------------------------------------------------------------------
+// TN split-M: block (tile of C, split) accumulates rows [r0, r1) into slab[split].  Staging transposes:
+// a thread owns one column of A (or B) and 8 consecutive rows (k), so its plane stores are one 16-byte
+// ds_write each (rows 48 B apart: 8 lanes cover the 32 banks).
+// ---------------------------------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(64 * WM * WN) x3_tn_kernel(const float* __restrict__ A, int64_t lda,
+                                                            const float* __restrict__ B, int64_t ldb, int M, int N1,
+                                                            int N2, int rows_per_split, float* __restrict__ slab,
+                                                            float* __restrict__ colsum_slab) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
+  constexpr int ROWS = BM + BN;
+  constexpr int NJOB = (ROWS * 2 + NT - 1) / NT;  // (column, 8-row half) jobs per thread per stage
+  static_assert(TI * WM * 32 == BM && TJ * WN * 32 == BN, "tile");
+  __shared__ Stage<ROWS> st[2];
+
+  const int nb1 = (N1 + BM - 1) / BM, nb2 = (N2 + BN - 1) / BN;
+  const int tiles = nb1 * nb2;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = id / tiles, t = id % tiles;
+  const int b1 = t / nb2, b2 = t % nb2;
+  const int n10 = b1 * BM, n20 = b2 * BN;
+  const int r0 = split * rows_per_split;
+  const int r1 = min(M, r0 + rows_per_split);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w / WN, wn = w % WN;
+  const int li = lane & 31, lh = lane >> 5;
+  const bool do_colsum = colsum_slab != nullptr && b2 == 0;
+
+  // job = half * ROWS + c: image row c (A column n10 + c, or B column n20 + c - BM), k rows 8*half .. +7
+  float rg[NJOB][8];
+  float csum[NJOB];
+#pragma unroll
+  for (int u = 0; u < NJOB; ++u) csum[u] = 0.f;
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < NJOB; ++u) {
+      const int job = tid + u * NT, half = job / ROWS, c = job - half * ROWS;
+      const float* src = nullptr;
+      int64_t ld = 0;
+      if (job < 2 * ROWS) {
+        if (c < BM) {
+          if (n10 + c < N1) { src = A + n10 + c; ld = lda; }
+        } else if (n20 + c - BM < N2) {
+          src = B + n20 + c - BM;
+          ld = ldb;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int r = k0 + half * 8 + e;
+        rg[u][e] = (src && r < r1) ? src[static_cast<int64_t>(r) * ld] : 0.f;
+      }
+    }
+  };
+  auto sstore = [&](Stage<ROWS>& s) {
+#pragma unroll
+    for (int u = 0; u < NJOB; ++u) {
+      const int job = tid + u * NT, half = job / ROWS, c = job - half * ROWS;
+      if (job >= 2 * ROWS) continue;
+      bf8 h, m, l;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        __bf16 a, b, cc;
+        split3(rg[u][e], a, b, cc);
+        h[e] = a; m[e] = b; l[e] = cc;
+      }
+      if (do_colsum && c < BM) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[u] += rg[u][e];
+      }
+      const int off = c * kPitch + half * 8;
+      *reinterpret_cast<bf8*>(&s.p[0][off]) = h;
+      *reinterpret_cast<bf8*>(&s.p[1][off]) = m;
+      *reinterpret_cast<bf8*>(&s.p[2][off]) = l;
+    }
+  };
+
+  f16v acc[TI][TJ];
+#pragma unroll
+  for (int i = 0; i < TI; ++i)
+#pragma unroll
+    for (int j = 0; j < TJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int nk = r1 > r0 ? (r1 - r0 + kBK - 1) / kBK : 0;
+  if (nk > 0) {
+    gload(r0);
+    sstore(st[0]);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(r0 + (kt + 1) * kBK);
+    stage_mfma<BM, TI, TJ, ROWS>(st[kt & 1], wm, wn, li, lh, acc);
+    if (kt + 1 < nk) sstore(st[(kt + 1) & 1]);
+    __syncthreads();
+  }
+
+  float* out = slab + static_cast<int64_t>(split) * N1 * N2;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int col = n20 + wn * TJ * 32 + j * 32 + li;
+    if (col >= N2) continue;
+#pragma unroll
+    for (int i = 0; i < TI; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int row = n10 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        if (row < N1) out[static_cast<int64_t>(row) * N2 + col] = acc[i][j][e];
+      }
+    }
+  }
+  if (do_colsum) {
+    // the two row halves of each A column: half 1 hands its sum to half 0 through LDS (stage 0 is free:
+    // the loop ended with a barrier)
+    float* red = reinterpret_cast<float*>(&st[0].p[0][0]);
+#pragma unroll
+    for (int u = 0; u < NJOB; ++u) {
+      const int job = tid + u * NT, half = job / ROWS, c = job - half * ROWS;
+      if (job < 2 * ROWS && half == 1 && c < BM) red[c] = csum[u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < NJOB; ++u) {
+      const int job = tid + u * NT, half = job / ROWS, c = job - half * ROWS;
+      if (job < 2 * ROWS && half == 0 && c < BM && n10 + c < N1)
+        colsum_slab[static_cast<int64_t>(split) * N1 + n10 + c] = csum[u] + red[c];
+    }
+  }
+}
+
+// out[i] = sum_s slab[s][i] in split order (deterministic); 4 independent chains per thread
+__global__ void __launch_bounds__(256) x3_slab_reduce(const float* __restrict__ slab, int splits, int64_t n,
+                                                      float* __restrict__ out, int64_t ldo, int ncols) {
+  const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i >= n) return;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 3 < splits; s += 4) {
+    a0 += slab[(s + 0) * n + i];
+    a1 += slab[(s + 1) * n + i];
+    a2 += slab[(s + 2) * n + i];
+    a3 += slab[(s + 3) * n + i];
+  }
+  for (; s < splits; ++s) a0 += slab[s * n + i];
+  const int64_t r = i / ncols, c = i % ncols;
+  out[r * ldo + c] = (a0 + a1) + (a2 + a3);
+}
+
+// TN tiles: 128 x 128 (4 waves, 2x2 of 64x64)
+constexpr int kTBM = 128, kTBN = 128, kTWM = 2, kTWN = 2;
+
+int tn_splits(int M, int N1, int N2) {
+  const int tiles = ((N1 + kTBM - 1) / kTBM) * ((N2 + kTBN - 1) / kTBN);
+  int splits = (512 + tiles - 1) / tiles;                       // ~512 blocks: 2 per CU
+  const int max_splits = (M + 8 * kBK - 1) / (8 * kBK);         // >= 8 K-steps per block
+  if (splits > max_splits) splits = max_splits;
+  return splits < 1 ? 1 : splits;
+}
+
+int tn_rows_per_split(int M, int splits) {
+  const int r = (M + splits - 1) / splits;
+  return (r + kBK - 1) / kBK * kBK;
+}
+
+}  // namespace
+
+extern "C" int m2f_gemm_f32x3_nt_workspace(int N, int K, int64_t* workspace_bytes) {
+  if (N <= 0 || K <= 0) return m2f::fail(M2F_EINVAL, "m2f_gemm_f32x3_nt_workspace: N %d K %d", N, K);
+  if (workspace_bytes) *workspace_bytes = nt_workspace(N, K);
+  return m2f::ok();
+}
+
+extern "C" int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
+                                 int relu, const float* mask, int64_t ldm, float* C, int64_t ldc, int M, int N, int K,
+                                 void* workspace, int64_t workspace_bytes, void* stream) {
+  const char* fn = "m2f_gemm_f32x3_nt";
+  if (M < 0 || N <= 0 || K <= 0) return m2f::fail(M2F_EINVAL, "%s: M %d N %d K %d", fn, M, N, K);
+  if (!A || !B || !C) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (K % 4 || lda % 4 || lda < K || ldb < (b_kn ? N : K) || ldc < N || !m2f::aligned(A, 16))
+    return m2f::fail(M2F_EINVAL, "%s: K, lda must be multiples of 4 (lda >= K), A 16-byte aligned", fn);
+  if (mask && ldm < N) return m2f::fail(M2F_EINVAL, "%s: ldm %lld < N", fn, static_cast<long long>(ldm));
+  if (relu && mask) return m2f::fail(M2F_EINVAL, "%s: relu and mask are exclusive", fn);
+  if (!workspace || workspace_bytes < nt_workspace(N, K) || !m2f::aligned(workspace, 16))
+    return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld (16-byte aligned)", fn,
+                     static_cast<long long>(workspace_bytes), static_cast<long long>(nt_workspace(N, K)));
+  if (M == 0) return m2f::ok();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int NP = static_cast<int>(nt_np(N)), nchunks = (K + kBK - 1) / kBK;
+  __bf16* Bs = static_cast<__bf16*>(workspace);
+  x3_presplit<<<m2f::ceil_div(static_cast<int64_t>(nchunks) * NP, 256), 256, 0, st>>>(B, ldb, b_kn, N, K, NP, nchunks, Bs);
+  if (int rc = m2f::check_launch(fn)) return rc;
+  const int epi = (bias ? kBias : 0) | (relu ? kRelu : 0) | (mask ? kMask : 0);
+  // 128-row blocks of 4 waves; 96-wide columns for N = 3 * 96 k (the 288-wide sampling projection), else 128
+  int cfg = (N % 128 != 0 && N % 96 == 0) ? 1 : 0;
+  if (const char* e = std::getenv("M2F_GEMM_X3_NT_CFG")) cfg = std::atoi(e);
+  switch (cfg) {
+    case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K, st);
+    case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K, st);
+    case 2: return launch_nt<256, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K, st);
+    case 3: return launch_nt<128, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K, st);
+    default: return m2f::fail(M2F_EINVAL, "%s: config %d", fn, cfg);
+  }
+}
+
+extern "C" int m2f_gemm_f32x3_tn_workspace(int M, int N1, int N2, int64_t* workspace_bytes) {
+  if (M < 0 || N1 <= 0 || N2 <= 0) return m2f::fail(M2F_EINVAL, "m2f_gemm_f32x3_tn_workspace: bad sizes");
+  const int splits = tn_splits(M, N1, N2);
+  if (workspace_bytes) *workspace_bytes = static_cast<int64_t>(splits) * (static_cast<int64_t>(N1) * N2 + N1) * 4;
+  return m2f::ok();
+}
+
+extern "C" int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                                 float* colsum, int M, int N1, int N2, void* workspace, int64_t workspace_bytes,
+                                 void* stream) {
+  const char* fn = "m2f_gemm_f32x3_tn";
+  if (M < 0 || N1 <= 0 || N2 <= 0) return m2f::fail(M2F_EINVAL, "%s: M %d N1 %d N2 %d", fn, M, N1, N2);
+  if ((M > 0 && (!A || !B)) || !C) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (lda < N1 || ldb < N2 || ldc < N2) return m2f::fail(M2F_EINVAL, "%s: leading dimensions too small", fn);
+  const int splits = tn_splits(M, N1, N2);
+  const int64_t need = static_cast<int64_t>(splits) * (static_cast<int64_t>(N1) * N2 + N1) * 4;
+  if (!workspace || workspace_bytes < need)
+    return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld", fn, static_cast<long long>(workspace_bytes),
+                     static_cast<long long>(need));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* slab = static_cast<float*>(workspace);
+  float* cslab = slab + static_cast<int64_t>(splits) * N1 * N2;
+  const int tiles = ((N1 + kTBM - 1) / kTBM) * ((N2 + kTBN - 1) / kTBN);
+  const int rps = tn_rows_per_split(M, splits);
+  x3_tn_kernel<kTBM, kTBN, kTWM, kTWN><<<splits * tiles, 64 * kTWM * kTWN, 0, st>>>(
+      A, lda, B, ldb, M, N1, N2, rps, slab, colsum ? cslab : nullptr);
+  if (int rc = m2f::check_launch(fn)) return rc;
+  const int64_t n = static_cast<int64_t>(N1) * N2;
+  x3_slab_reduce<<<m2f::ceil_div(n, 256), 256, 0, st>>>(slab, splits, n, C, ldc, N2);
+  if (int rc = m2f::check_launch(fn)) return rc;
+  if (colsum) {
+    x3_slab_reduce<<<m2f::ceil_div(N1, 256), 256, 0, st>>>(cslab, splits, N1, colsum, N1, N1);
+    return m2f::check_launch(fn);
+  }
+  return m2f::ok();
+}

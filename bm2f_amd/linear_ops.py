@@ -22,6 +22,7 @@ every fused-epilogue product and the 256-wide products run on libbm2f.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
@@ -29,6 +30,18 @@ from torch import nn
 from torch.autograd import Function
 
 from . import _native
+
+
+# Which fp32 GEMM engine the encoder linears use: "x3" (bf16 MFMA on exact three-way operand splits,
+# csrc/gemm_x3.hip, fp32-accurate at 2.7x the f32 MFMA rate) or "exact" (f32-input MFMA, csrc/gemm.hip).
+ENGINE = os.environ.get("M2F_F32_GEMM", "x3")
+
+
+def _engine(engine):
+    e = engine or ENGINE
+    if e not in ("x3", "exact"):
+        raise ValueError(f"fp32 GEMM engine {e!r}: expected 'x3' or 'exact'")
+    return e
 
 
 def _stream(t):
@@ -39,29 +52,44 @@ def _c64(v):
     return ctypes.c_int64(int(v))
 
 
-def gemm_nt(a, b, bias=None, relu=False, mask=None, out=None):
-    """C = a @ b.T (+ bias) (ReLU | * (mask > 0)); a (M, K), b (N, K) fp32 row-major (unit column stride)."""
+def gemm_nt(a, b, bias=None, relu=False, mask=None, out=None, engine=None, b_kn=False):
+    """C = a @ b.T (+ bias) (ReLU | * (mask > 0)); a (M, K), b (N, K) fp32 row-major (unit column stride).
+    With ``b_kn`` b is (K, N) and C = a @ b (x3 engine: read in place; exact engine: transposed copy)."""
     M, K = a.shape
-    N = b.shape[0]
+    N = b.shape[1] if b_kn else b.shape[0]
     if out is None:
         out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    msk = (mask.data_ptr() if mask is not None else None, _c64(mask.stride(0) if mask is not None else 0))
+    if _engine(engine) == "x3":
+        wsb = ctypes.c_int64(0)
+        _native.call("m2f_gemm_f32x3_nt_workspace", N, K, ctypes.byref(wsb))
+        ws = torch.empty(max(wsb.value, 16), device=a.device, dtype=torch.uint8)
+        _native.call("m2f_gemm_f32x3_nt", a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)),
+                     1 if b_kn else 0, bias.data_ptr() if bias is not None else None, 1 if relu else 0, *msk,
+                     out.data_ptr(), _c64(out.stride(0)), M, N, K, ws.data_ptr(), _c64(ws.numel()), _stream(a))
+        return out
+    if b_kn:
+        b = b.t().contiguous()
     _native.call("m2f_gemm_f32_nt", a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)),
-                 bias.data_ptr() if bias is not None else None, 1 if relu else 0,
-                 mask.data_ptr() if mask is not None else None, _c64(mask.stride(0) if mask is not None else 0),
+                 bias.data_ptr() if bias is not None else None, 1 if relu else 0, *msk,
                  out.data_ptr(), _c64(out.stride(0)), M, N, K, _stream(a))
     return out
 
 
-def gemm_tn(a, b, colsum=False):
+def gemm_tn(a, b, colsum=False, engine=None):
     """(a.T @ b, a.sum(0) if colsum) for a (M, N1), b (M, N2) fp32 row-major."""
     M, N1 = a.shape
     N2 = b.shape[1]
     out = torch.empty(N1, N2, device=a.device, dtype=torch.float32)
     cs = torch.empty(N1, device=a.device, dtype=torch.float32) if colsum else None
+    # x3 TN on 128-multiples only: its 128x128 tiles waste a third of the work on the 288-wide projection,
+    # where the exact engine is faster (tools/gemm_x3_bench.py)
+    x3 = _engine(engine) == "x3" and (engine == "x3" or (N1 % 128 == 0 and N2 % 128 == 0))
+    fn = "m2f_gemm_f32x3_tn" if x3 else "m2f_gemm_f32_tn"
     wsb = ctypes.c_int64(0)
-    _native.call("m2f_gemm_f32_tn_workspace", M, N1, N2, ctypes.byref(wsb))
+    _native.call(fn + "_workspace", M, N1, N2, ctypes.byref(wsb))
     ws = torch.empty(max(wsb.value, 4), device=a.device, dtype=torch.uint8)
-    _native.call("m2f_gemm_f32_tn", a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)),
+    _native.call(fn, a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)),
                  out.data_ptr(), _c64(N2), cs.data_ptr() if cs is not None else None, M, N1, N2, ws.data_ptr(),
                  _c64(ws.numel()), _stream(a))
     return out, cs
@@ -72,8 +100,9 @@ def _rows(x):
 
 
 def _blas_preferred(k):
-    """Plain (no-epilogue) NT product with reduction depth k: hipBLASLt wins at k >= 1024 or k % 128 != 0."""
-    return k >= 1024 or k % 128 != 0
+    """Plain (no-epilogue) NT product with reduction depth k: with the exact-f32 engine hipBLASLt wins at
+    k >= 1024 or k % 128 != 0; the x3 engine wins everywhere."""
+    return ENGINE == "exact" and (k >= 1024 or k % 128 != 0)
 
 
 def _mm_nt(a, b, bias=None):
@@ -87,7 +116,7 @@ def _mm_nn(a, w):
     """a @ w (an input gradient through weight w of shape (out, in))."""
     if _blas_preferred(a.shape[1]):
         return a @ w
-    return gemm_nt(a, w.t().contiguous())
+    return gemm_nt(a, w, b_kn=True)
 
 
 class LinearF32(Function):
@@ -145,7 +174,7 @@ class FFNF32(Function):
             g = g.contiguous()
         nig = ctx.needs_input_grad
         dw2, db2 = gemm_tn(g, h, colsum=ctx.biases[1] and nig[4]) if (nig[3] or nig[4]) else (None, None)
-        gh = gemm_nt(g, w2.t().contiguous(), mask=h)            # grad_h with the ReLU mask (h > 0)
+        gh = gemm_nt(g, w2, mask=h, b_kn=True)                  # grad_h with the ReLU mask (h > 0)
         del h
         dw1, db1 = gemm_tn(gh, x2, colsum=ctx.biases[0] and nig[2]) if (nig[1] or nig[2]) else (None, None)
         dx = _mm_nn(gh, w1).view(ctx.in_shape) if nig[0] else None

@@ -187,6 +187,24 @@ int m2f_gemm_f32_tn(const float* A, int64_t lda, const float* B, int64_t ldb, fl
                     float* colsum, int M, int N1, int N2, void* workspace, int64_t workspace_bytes,
                     void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * fp32 GEMMs on the bf16 MFMA by exact three-way operand splitting (x = h + m + l, three bf16
+ * planes; the six products of order <= 2^-16 kept: error at the level of one fp32 rounding), at
+ * 2.7x the f32-MFMA peak.  Same math as m2f_gemm_f32_nt / _tn above (fp32 in, fp32 out).
+ * m2f_gemm_f32x3_nt:  B is [N][K] (ldb >= K), or [K][N] when b_kn (ldb >= N; e.g. the weight
+ *   itself for an input gradient, no transpose copy).  Needs m2f_gemm_f32x3_nt_workspace() bytes
+ *   (16-byte aligned) for the split B.  K, lda multiples of 4; A 16-byte aligned.
+ * m2f_gemm_f32x3_tn:  as m2f_gemm_f32_tn, with m2f_gemm_f32x3_tn_workspace() bytes; no alignment
+ *   requirement. */
+int m2f_gemm_f32x3_nt_workspace(int N, int K, int64_t* workspace_bytes);
+int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
+                      int relu, const float* mask, int64_t ldm, float* C, int64_t ldc, int M, int N, int K,
+                      void* workspace, int64_t workspace_bytes, void* stream);
+int m2f_gemm_f32x3_tn_workspace(int M, int N1, int N2, int64_t* workspace_bytes);
+int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
+                      float* colsum, int M, int N1, int N2, void* workspace, int64_t workspace_bytes,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

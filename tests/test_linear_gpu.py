@@ -18,13 +18,15 @@ def _rel(a, b):
 @pytest.mark.parametrize("M,N,K", [(1, 4, 4), (37, 256, 256), (1000, 288, 256), (129, 1024, 256), (300, 256, 1024),
                                    (5000, 96, 36), (77, 132, 260)])
 @pytest.mark.parametrize("epi", ["none", "bias", "relu", "bias_relu", "mask", "bias_mask"])
-def test_gemm_nt_vs_fp64(device, M, N, K, epi):
+@pytest.mark.parametrize("engine,b_kn", [("exact", False), ("x3", False), ("x3", True)])
+def test_gemm_nt_vs_fp64(device, M, N, K, epi, engine, b_kn):
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     a = torch.randn(M, K, generator=g).to(device)
     b = torch.randn(N, K, generator=g).to(device)
     bias = torch.randn(N, generator=g).to(device) if "bias" in epi else None
     mask = torch.randn(M, N, generator=g).to(device) if "mask" in epi else None
-    out = linear_ops.gemm_nt(a, b, bias, relu="relu" in epi, mask=mask)
+    bb = b.t().contiguous() if b_kn else b
+    out = linear_ops.gemm_nt(a, bb, bias, relu="relu" in epi, mask=mask, engine=engine, b_kn=b_kn)
     ref = a.double() @ b.double().t()
     if bias is not None:
         ref = ref + bias.double()
@@ -37,21 +39,23 @@ def test_gemm_nt_vs_fp64(device, M, N, K, epi):
 
 @pytest.mark.parametrize("M,N1,N2", [(1, 4, 4), (31, 256, 256), (4097, 288, 256), (10000, 1024, 256),
                                      (777, 256, 1024), (33, 132, 8)])
-def test_gemm_tn_vs_fp64(device, M, N1, N2):
+@pytest.mark.parametrize("engine", ["exact", "x3"])
+def test_gemm_tn_vs_fp64(device, M, N1, N2, engine):
     g = torch.Generator(device="cpu").manual_seed(M * 3 + N1)
     a = torch.randn(M, N1, generator=g).to(device)
     b = torch.randn(M, N2, generator=g).to(device)
-    c, cs = linear_ops.gemm_tn(a, b, colsum=True)
+    c, cs = linear_ops.gemm_tn(a, b, colsum=True, engine=engine)
     assert _rel(c, a.double().t() @ b.double()) < 2e-6
     assert _rel(cs, a.double().sum(0)) < 2e-6
-    c2, cs2 = linear_ops.gemm_tn(a, b, colsum=True)     # fixed-order slab reduce: bitwise repeatable
+    c2, cs2 = linear_ops.gemm_tn(a, b, colsum=True, engine=engine)     # fixed-order slab reduce: repeatable
     assert torch.equal(c, c2) and torch.equal(cs, cs2)
 
 
-def test_gemm_tn_zero_rows(device):
+@pytest.mark.parametrize("engine", ["exact", "x3"])
+def test_gemm_tn_zero_rows(device, engine):
     a = torch.empty(0, 8, device=device)
     b = torch.empty(0, 4, device=device)
-    c, cs = linear_ops.gemm_tn(a, b, colsum=True)
+    c, cs = linear_ops.gemm_tn(a, b, colsum=True, engine=engine)
     assert torch.equal(c, torch.zeros(8, 4, device=device)) and torch.equal(cs, torch.zeros(8, device=device))
 
 
@@ -107,3 +111,31 @@ def test_gemm_rejects(device):
     with pytest.raises(RuntimeError, match="exclusive"):
         linear_ops.gemm_nt(torch.randn(4, 8, device=device), torch.randn(4, 8, device=device), relu=True,
                            mask=torch.ones(4, 4, device=device))
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 256, 256), (2048, 1024, 256), (2048, 256, 1024)])
+def test_x3_error_matches_exact_fp32(device, M, N, K):
+    """The split-bf16 engine is an fp32 GEMM: its error vs fp64 stays at the exact-f32 MFMA's level,
+    elementwise and in norm, on wide-dynamic-range data (values spanning 2^-20 .. 2^20)."""
+    g = torch.Generator(device="cpu").manual_seed(7)
+    a = torch.randn(M, K, generator=g) * torch.exp2(torch.randint(-20, 21, (M, K), generator=g).float())
+    b = torch.randn(N, K, generator=g)
+    a, b = a.to(device), b.to(device)
+    ref = a.double() @ b.double().t()
+    scale = a.double().abs() @ b.double().abs().t()       # sum |a||b| per element: the fp32 error scale
+    e_x3 = ((linear_ops.gemm_nt(a, b, engine="x3").double() - ref).abs() / scale).max().item()
+    e_ex = ((linear_ops.gemm_nt(a, b, engine="exact").double() - ref).abs() / scale).max().item()
+    assert e_x3 < 4 * 2.0 ** -24 * K ** 0.5 + 2 * e_ex, (e_x3, e_ex)
+
+
+def test_x3_nonfinite_inputs_propagate(device):
+    """A non-finite input gives non-finite outputs exactly where fp32 does.  (An inf can come out as a
+    NaN: inf times the split planes of one finite operand can meet opposite signs.)"""
+    a = torch.randn(64, 32, device=device)
+    b = torch.randn(16, 32, device=device)
+    a[3, 5] = float("inf")
+    a[7, 1] = float("nan")
+    for eng in ("x3", "exact"):
+        c = linear_ops.gemm_nt(a, b, engine=eng)
+        ref = a @ b.t()
+        assert torch.equal(torch.isfinite(c), torch.isfinite(ref))
