@@ -277,17 +277,24 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 //
 // Workgroup = (spatial tile, head m, image n).  A tile is the same normalised rectangle on every level
 // (level l's tile ty spans rows [ty*H_l/nty, (ty+1)*H_l/nty)), so its queries at every level sample the
-// same neighbourhood.  Phase 0 takes the bounding box of the corners the tile's samples touch per level;
-// the window = that box clipped to the tile +- halo (halo shrunk until all windows fit the LDS budget).
-// Phase 2 accumulates grad_value corner rows into the LDS windows as exact fixed point: every
-// contribution w*g*a is bounded by B = max|g| * max|a| over the workgroup (phase 0), scaled by 2^e with
-// 2^e * B * (contributions per element <= Qt*L*P) < 2^62 (no int64 overflow) and added with ds_add_u64.
-// gfx950's ds_add_f32 runs at ~190 cycles per wave-instruction, ds_add_u64 at ~30 (tools/ubench), and
-// the integer sum is order-independent.  Corners outside the windows go straight to HBM atomics.
-// Phase 3 converts every non-zero element back (x 2^-e) and adds it to HBM with row-contiguous atomics
-// (32 lanes = one 128 B row).  A workgroup whose bound is 0 / non-finite uses direct atomics only.
-// grad_loc / grad_attn are owned per (q, m) and written once.  Results do not depend on where the
-// windows land, only the atomic traffic does.
+// same neighbourhood.  Phase 0 takes the bounding box of the corners the tile's samples touch per level,
+// the contribution bound, and stages the tile's grad_output rows (this head) in LDS; the window = that box
+// clipped to the tile +- halo (halo shrunk until the window fits the index budget).
+//
+// grad_value is a scatter: every (query, point, corner) adds w_c * a * g[query] (32 channels) to one
+// pixel row.  Scattering those rows into LDS costs 16 LDS atomics per corner per 8-lane group, and
+// gfx950's LDS atomics are slow (ds_add_f32 ~190 cycles per wave-instruction, ds_add_u64 ~30:
+// tools/ubench).  Instead the scatter is turned into a gather inside the workgroup:
+//   phase 2  for each in-window corner ONE lane stores the record's coefficient w_c * a and pushes the
+//            record onto its window row's list (one ds_wrxchg per corner: head[row] <-> record id;
+//            the record id encodes (query, level, point, corner), so only coef + next are stored);
+//   phase 3  an 8-lane group per window row walks the row's list, accumulating coef * g[query] (g from
+//            LDS) in registers as exact int64 fixed point (scale 2^e from the phase-0 bound so no sum can
+//            overflow: order-independent, hence deterministic), and adds the row to HBM once with
+//            row-contiguous atomics (32 lanes = 128 B).
+// Corners outside the window, and workgroups whose bound is 0 or non-finite, use direct fp32 atomics, so
+// NaN/inf propagate exactly as in the reference.  grad_loc / grad_attn are owned per (q, m) and written
+// once; channel reductions use DPP within the 8-lane group.
 //
 // FUSED = true is the same kernel for the fused front end (see msda_fused_fwd): the samples come from the
 // raw projection (offsets | logits) and the reference points, and the outputs are the gradients w.r.t.
@@ -324,7 +331,7 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
     float* __restrict__ gloc, float* __restrict__ gattn) {
   constexpr int D = 32;
-  extern __shared__ __attribute__((aligned(16))) unsigned long long win[];
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   __shared__ TileState ts;
 
   const int tile = blockIdx.x, m = blockIdx.y, n = blockIdx.z;
@@ -334,6 +341,13 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
   const int j = lane & 7, gq = lane >> 3;
   const int64_t rs = static_cast<int64_t>(M) * D;
   const int MLP2 = M * L * P * 2;  // fused: column of the first logit in a projection row
+  const int LP4 = L * P * 4;       // records per query
+  // LDS carve-up: g rows [max_qt][32] f32 | coef [max_qt * LP4] f32 | next [max_qt * LP4] u16 | head [max_rows] i32
+  float* gsh = reinterpret_cast<float*>(lds_raw);
+  float* coef = gsh + geo.max_qt * D;
+  unsigned short* nxt = reinterpret_cast<unsigned short*>(coef + geo.max_qt * LP4);
+  int* head = reinterpret_cast<int*>(lds_raw + ((geo.max_qt * D + geo.max_qt * LP4) * 4 +
+                                                ((geo.max_qt * LP4 * 2 + 15) & ~15)));
 
   if (tid < L) {
     const int l = tid;
@@ -366,6 +380,7 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
         const int q = tile_query(ts, geo, qi);
         const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
         const f4 gv4 = ld4(gout + pair * D + 4 * j);
+        *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = gv4;
         const float gm = fmaxf(fmaxf(fabsf(gv4.x), fabsf(gv4.y)), fmaxf(fabsf(gv4.z), fabsf(gv4.w)));
         // fmaxf drops NaN: fold non-finite values in as +inf so the workgroup takes the atomic path
         const bool gbad = !(isfinite(gv4.x) && isfinite(gv4.y) && isfinite(gv4.z) && isfinite(gv4.w));
@@ -433,9 +448,10 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
   if (tid == 0) {
     const float bound = __uint_as_float(ts.gmax) * __uint_as_float(ts.amax);
     const bool use_lds = bound > 1e-30f && bound < 1e30f;  // else: direct atomics (zeros, inf or NaN)
-    // at most Qt*L*P contributions reach one element: keep their sum below 2^62
+    // at most Qt*L*P contributions reach one element: keep their sum below 2^52 so the f64
+    // accumulation of integer-valued terms in phase 3 is exact
     const int cnt_bits = 32 - __clz(max(Qt * L * P, 1)) + 1;
-    const int e = use_lds ? 62 - cnt_bits - static_cast<int>(ceilf(log2f(bound))) : 0;
+    const int e = use_lds ? 52 - cnt_bits - static_cast<int>(ceilf(log2f(bound))) : 0;
     ts.scale = use_lds ? ldexpf(1.f, e) : 0.f;
     ts.unscale = use_lds ? ldexp(1.0, -e) : 0.0;
     for (int halo = use_lds ? geo.max_halo : -1; halo >= 0; --halo) {
@@ -467,7 +483,7 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
   __syncthreads();
   const int rows_total = ts.woff[L];
   const float fscale = ts.scale;
-  for (int i = tid; i < rows_total * D; i += blockDim.x) win[i] = 0ull;
+  for (int i = tid; i < rows_total; i += blockDim.x) head[i] = -1;
   __syncthreads();
 
   // ---- phase 2: gradients; grad_value into the windows --------------------------------------------
@@ -547,28 +563,28 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
           const bool iny0 = dy >= 0 && dy < wh, iny1 = dy + 1 >= 0 && dy + 1 < wh;
           const bool inx0 = dx >= 0 && dx < ww, inx1 = dx + 1 >= 0 && dx + 1 < ww;
           const int rbase = woff + dy * ww + dx;
+          // lane j < 4 pushes corner j's record onto its row list (one LDS exchange per corner)
+          if (j < 4) {
+            const bool valid = j == 0 ? k.c1 : (j == 1 ? k.c2 : (j == 2 ? k.c3 : k.c4));
+            const bool inside = (j < 2 ? iny0 : iny1) && ((j & 1) ? inx1 : inx0);
+            if (valid && inside && !(geo.ablate & 1)) {
+              const float wc = j == 0 ? k.w1 : (j == 1 ? k.w2 : (j == 2 ? k.w3 : k.w4));
+              const int id = ((qi * L + l) * P + p) * 4 + j;
+              coef[id] = wc * a;
+              const int old = atomicExch(head + rbase + (j >> 1) * ww + (j & 1), id);
+              nxt[id] = static_cast<unsigned short>(old);
+            }
+          }
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             const bool valid = c == 0 ? k.c1 : (c == 1 ? k.c2 : (c == 2 ? k.c3 : k.c4));
-            if (!valid) continue;
-            const float wc = c == 0 ? k.w1 : (c == 1 ? k.w2 : (c == 2 ? k.w3 : k.w4));
             const bool inside = (c < 2 ? iny0 : iny1) && ((c & 1) ? inx1 : inx0);
+            if (!valid || inside || (geo.ablate & 4)) continue;
+            const float wc = c == 0 ? k.w1 : (c == 1 ? k.w2 : (c == 2 ? k.w3 : k.w4));
             const f4 contrib = wc * tg;
-            if (inside) {
-              if (geo.ablate & 1) continue;
-              unsigned long long* row = win + (rbase + (c >> 1) * ww + (c & 1)) * D + 4 * j;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int comp = (e + gq) & 3;  // the 4 lane groups of a half-wave hit disjoint banks
-                const long long fxp = __float2ll_rn(pick4(contrib, comp) * fscale);
-                atomicAdd(row + comp, static_cast<unsigned long long>(fxp));
-              }
-            } else {
-              if (geo.ablate & 4) continue;
-              const int64_t o = c == 0 ? k.o1 : (c == 1 ? k.o2 : (c == 2 ? k.o3 : k.o4));
-              atomicAdd(gvalue + o, contrib.x); atomicAdd(gvalue + o + 1, contrib.y);
-              atomicAdd(gvalue + o + 2, contrib.z); atomicAdd(gvalue + o + 3, contrib.w);
-            }
+            const int64_t o = c == 0 ? k.o1 : (c == 1 ? k.o2 : (c == 2 ? k.o3 : k.o4));
+            atomicAdd(gvalue + o, contrib.x); atomicAdd(gvalue + o + 1, contrib.y);
+            atomicAdd(gvalue + o + 2, contrib.z); atomicAdd(gvalue + o + 3, contrib.w);
           }
         }
       }
@@ -591,20 +607,37 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
   }
   __syncthreads();
 
-  // ---- phase 3: flush the windows ----------------------------------------------------------------
-  const int flush_end = (geo.ablate & 2) ? 0 : rows_total * D;
-  const double unscale = ts.unscale;
-  for (int idx = tid; idx < flush_end; idx += blockDim.x) {
-    const long long fxp = static_cast<long long>(win[idx]);
-    if (fxp == 0) continue;
-    const float v = static_cast<float>(static_cast<double>(fxp) * unscale);
-    const int row = idx >> 5, ch = idx & 31;
-    int l = 0;
-    while (row >= ts.woff[l + 1]) ++l;
-    const int rr = row - ts.woff[l];
-    const int y = ts.wy0[l] + rr / ts.ww[l], x = ts.wx0[l] + rr % ts.ww[l];
-    const int64_t o = ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D + ch;
-    atomicAdd(gvalue + o, v);
+  // ---- phase 3: per window row, an 8-lane group walks its list and adds the row to HBM once -------
+  if (!(geo.ablate & 2)) {
+    const double unscale = ts.unscale;
+    const float inv_lp4 = 1.f / static_cast<float>(LP4);
+    const int ngroups = blockDim.x >> 3;
+    for (int row = tid >> 3; row < rows_total; row += ngroups) {
+      int id = head[row];
+      if (id < 0) continue;  // the 8 lanes of a group share the row
+      // every term is an integer (fixed point, |sum| < 2^52): the f64 adds are exact, so the result does
+      // not depend on the list order
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      while (id != 0xffff) {
+        const float c = coef[id] * fscale;
+        const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
+        const f4 g = *reinterpret_cast<const f4*>(gsh + q * D + 4 * j);
+        a0 += static_cast<double>(rintf(c * g.x));
+        a1 += static_cast<double>(rintf(c * g.y));
+        a2 += static_cast<double>(rintf(c * g.z));
+        a3 += static_cast<double>(rintf(c * g.w));
+        id = nxt[id];
+      }
+      int l = 0;
+      while (row >= ts.woff[l + 1]) ++l;
+      const int rr = row - ts.woff[l];
+      const int y = ts.wy0[l] + rr / ts.ww[l], x = ts.wx0[l] + rr % ts.ww[l];
+      float* dst = gvalue + ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D + 4 * j;
+      if (a0 != 0.0) atomicAdd(dst + 0, static_cast<float>(a0 * unscale));
+      if (a1 != 0.0) atomicAdd(dst + 1, static_cast<float>(a1 * unscale));
+      if (a2 != 0.0) atomicAdd(dst + 2, static_cast<float>(a2 * unscale));
+      if (a3 != 0.0) atomicAdd(dst + 3, static_cast<float>(a3 * unscale));
+    }
   }
 }
 
@@ -760,22 +793,27 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   if (total != d.S) return false;
-  const int tile = env_int("M2F_MSDA_TILE", 12);
+  const int tile = env_int("M2F_MSDA_TILE", 16);
   threads = env_int("M2F_MSDA_THREADS", 1024);
   geo.nty = (geo.H[fi] + tile - 1) / tile;
   geo.ntx = (geo.W[fi] + tile - 1) / tile;
-  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 576);
+  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 2048);
   geo.max_halo = env_int("M2F_MSDA_HALO", 8);
   geo.ablate = env_int("M2F_MSDA_ABLATE", 0);
-  // the budget must hold every level's share of one tile (halo 0)
-  int own = 0;
+  // the index budget must hold every level's share of one tile (halo 0); tiles span at most
+  // ceil(n / nt) pixels per axis (tile_lo)
+  int own = 0, qt = 0;
   for (int l = 0; l < d.L; ++l) {
-    const int th = (geo.H[l] + geo.nty - 1) / geo.nty + 1, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx + 1;
-    own += th * tw;
+    const int th = (geo.H[l] + geo.nty - 1) / geo.nty, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx;
+    own += (th + 1) * (tw + 1);
+    qt += th * tw;
   }
-  if (own > geo.max_rows) return false;
-  lds = static_cast<size_t>(geo.max_rows) * 32 * sizeof(unsigned long long);
-  return lds <= 150 * 1024 && (threads == 256 || threads == 512 || threads == 1024);
+  geo.max_qt = qt;
+  const int lp4 = d.L * d.P * 4;
+  if (own > geo.max_rows || static_cast<int64_t>(qt) * lp4 >= 0xffff) return false;
+  lds = static_cast<size_t>(qt) * 32 * 4 + static_cast<size_t>(qt) * lp4 * 4 +
+        ((static_cast<size_t>(qt) * lp4 * 2 + 15) & ~static_cast<size_t>(15)) + static_cast<size_t>(geo.max_rows) * 4;
+  return lds <= 150 * 1024 && threads >= 64 && threads <= 1024 && threads % 64 == 0;
 }
 
 template <int P, int LT, bool FUSED>

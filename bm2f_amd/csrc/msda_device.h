@@ -55,9 +55,10 @@ struct TileGeom {
   int L;
   int H[kTileMaxL], W[kTileMaxL], start[kTileMaxL];
   int nty, ntx;   // tile grid shared by all levels
-  int max_rows;   // LDS window budget (rows of 32 floats)
+  int max_rows;   // window index space (rows = pixels of one head): list heads in LDS
   int max_halo;   // windows never extend more than this many pixels past the tile
-  int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no LDS adds, 2 no flush, 4 no spill atomics
+  int max_qt;     // queries of the largest tile (sizes the LDS carve-up)
+  int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no list inserts, 2 no flush, 4 no spill atomics
 };
 
 __device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }

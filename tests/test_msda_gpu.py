@@ -183,8 +183,8 @@ def _pyramid_case(shapes, N, M, far_frac, seed):
     return value, st, lsi, loc.contiguous(), attn, gout
 
 
-@pytest.mark.parametrize("tile,rows,halo,threads", [(16, 576, 8, 1024), (8, 480, 8, 512), (4, 64, 2, 256),
-                                                     (8, 200, 0, 1024)])
+@pytest.mark.parametrize("tile,rows,halo,threads", [(16, 2048, 8, 1024), (12, 2048, 8, 768), (8, 480, 8, 512),
+                                                     (4, 64, 2, 256), (8, 200, 0, 1024), (6, 2048, 12, 320)])
 def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, threads):
     from bm2f_amd import msda
     monkeypatch.setenv("M2F_MSDA_TILE", str(tile))
