@@ -43,7 +43,6 @@ using bf8 = __bf16 __attribute__((ext_vector_type(8)));
 using bf4 = __bf16 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 16;     // k per stage = one 32x32x16 MFMA step
-constexpr int kPitch = 24;  // bf16 per LDS row (48 B): 16 data + 8 pad
 
 __device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
@@ -65,42 +64,6 @@ __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l)
 }
 
 enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4 };
-
-// One stage's LDS image: [plane][row][kPitch] for ROWS = (A rows + B rows).
-template <int ROWS>
-struct Stage {
-  __bf16 p[3][ROWS * kPitch];
-};
-
-// MFMA core shared by NT and TN: wave (wm, wn) owns TI x TJ tiles of 32x32 at rows wm*TI*32 of the A
-// image and wn*TJ*32 of the B image (B image rows start at BM).
-template <int BM, int TI, int TJ, int ROWS>
-__device__ __forceinline__ void stage_mfma(const Stage<ROWS>& s, int wm, int wn, int li, int lh,
-                                           f16v (&acc)[TI][TJ]) {
-  bf8 fa[3][TI], fb[3][TJ];
-#pragma unroll
-  for (int pl = 0; pl < 3; ++pl) {
-#pragma unroll
-    for (int i = 0; i < TI; ++i)
-      fa[pl][i] = *reinterpret_cast<const bf8*>(&s.p[pl][(wm * TI * 32 + i * 32 + li) * kPitch + lh * 8]);
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-      fb[pl][j] = *reinterpret_cast<const bf8*>(&s.p[pl][(BM + wn * TJ * 32 + j * 32 + li) * kPitch + lh * 8]);
-  }
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j) {
-      f16v c = acc[i][j];
-      c = mfma(fa[2][i], fb[0][j], c);  // al.bh
-      c = mfma(fa[1][i], fb[1][j], c);  // am.bm
-      c = mfma(fa[0][i], fb[2][j], c);  // ah.bl
-      c = mfma(fa[1][i], fb[0][j], c);  // am.bh
-      c = mfma(fa[0][i], fb[1][j], c);  // ah.bm
-      c = mfma(fa[0][i], fb[0][j], c);  // ah.bh
-      acc[i][j] = c;
-    }
-}
 
 // ---------------------------------------------------------------------------------------------------
 // NT: C[M,N] = A[M,K] . B[N,K]^T.
@@ -338,134 +301,204 @@ int64_t nt_workspace(int N, int K) {
 }
 
 // ---------------------------------------------------------------------------------------------------
-// TN split-M: block (tile of C, split) accumulates rows [r0, r1) into slab[split].  Staging transposes:
-// a thread owns one column of A (or B) and 8 consecutive rows (k), so its plane stores are one 16-byte
-// ds_write each (rows 48 B apart: 8 lanes cover the 32 banks).
+// TN split-M: C[N1,N2] = sum over m of A[m,n1] B[m,n2], rows m split over workgroups (slabs reduced in a
+// fixed order afterwards: deterministic).  The orientation is chosen so the wider operand is A.
+//
+// A block of NW waves owns NW*32 columns of A (rows of C) and 256 columns of B for one M-slab.  Each wave
+// loads its own A^T fragments straight from HBM into registers (lane (r, h): column r, rows 8h .. 8h+7 of
+// the chunk -- eight 4-byte loads, each instruction two 128-byte row segments), splits them there and
+// keeps its 32 C rows x 256 C columns in accumulators.  The block's B chunk (16 rows x 256 columns) is
+// split once while being transposed into the dense swizzled LDS image of the NT kernel (a thread owns one
+// column x 8 rows: one 16-byte store per plane).  Two-deep register prefetch, one barrier per chunk.
+// C tiles leave through a per-wave LDS image as float4 rows (transposed when the operands were swapped).
 // ---------------------------------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN>
-__global__ void __launch_bounds__(64 * WM * WN) x3_tn_kernel(const float* __restrict__ A, int64_t lda,
-                                                            const float* __restrict__ B, int64_t ldb, int M, int N1,
-                                                            int N2, int rows_per_split, float* __restrict__ slab,
-                                                            float* __restrict__ colsum_slab) {
-  constexpr int NT = 64 * WM * WN;
-  constexpr int TI = BM / WM / 32, TJ = BN / WN / 32;
-  constexpr int ROWS = BM + BN;
-  constexpr int NJOB = (ROWS * 2 + NT - 1) / NT;  // (column, 8-row half) jobs per thread per stage
-  static_assert(TI * WM * 32 == BM && TJ * WN * 32 == BN, "tile");
-  __shared__ Stage<ROWS> st[2];
+template <int NW>
+__global__ void __launch_bounds__(64 * NW, 2) x3_tn_kernel(const float* __restrict__ A, int64_t lda,
+                                                           const float* __restrict__ B, int64_t ldb, int M, int N1,
+                                                           int N2, int rows_per_split, int trans_out,
+                                                           float* __restrict__ slab, float* __restrict__ colsum_slab,
+                                                           int colsum_b) {
+  constexpr int NT = 64 * NW, BN = 256, TJ = BN / 32;
+  constexpr int JOBS = BN * 2;                       // (B column, 8-row half) per chunk
+  constexpr int NJ = (JOBS + NT - 1) / NT;
+  constexpr int CHUNK = 3 * BN * 16;                 // bf16 per LDS image
+  constexpr int EP = 36;
+  constexpr int LDS_B = 2 * CHUNK * 2, LDS_E = NW * 32 * EP * 4;
+  __shared__ __attribute__((aligned(16))) char smem[LDS_B > LDS_E ? LDS_B : LDS_E];
+  __bf16(*sb)[CHUNK] = reinterpret_cast<__bf16(*)[CHUNK]>(smem);
 
-  const int nb1 = (N1 + BM - 1) / BM, nb2 = (N2 + BN - 1) / BN;
+  const int nb1 = (N1 + 32 * NW - 1) / (32 * NW), nb2 = (N2 + BN - 1) / BN;
   const int tiles = nb1 * nb2;
   const int id = xcd_remap(blockIdx.x, gridDim.x);
   const int split = id / tiles, t = id % tiles;
   const int b1 = t / nb2, b2 = t % nb2;
-  const int n10 = b1 * BM, n20 = b2 * BN;
+  const int n10 = b1 * 32 * NW, n20 = b2 * BN;
   const int r0 = split * rows_per_split;
   const int r1 = min(M, r0 + rows_per_split);
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w / WN, wn = w % WN;
   const int li = lane & 31, lh = lane >> 5;
-  const bool do_colsum = colsum_slab != nullptr && b2 == 0;
-
-  // job = half * ROWS + c: image row c (A column n10 + c, or B column n20 + c - BM), k rows 8*half .. +7
-  float rg[NJOB][8];
-  float csum[NJOB];
-#pragma unroll
-  for (int u = 0; u < NJOB; ++u) csum[u] = 0.f;
-  auto gload = [&](int k0) {
-#pragma unroll
-    for (int u = 0; u < NJOB; ++u) {
-      const int job = tid + u * NT, half = job / ROWS, c = job - half * ROWS;
-      const float* src = nullptr;
-      int64_t ld = 0;
-      if (job < 2 * ROWS) {
-        if (c < BM) {
-          if (n10 + c < N1) { src = A + n10 + c; ld = lda; }
-        } else if (n20 + c - BM < N2) {
-          src = B + n20 + c - BM;
-          ld = ldb;
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int r = k0 + half * 8 + e;
-        rg[u][e] = (src && r < r1) ? src[static_cast<int64_t>(r) * ld] : 0.f;
-      }
-    }
-  };
-  auto sstore = [&](Stage<ROWS>& s) {
-#pragma unroll
-    for (int u = 0; u < NJOB; ++u) {
-      const int job = tid + u * NT, half = job / ROWS, c = job - half * ROWS;
-      if (job >= 2 * ROWS) continue;
-      bf8 h, m, l;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        __bf16 a, b, cc;
-        split3(rg[u][e], a, b, cc);
-        h[e] = a; m[e] = b; l[e] = cc;
-      }
-      if (do_colsum && c < BM) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) csum[u] += rg[u][e];
-      }
-      const int off = c * kPitch + half * 8;
-      *reinterpret_cast<bf8*>(&s.p[0][off]) = h;
-      *reinterpret_cast<bf8*>(&s.p[1][off]) = m;
-      *reinterpret_cast<bf8*>(&s.p[2][off]) = l;
-    }
-  };
-
-  f16v acc[TI][TJ];
-#pragma unroll
-  for (int i = 0; i < TI; ++i)
-#pragma unroll
-    for (int j = 0; j < TJ; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-
+  const int acol = min(n10 + w * 32 + li, N1 - 1);
+  const float* ap = A + acol;
   const int nk = r1 > r0 ? (r1 - r0 + kBK - 1) / kBK : 0;
+  const bool csum_a = colsum_slab != nullptr && !colsum_b && b2 == 0;
+  const bool csum_b = colsum_slab != nullptr && colsum_b && b1 == 0;
+
+  struct Regs {
+    float a[8];
+    float b[NJ][8];
+  };
+  // rows >= r1 are clamped in-bounds here and zeroed when split (never waited on at the load)
+  auto gload = [&](Regs& r, int c) {
+    const int m = r0 + c * kBK;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) r.a[e] = ap[static_cast<int64_t>(min(m + lh * 8 + e, M - 1)) * lda];
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) {
+      const int job = min(tid + u * NT, JOBS - 1), half = job / BN, col = min(n20 + job % BN, N2 - 1);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r.b[u][e] = B[static_cast<int64_t>(min(m + half * 8 + e, M - 1)) * ldb + col];
+    }
+  };
+  float csa = 0.f, csb[NJ];
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) csb[u] = 0.f;
+  auto bstore = [&](const Regs& r, int c, int buf) {
+    const int m = r0 + c * kBK;
+#pragma unroll
+    for (int u = 0; u < NJ; ++u) {
+      const int job = tid + u * NT;
+      if (JOBS % NT != 0 && job >= JOBS) continue;
+      const int half = job / BN, col = job % BN;
+      bf8 h, mm, l;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = m + half * 8 + e < r1 ? r.b[u][e] : 0.f;
+        if (csum_b) csb[u] += v;
+        __bf16 x, y, z;
+        split3(v, x, y, z);
+        h[e] = x; mm[e] = y; l[e] = z;
+      }
+      const int off = col * 16 + ((half ^ swz(col)) * 8);
+      *reinterpret_cast<bf8*>(&sb[buf][off]) = h;
+      *reinterpret_cast<bf8*>(&sb[buf][BN * 16 + off]) = mm;
+      *reinterpret_cast<bf8*>(&sb[buf][2 * BN * 16 + off]) = l;
+    }
+  };
+  auto asplit = [&](const Regs& r, int c, bf8 (&fa)[3]) {
+    const int m = r0 + c * kBK + lh * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = m + e < r1 ? r.a[e] : 0.f;
+      if (csum_a) csa += v;
+      __bf16 h, mm, l;
+      split3(v, h, mm, l);
+      fa[0][e] = h; fa[1][e] = mm; fa[2][e] = l;
+    }
+  };
+
+  f16v acc[TJ];
+#pragma unroll
+  for (int j = 0; j < TJ; ++j)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[j][e] = 0.f;
+
+  const int boff = li * 16 + ((lh ^ swz(li)) * 8);
+  auto chunk_mfma = [&](int buf, const bf8 (&fa)[3]) {
+    const __bf16* base = &sb[buf][0];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int off = j * 32 * 16 + boff;
+      const bf8 bh = *reinterpret_cast<const bf8*>(base + off);
+      const bf8 bmv = *reinterpret_cast<const bf8*>(base + BN * 16 + off);
+      const bf8 bl = *reinterpret_cast<const bf8*>(base + 2 * BN * 16 + off);
+      f16v x = acc[j];
+      x = mfma(fa[2], bh, x);   // al.bh
+      x = mfma(fa[1], bmv, x);  // am.bm
+      x = mfma(fa[0], bl, x);   // ah.bl
+      x = mfma(fa[1], bh, x);   // am.bh
+      x = mfma(fa[0], bmv, x);  // ah.bm
+      x = mfma(fa[0], bh, x);   // ah.bh
+      acc[j] = x;
+    }
+  };
+
   if (nk > 0) {
-    gload(r0);
-    sstore(st[0]);
-  }
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload(r0 + (kt + 1) * kBK);
-    stage_mfma<BM, TI, TJ, ROWS>(st[kt & 1], wm, wn, li, lh, acc);
-    if (kt + 1 < nk) sstore(st[(kt + 1) & 1]);
+    Regs r0s, r1s;
+    bf8 fa[3];
+    gload(r0s, 0);
+    if (nk > 1) gload(r1s, 1);
+    bstore(r0s, 0, 0);
+    asplit(r0s, 0, fa);
     __syncthreads();
+    auto step = [&](int c, Regs& cur, Regs& nxt) {
+      if (c + 2 < nk) gload(cur, c + 2);
+      chunk_mfma(c & 1, fa);
+      if (c + 1 < nk) {
+        bstore(nxt, c + 1, (c + 1) & 1);
+        asplit(nxt, c + 1, fa);
+      }
+      __syncthreads();
+    };
+    for (int c = 0; c < nk; c += 2) {
+      step(c, r0s, r1s);
+      if (c + 1 < nk) step(c + 1, r1s, r0s);
+    }
   }
 
+  // ---- epilogue: slab[split] is [N1][N2] (or [N2][N1] when trans_out) --------------------------------
+  const int R = trans_out ? N2 : N1, Cn = trans_out ? N1 : N2;
   float* out = slab + static_cast<int64_t>(split) * N1 * N2;
+  float* img = reinterpret_cast<float*>(smem) + w * 32 * EP;
+  const int er = lane >> 3, ec = (lane & 7) * 4;
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
-    const int col = n20 + wn * TJ * 32 + j * 32 + li;
-    if (col >= N2) continue;
 #pragma unroll
-    for (int i = 0; i < TI; ++i) {
+    for (int e = 0; e < 16; ++e) {
+      const int rr = (e & 3) + 8 * (e >> 2) + 4 * lh;   // C row (n1) within the tile; column = li (n2)
+      if (trans_out) img[li * EP + rr] = acc[j][e];
+      else img[rr * EP + li] = acc[j][e];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // image rows: n1 (normal) or n2 (transposed); columns the other index
+    const int row0 = trans_out ? n20 + j * 32 : n10 + w * 32;
+    const int col0 = trans_out ? n10 + w * 32 : n20 + j * 32;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int row = n10 + wm * TI * 32 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * lh;
-        if (row < N1) out[static_cast<int64_t>(row) * N2 + col] = acc[i][j][e];
+    for (int q = 0; q < 4; ++q) {
+      const int lr = q * 8 + er, row = row0 + lr, col = col0 + ec;
+      const f4 v = *reinterpret_cast<const f4*>(&img[lr * EP + ec]);
+      if (row >= R) continue;
+      if (col + 3 < Cn && (Cn & 3) == 0) {
+        *reinterpret_cast<f4*>(out + static_cast<int64_t>(row) * Cn + col) = v;
+      } else {
+        for (int t2 = 0; t2 < 4 && col + t2 < Cn; ++t2) out[static_cast<int64_t>(row) * Cn + col + t2] = v[t2];
       }
     }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  if (do_colsum) {
-    // the two row halves of each A column: half 1 hands its sum to half 0 through LDS (stage 0 is free:
-    // the loop ended with a barrier)
-    float* red = reinterpret_cast<float*>(&st[0].p[0][0]);
+  if (csum_a) {
+    csa += __shfl_xor(csa, 32);
+    const int col = n10 + w * 32 + li;
+    if (lh == 0 && col < N1) colsum_slab[static_cast<int64_t>(split) * N1 + col] = csa;
+  }
+  if (csum_b) {
+    // the two 8-row halves of each B column: half 1 hands its sum to half 0 through LDS
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(smem);
 #pragma unroll
-    for (int u = 0; u < NJOB; ++u) {
-      const int job = tid + u * NT, half = job / ROWS, c = job - half * ROWS;
-      if (job < 2 * ROWS && half == 1 && c < BM) red[c] = csum[u];
+    for (int u = 0; u < NJ; ++u) {
+      const int job = tid + u * NT;
+      if (job < JOBS && job / BN == 1) red[job % BN] = csb[u];
     }
     __syncthreads();
 #pragma unroll
-    for (int u = 0; u < NJOB; ++u) {
-      const int job = tid + u * NT, half = job / ROWS, c = job - half * ROWS;
-      if (job < 2 * ROWS && half == 0 && c < BM && n10 + c < N1)
-        colsum_slab[static_cast<int64_t>(split) * N1 + n10 + c] = csum[u] + red[c];
+    for (int u = 0; u < NJ; ++u) {
+      const int job = tid + u * NT, col = n20 + job % BN;
+      if (job < JOBS && job / BN == 0 && col < N2)
+        colsum_slab[static_cast<int64_t>(split) * N2 + col] = csb[u] + red[job % BN];
     }
   }
 }
@@ -488,20 +521,28 @@ __global__ void __launch_bounds__(256) x3_slab_reduce(const float* __restrict__ 
   out[r * ldo + c] = (a0 + a1) + (a2 + a3);
 }
 
-// TN tiles: 128 x 128 (4 waves, 2x2 of 64x64)
-constexpr int kTBM = 128, kTBN = 128, kTWM = 2, kTWN = 2;
+struct TnPlan {
+  bool swap;   // A <-> B (the wider operand goes to the wave-direct side)
+  int nw;      // waves per block (32 C rows each)
+  int n1, n2;  // sizes after the swap
+  int tiles, splits, rows;
+};
 
-int tn_splits(int M, int N1, int N2) {
-  const int tiles = ((N1 + kTBM - 1) / kTBM) * ((N2 + kTBN - 1) / kTBN);
-  int splits = (512 + tiles - 1) / tiles;                       // ~512 blocks: 2 per CU
-  const int max_splits = (M + 8 * kBK - 1) / (8 * kBK);         // >= 8 K-steps per block
+TnPlan tn_plan(int M, int N1, int N2) {
+  TnPlan p;
+  p.swap = N2 > N1;
+  p.n1 = p.swap ? N2 : N1;
+  p.n2 = p.swap ? N1 : N2;
+  p.nw = 4;  // 3 (96-row tiles, exact for 288) measured slower: fewer threads share the B staging
+  if (const char* e = std::getenv("M2F_GEMM_X3_TN_NW")) p.nw = std::atoi(e) == 3 ? 3 : 4;
+  p.tiles = ((p.n1 + 32 * p.nw - 1) / (32 * p.nw)) * ((p.n2 + 255) / 256);
+  int splits = (512 + p.tiles - 1) / p.tiles;                // ~512 blocks: 2 per CU
+  const int max_splits = (M + 8 * kBK - 1) / (8 * kBK);       // >= 8 chunks per block
   if (splits > max_splits) splits = max_splits;
-  return splits < 1 ? 1 : splits;
-}
-
-int tn_rows_per_split(int M, int splits) {
-  const int r = (M + splits - 1) / splits;
-  return (r + kBK - 1) / kBK * kBK;
+  p.splits = splits < 1 ? 1 : splits;
+  const int r = (M + p.splits - 1) / p.splits;
+  p.rows = (r + kBK - 1) / kBK * kBK;
+  return p;
 }
 
 }  // namespace
@@ -546,8 +587,8 @@ extern "C" int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, in
 
 extern "C" int m2f_gemm_f32x3_tn_workspace(int M, int N1, int N2, int64_t* workspace_bytes) {
   if (M < 0 || N1 <= 0 || N2 <= 0) return m2f::fail(M2F_EINVAL, "m2f_gemm_f32x3_tn_workspace: bad sizes");
-  const int splits = tn_splits(M, N1, N2);
-  if (workspace_bytes) *workspace_bytes = static_cast<int64_t>(splits) * (static_cast<int64_t>(N1) * N2 + N1) * 4;
+  const TnPlan p = tn_plan(M, N1, N2);
+  if (workspace_bytes) *workspace_bytes = static_cast<int64_t>(p.splits) * (static_cast<int64_t>(N1) * N2 + N1) * 4;
   return m2f::ok();
 }
 
@@ -558,25 +599,42 @@ extern "C" int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, in
   if (M < 0 || N1 <= 0 || N2 <= 0) return m2f::fail(M2F_EINVAL, "%s: M %d N1 %d N2 %d", fn, M, N1, N2);
   if ((M > 0 && (!A || !B)) || !C) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
   if (lda < N1 || ldb < N2 || ldc < N2) return m2f::fail(M2F_EINVAL, "%s: leading dimensions too small", fn);
-  const int splits = tn_splits(M, N1, N2);
-  const int64_t need = static_cast<int64_t>(splits) * (static_cast<int64_t>(N1) * N2 + N1) * 4;
+  const TnPlan p = tn_plan(M, N1, N2);
+  const int64_t need = static_cast<int64_t>(p.splits) * (static_cast<int64_t>(N1) * N2 + N1) * 4;
   if (!workspace || workspace_bytes < need)
     return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld", fn, static_cast<long long>(workspace_bytes),
                      static_cast<long long>(need));
   hipStream_t st = static_cast<hipStream_t>(stream);
   float* slab = static_cast<float*>(workspace);
-  float* cslab = slab + static_cast<int64_t>(splits) * N1 * N2;
-  const int tiles = ((N1 + kTBM - 1) / kTBM) * ((N2 + kTBN - 1) / kTBN);
-  const int rps = tn_rows_per_split(M, splits);
-  x3_tn_kernel<kTBM, kTBN, kTWM, kTWN><<<splits * tiles, 64 * kTWM * kTWN, 0, st>>>(
-      A, lda, B, ldb, M, N1, N2, rps, slab, colsum ? cslab : nullptr);
-  if (int rc = m2f::check_launch(fn)) return rc;
-  const int64_t n = static_cast<int64_t>(N1) * N2;
-  x3_slab_reduce<<<m2f::ceil_div(n, 256), 256, 0, st>>>(slab, splits, n, C, ldc, N2);
-  if (int rc = m2f::check_launch(fn)) return rc;
-  if (colsum) {
-    x3_slab_reduce<<<m2f::ceil_div(N1, 256), 256, 0, st>>>(cslab, splits, N1, colsum, N1, N1);
-    return m2f::check_launch(fn);
+  float* cslab = slab + static_cast<int64_t>(p.splits) * N1 * N2;
+  const float* a = p.swap ? B : A;
+  const float* b = p.swap ? A : B;
+  const int64_t la = p.swap ? ldb : lda, lb = p.swap ? lda : ldb;
+  const unsigned grid = static_cast<unsigned>(p.splits * p.tiles);
+  // slab orientation is always [N1][N2] (the caller's): transposed store when swapped
+  if (M > 0) {
+    if (p.nw == 3)
+      x3_tn_kernel<3><<<grid, 192, 0, st>>>(a, la, b, lb, M, p.n1, p.n2, p.rows, p.swap ? 1 : 0, slab,
+                                            colsum ? cslab : nullptr, p.swap ? 1 : 0);
+    else
+      x3_tn_kernel<4><<<grid, 256, 0, st>>>(a, la, b, lb, M, p.n1, p.n2, p.rows, p.swap ? 1 : 0, slab,
+                                            colsum ? cslab : nullptr, p.swap ? 1 : 0);
+    if (int rc = m2f::check_launch(fn)) return rc;
   }
+  const int64_t n = static_cast<int64_t>(N1) * N2;
+  if (M > 0) {
+    x3_slab_reduce<<<m2f::ceil_div(n, 256), 256, 0, st>>>(slab, p.splits, n, C, ldc, N2);
+    if (int rc = m2f::check_launch(fn)) return rc;
+    if (colsum) {
+      x3_slab_reduce<<<m2f::ceil_div(N1, 256), 256, 0, st>>>(cslab, p.splits, N1, colsum, N1, N1);
+      return m2f::check_launch(fn);
+    }
+    return m2f::ok();
+  }
+  // M == 0: C = 0, colsum = 0
+  if (hipMemset2DAsync(C, static_cast<size_t>(ldc) * 4, 0, static_cast<size_t>(N2) * 4, N1, st) != hipSuccess)
+    return m2f::fail(M2F_ELAUNCH, "%s: memset", fn);
+  if (colsum && hipMemsetAsync(colsum, 0, static_cast<size_t>(N1) * 4, st) != hipSuccess)
+    return m2f::fail(M2F_ELAUNCH, "%s: memset", fn);
   return m2f::ok();
 }

@@ -82,10 +82,7 @@ def gemm_tn(a, b, colsum=False, engine=None):
     N2 = b.shape[1]
     out = torch.empty(N1, N2, device=a.device, dtype=torch.float32)
     cs = torch.empty(N1, device=a.device, dtype=torch.float32) if colsum else None
-    # x3 TN on 128-multiples only: its 128x128 tiles waste a third of the work on the 288-wide projection,
-    # where the exact engine is faster (tools/gemm_x3_bench.py)
-    x3 = _engine(engine) == "x3" and (engine == "x3" or (N1 % 128 == 0 and N2 % 128 == 0))
-    fn = "m2f_gemm_f32x3_tn" if x3 else "m2f_gemm_f32_tn"
+    fn = "m2f_gemm_f32x3_tn" if _engine(engine) == "x3" else "m2f_gemm_f32_tn"
     wsb = ctypes.c_int64(0)
     _native.call(fn + "_workspace", M, N1, N2, ctypes.byref(wsb))
     ws = torch.empty(max(wsb.value, 4), device=a.device, dtype=torch.uint8)
