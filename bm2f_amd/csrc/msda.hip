@@ -325,12 +325,14 @@ __device__ __forceinline__ int tile_query(const TileState& ts, const TileGeom& g
   return geo.start[lq] + (ts.qy0[lq] + r / ts.qw[lq]) * geo.W[lq] + ts.qx0[lq] + r % ts.qw[lq];
 }
 
-template <int P, int LT, bool FUSED>
-__global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
+template <int P, int LT, bool FUSED, int TPB>
+__global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
     float* __restrict__ gloc, float* __restrict__ gattn) {
   constexpr int D = 32;
+  constexpr int PB = TPB <= 768 ? 4 : 1;  // points per gather batch (1024 threads: 128 VGPRs, no room)
+  static_assert(P % PB == 0, "batches cover the points");
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   __shared__ TileState ts;
 
@@ -407,7 +409,7 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
           }
           const int H = geo.H[l], W = geo.W[l];
           const float h = ly * H - 0.5f, w = lx * W - 0.5f;
-          if (h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W)) {
+          if (geo.bbox && h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W)) {
             const int h0 = static_cast<int>(floorf(h)), w0 = static_cast<int>(floorf(w));
             const int ylo = max(h0, 0), yhi = min(h0 + 1, H - 1), xlo = max(w0, 0), xhi = min(w0 + 1, W - 1);
 #pragma unroll
@@ -420,10 +422,14 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
         }
       }
     }
+    if (!geo.bbox) {  // window = tile +- halo: no reduction
+#pragma unroll
+      for (int l = 0; l < kTileMaxL; ++l) { bmin_y[l] = 0; bmax_y[l] = 0x3fffffff; bmin_x[l] = 0; bmax_x[l] = 0x3fffffff; }
+    }
 #pragma unroll
     for (int l = 0; l < kTileMaxL; ++l) {
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
+      for (int o = 32; o > 0 && geo.bbox; o >>= 1) {
         bmin_y[l] = min(bmin_y[l], __shfl_xor(bmin_y[l], o)); bmax_y[l] = max(bmax_y[l], __shfl_xor(bmax_y[l], o));
         bmin_x[l] = min(bmin_x[l], __shfl_xor(bmin_x[l], o)); bmax_x[l] = max(bmax_x[l], __shfl_xor(bmax_x[l], o));
       }
@@ -520,22 +526,39 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
       static_assert(P <= 4, "one lane per grad_loc component: 2P <= 8");
       float2 rf = make_float2(0.f, 0.f);
       if constexpr (FUSED) rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
+      // points in batches of PB: every corner load of a batch is issued before any of its math, so a
+      // wave keeps 4*PB row gathers in flight (the kernel is gather-latency bound)
 #pragma unroll
-      for (int p = 0; p < P; ++p) {
-        const int64_t kk = (pair * L + l) * P + p;
-        float sx, sy, a;
-        if constexpr (FUSED) {
-          const float2 off = *reinterpret_cast<const float2*>(prow + (m * LT * P + l * P + p) * 2);
-          sx = rf.x + off.x / static_cast<float>(W);
-          sy = rf.y + off.y / static_cast<float>(H);
-          a = expf(lgt[l * P + p] - smx) * sinv;
-        } else {
-          const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * kk);
-          sx = xy.x; sy = xy.y; a = attn[kk];
+      for (int p0 = 0; p0 < P; p0 += PB) {
+        Corners kb[PB];
+        float ab[PB];
+        f4 vb[PB][4];
+#pragma unroll
+        for (int pp = 0; pp < PB; ++pp) {
+          const int p = p0 + pp;
+          const int64_t kk = (pair * L + l) * P + p;
+          float sx, sy, a;
+          if constexpr (FUSED) {
+            const float2 off = *reinterpret_cast<const float2*>(prow + (m * LT * P + l * P + p) * 2);
+            sx = rf.x + off.x / static_cast<float>(W);
+            sy = rf.y + off.y / static_cast<float>(H);
+            a = expf(lgt[l * P + p] - smx) * sinv;
+          } else {
+            const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * kk);
+            sx = xy.x; sy = xy.y; a = attn[kk];
+          }
+          kb[pp] = make_corners(sx, sy, H, W, lbase, rs);
+          ab[pp] = a;
+          vb[pp][0] = ld4(value + kb[pp].o1); vb[pp][1] = ld4(value + kb[pp].o2);
+          vb[pp][2] = ld4(value + kb[pp].o3); vb[pp][3] = ld4(value + kb[pp].o4);
         }
-        const Corners k = make_corners(sx, sy, H, W, lbase, rs);
-        f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
-        v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
+#pragma unroll
+        for (int pp = 0; pp < PB; ++pp) {
+        const int p = p0 + pp;
+        const Corners& k = kb[pp];
+        const float a = ab[pp];
+        const f4 v1 = k.c1 ? vb[pp][0] : z, v2 = k.c2 ? vb[pp][1] : z;
+        const f4 v3 = k.c3 ? vb[pp][2] : z, v4 = k.c4 ? vb[pp][3] : z;
         const f4 tg = g * a;
         const f4 val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
         const f4 gw = -k.hy * v1 + k.hy * v2 - k.ly * v3 + k.ly * v4;
@@ -586,6 +609,7 @@ __global__ void __launch_bounds__(1024) msda_bwd_f32_tiled(
             atomicAdd(gvalue + o, contrib.x); atomicAdd(gvalue + o + 1, contrib.y);
             atomicAdd(gvalue + o + 2, contrib.z); atomicAdd(gvalue + o + 3, contrib.w);
           }
+        }
         }
       }
       if constexpr (FUSED) {
@@ -800,6 +824,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 2048);
   geo.max_halo = env_int("M2F_MSDA_HALO", 8);
   geo.ablate = env_int("M2F_MSDA_ABLATE", 0);
+  geo.bbox = env_int("M2F_MSDA_BBOX", 1);
   // the index budget must hold every level's share of one tile (halo 0); tiles span at most
   // ceil(n / nt) pixels per axis (tile_lo)
   int own = 0, qt = 0;
@@ -816,18 +841,31 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   return lds <= 150 * 1024 && threads >= 64 && threads <= 1024 && threads % 64 == 0;
 }
 
-template <int P, int LT, bool FUSED>
-void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                  const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                  hipStream_t st) {
+template <int P, int LT, bool FUSED, int TPB>
+void launch_tiled_t(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                    const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
+                    hipStream_t st) {
   static bool attr = false;  // one flag per instantiation
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<P, LT, FUSED>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<P, LT, FUSED, TPB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     attr = true;
   }
   const dim3 grid(geo.nty * geo.ntx, d.M, d.N);
-  msda_bwd_f32_tiled<P, LT, FUSED><<<grid, threads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+  msda_bwd_f32_tiled<P, LT, FUSED, TPB><<<grid, threads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+}
+
+// the register budget follows the block size: <= 512 threads get 2 waves/SIMD worth, 768 three, 1024 four
+template <int P, int LT, bool FUSED>
+void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                  const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
+                  hipStream_t st) {
+  if (threads <= 512)
+    launch_tiled_t<P, LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st);
+  else if (threads <= 768)
+    launch_tiled_t<P, LT, FUSED, 768>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st);
+  else
+    launch_tiled_t<P, LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st);
 }
 
 bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,

@@ -58,6 +58,7 @@ struct TileGeom {
   int max_rows;   // window index space (rows = pixels of one head): list heads in LDS
   int max_halo;   // windows never extend more than this many pixels past the tile
   int max_qt;     // queries of the largest tile (sizes the LDS carve-up)
+  int bbox;       // 1: shrink the window to the bounding box of the touched corners (phase 0 pass)
   int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no list inserts, 2 no flush, 4 no spill atomics
 };
 
