@@ -19,6 +19,7 @@ import math
 
 import torch
 from torch.autograd import Function
+from torch.nn import functional as F
 
 from . import _native
 
@@ -265,3 +266,52 @@ def image_mask_fold(mask_features, mask_features_lp=None):
     lp = mask_features if mask_features_lp is None else mask_features_lp
     B, C, H, W = lp.shape
     return MaskFeatureFold(mask_features, lp.detach().reshape(B, C, H * W), (H, W), lambda df, shape: df.view(shape))
+
+
+class _TokenLinear(Function):
+    """y = x W^T + b for the cross-attention K/V projections over the memory tokens (B * HW_l rows, up to
+    262,144 at 1024^2 bs16; reference: nn.MultiheadAttention's in_proj, mask2former_transformer_decoder.py
+    :103-108).  Same forward; the weight gradient G^T X, a 256 x 256 output over that long reduction, runs
+    as a split-K batched GEMM (2048-row chunks, fp32 chunk outputs summed in a fixed order) because the
+    library's single-GEMM kernel for this shape reaches ~70 TF against ~500 TF batched
+    (tools/wgrad_bf16_bench.py)."""
+
+    CHUNK = 2048
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, grad):
+        x, w = ctx.saved_tensors
+        g2 = grad.reshape(-1, grad.shape[-1])
+        x2 = x.reshape(-1, x.shape[-1])
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = (g2 @ w).view(x.shape)
+        if ctx.needs_input_grad[1]:
+            R, ch = g2.shape[0], _TokenLinear.CHUNK
+            if g2.is_cuda and R % ch == 0 and R >= 2 * ch and g2.is_contiguous() and x2.is_contiguous():
+                part = torch.bmm(g2.view(-1, ch, g2.shape[1]).transpose(1, 2), x2.view(-1, ch, x2.shape[1]),
+                                 out_dtype=torch.float32)
+                gw = part.sum(0).to(w.dtype)
+            else:
+                gw = g2.t() @ x2
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = g2.sum(0, dtype=torch.float32).to(w.dtype)
+        return gx, gw, gb
+
+
+def token_linear(x, weight, bias=None):
+    """``F.linear`` for memory-token projections (autocast applied here as F.linear would)."""
+    if x.is_cuda and torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        x, weight = x.to(dt), weight.to(dt)
+        bias = bias.to(dt) if bias is not None else None
+    if x.dtype not in (torch.bfloat16, torch.float16) or not x.is_cuda:
+        return F.linear(x, weight, bias)
+    with torch.autocast("cuda", enabled=False):
+        return _TokenLinear.apply(x, weight, bias)

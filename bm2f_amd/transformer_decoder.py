@@ -104,8 +104,8 @@ class CrossAttentionLayer(nn.Module):
         C = query.shape[-1]
         w, b = a.in_proj_weight, a.in_proj_bias
         q = F.linear(query, w[:C], b[:C])
-        k = F.linear(key, w[C:2 * C], b[C:2 * C])
-        v = F.linear(value, w[2 * C:], b[2 * C:])
+        k = decoder_ops.token_linear(key, w[C:2 * C], b[C:2 * C])
+        v = decoder_ops.token_linear(value, w[2 * C:], b[2 * C:])
         o = decoder_ops.masked_attention(q, k, v, bits, a.num_heads)
         return F.linear(o, a.out_proj.weight, a.out_proj.bias)
 

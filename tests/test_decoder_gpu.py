@@ -111,3 +111,24 @@ def test_masked_attention_fully_blocked_row_is_zero(device):
     out.sum().backward()
     assert qa.grad[:, 5].abs().max().item() == 0.0
     assert torch.isfinite(qa.grad).all()
+
+
+@pytest.mark.parametrize("rows", [262144, 6000])
+def test_token_linear_split_k_wgrad(device, rows):
+    """The K/V projection over memory tokens: forward == F.linear, weight gradient by split-K bmm within
+    bf16 rounding of the fp64 product (one rounding of an fp32 sum, like the library GEMM)."""
+    from bm2f_amd import decoder_ops
+    torch.manual_seed(rows)
+    x = torch.randn(rows, 256, device=device, dtype=torch.bfloat16, requires_grad=True)
+    w = (torch.randn(256, 256, device=device) * 0.05).bfloat16().requires_grad_()
+    b = torch.randn(256, device=device, dtype=torch.bfloat16, requires_grad=True)
+    y = decoder_ops._TokenLinear.apply(x, w, b)
+    torch.testing.assert_close(y, torch.nn.functional.linear(x, w, b), rtol=0, atol=0)
+    g = torch.randn_like(y)
+    y.backward(g)
+    ref_w = g.double().t() @ x.double()
+    err = ((w.grad.double() - ref_w).abs().max() / ref_w.abs().max()).item()
+    assert err < 8e-3, err   # bf16 output rounding (2^-8 relative)
+    ref_b = g.double().sum(0)
+    assert ((b.grad.double() - ref_b).abs().max() / ref_b.abs().max()).item() < 8e-3
+    torch.testing.assert_close(x.grad, g @ w)
