@@ -1,0 +1,110 @@
+"""fp32 convolutions of the pixel decoder's dense tail on the x3 MFMA engine (csrc/conv_x3.hip).
+
+The reference runs the pixel decoder with autocast off (msdeformattn.py:314,320), so its 1x1 input
+projections / lateral conv / mask_features conv and the 3x3 output conv are fp32 convs on the vendor
+library (reference: cuDNN, :213-292).  Here forward and input gradient are implicit GEMMs with the
+weights split exactly into three bf16 planes and the activations split in registers (fp32-accurate, see
+csrc/gemm_x3.hip), the weight gradient a split-over-pixels GEMM with its slabs summed in a fixed order.
+CUDA fp32 NCHW inputs that meet the kernel's shape rules run here (a missing library raises); anything
+else uses ``F.conv2d``.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+import torch.nn.functional as F
+from torch.autograd import Function
+
+from . import _native
+
+
+def _stream(t):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _workspace(N, Ci, Co, H, W, k, device):
+    b = ctypes.c_int64(0)
+    _native.call("m2f_conv_f32x3_workspace", N, Ci, Co, H, W, k, ctypes.byref(b))
+    return torch.empty(max(b.value, 16), device=device, dtype=torch.uint8)
+
+
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+class Conv2dX3(Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x = x.contiguous()
+        weight = weight.contiguous()
+        N, Ci, H, W = x.shape
+        Co, k = weight.shape[0], weight.shape[-1]
+        out = torch.empty(N, Co, H, W, device=x.device, dtype=torch.float32)
+        ws = _workspace(N, Ci, Co, H, W, k, x.device)
+        _native.call("m2f_conv_f32x3", x.data_ptr(), weight.data_ptr(), _ptr(bias), out.data_ptr(), N, Ci, Co, H, W,
+                     k, 0, ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(x))
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        x, weight = ctx.saved_tensors
+        g = grad.contiguous()
+        N, Ci, H, W = x.shape
+        Co, k = weight.shape[0], weight.shape[-1]
+        ws = _workspace(N, Ci, Co, H, W, k, x.device)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            _native.call("m2f_conv_f32x3", g.data_ptr(), weight.data_ptr(), None, dx.data_ptr(), N, Ci, Co, H, W, k, 1,
+                         ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(g))
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if k == 3 and (ctx.needs_input_grad[1] or want_b):
+            # 3x3 weight gradient on the library: in NCHW both operands of this pixel reduction are
+            # channel-strided, and the wave-direct loads of the x3 kernel (one channel per lane) measured
+            # 1.7x slower than MIOpen here (tools/conv_bench.py); forward and input gradient stay x3
+            _, dw, db = torch.ops.aten.convolution_backward(
+                g, x, weight, [Co] if want_b else None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
+                [False, bool(ctx.needs_input_grad[1]), want_b])
+        elif ctx.needs_input_grad[1] or want_b:
+            tck = torch.empty(k * k, Ci, Co, device=x.device, dtype=torch.float32)
+            db = torch.empty(Co, device=x.device, dtype=torch.float32) if want_b else None
+            _native.call("m2f_conv_f32x3_wgrad", g.data_ptr(), x.data_ptr(), tck.data_ptr(), _ptr(db), N, Ci, Co, H, W,
+                         k, ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(g))
+            dw = tck.permute(2, 1, 0).reshape(Co, Ci, k, k) if ctx.needs_input_grad[1] else None
+        return dx, dw, db
+
+
+def eligible(x, conv) -> bool:
+    """Shapes and settings the x3 conv kernels cover (else F.conv2d)."""
+    if not (x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32 and x.dim() == 4):
+        return False
+    k = conv.weight.shape[-1]
+    if conv.weight.shape[-2] != k or k not in (1, 3) or conv.groups != 1:
+        return False
+    if tuple(conv.stride) != (1, 1) or tuple(conv.dilation) != (1, 1) or tuple(conv.padding) != (k // 2, k // 2):
+        return False
+    N, Ci, H, W = x.shape
+    Co = conv.weight.shape[0]
+    return Ci % 16 == 0 and Co % 16 == 0 and (H * W) % 128 == 0 and W % 8 == 0
+
+
+def conv2d(x, conv):
+    """``F.conv2d(x, conv.weight, conv.bias, ...)`` for an nn.Conv2d (no norm / activation applied)."""
+    if eligible(x, conv):
+        return Conv2dX3.apply(x, conv.weight, conv.bias)
+    return F.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding, conv.dilation, conv.groups)
+
+
+def conv_norm_act(x, conv):
+    """A detectron2-style Conv2d (conv -> norm -> activation) with the conv on the x3 kernels."""
+    y = conv2d(x, conv)
+    norm = getattr(conv, "norm", None)
+    act = getattr(conv, "activation", None)
+    if norm is not None:
+        y = norm(y)
+    if act is not None:
+        y = act(y)
+    return y

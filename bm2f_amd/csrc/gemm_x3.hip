@@ -30,6 +30,7 @@
 // barrier per k-step, the next step's global loads in flight during the MFMAs.
 #include "bm2f.h"
 #include "common.h"
+#include "x3_device.h"
 
 #include <hip/hip_runtime.h>
 
@@ -37,31 +38,7 @@
 
 namespace {
 
-using f4 = float __attribute__((ext_vector_type(4)));
-using f16v = float __attribute__((ext_vector_type(16)));
-using bf8 = __bf16 __attribute__((ext_vector_type(8)));
-using bf4 = __bf16 __attribute__((ext_vector_type(4)));
-
-constexpr int kBK = 16;     // k per stage = one 32x32x16 MFMA step
-
-__device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ int xcd_remap(int id, int nwg) {
-  const int q = nwg / 8, r = nwg % 8, xcd = id % 8;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
-}
-
-// x -> (h, m, l); non-finite x keeps h = x (inf / nan propagate as in fp32), m = l = 0
-__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
-  h = static_cast<__bf16>(x);
-  const float r1 = x - static_cast<float>(h);
-  m = static_cast<__bf16>(r1);
-  const float r2 = r1 - static_cast<float>(m);
-  l = static_cast<__bf16>(r2);
-  if (!isfinite(x)) { m = static_cast<__bf16>(0.f); l = static_cast<__bf16>(0.f); }
-}
+using namespace m2f_x3;
 
 enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4 };
 
@@ -83,7 +60,6 @@ enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4 };
 // Epilogue: each 32x32 accumulator tile goes through a per-wave LDS image and leaves as float4 rows, with
 // the bias / ReLU / ReLU-mask applied on the way (mask reads coalesced like the stores).
 // ---------------------------------------------------------------------------------------------------
-__device__ __forceinline__ int swz(int n) { return (n >> 3) & 1; }  // half swap of B row n
 
 __global__ void __launch_bounds__(256) x3_presplit(const float* __restrict__ B, int64_t ldb, int b_kn, int N, int K,
                                                    int NP, int nchunks, __bf16* __restrict__ Bs) {

@@ -1,0 +1,51 @@
+// Device helpers of the x3 (three-way split-bf16, fp32-accurate) MFMA kernels: gemm_x3.hip, conv_x3.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace m2f_x3 {
+
+using f4 = float __attribute__((ext_vector_type(4)));
+using f16v = float __attribute__((ext_vector_type(16)));
+using bf8 = __bf16 __attribute__((ext_vector_type(8)));
+using bf4 = __bf16 __attribute__((ext_vector_type(4)));
+
+constexpr int kBK = 16;  // k per stage = one 32x32x16 MFMA step
+
+__device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// the six product terms of order <= 2^-16 of (ah + am + al) . (bh + bm + bl), small terms first
+__device__ __forceinline__ f16v mfma_x3(const bf8 (&a)[3], bf8 bh, bf8 bm, bf8 bl, f16v c) {
+  c = mfma(a[2], bh, c);  // al.bh
+  c = mfma(a[1], bm, c);  // am.bm
+  c = mfma(a[0], bl, c);  // ah.bl
+  c = mfma(a[1], bh, c);  // am.bh
+  c = mfma(a[0], bm, c);  // ah.bm
+  return mfma(a[0], bh, c);  // ah.bh
+}
+
+// bijective XCD-aware remap: consecutive logical ids land on the same XCD (blocks id, id+8, ... share one)
+__device__ __forceinline__ int xcd_remap(int id, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = id % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
+}
+
+// x -> (h, m, l) exactly (x = h + m + l to the last fp32 bit); non-finite x keeps h = x, m = l = 0
+__device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
+  h = static_cast<__bf16>(x);
+  const float r1 = x - static_cast<float>(h);
+  m = static_cast<__bf16>(r1);
+  const float r2 = r1 - static_cast<float>(m);
+  l = static_cast<__bf16>(r2);
+  if (!isfinite(x)) { m = static_cast<__bf16>(0.f); l = static_cast<__bf16>(0.f); }
+}
+
+// B images are rows of 16 bf16 (32 B) with the two 16-B halves swapped on rows whose bit 3 is set: the
+// dense image is then conflict-free for the 32x32x16 operand read (ds_read_b128 lane groups
+// {0-3,12-15,20-27}, ... cover all 64 banks once)
+__device__ __forceinline__ int swz(int n) { return (n >> 3) & 1; }
+
+}  // namespace m2f_x3

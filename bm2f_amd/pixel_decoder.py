@@ -22,7 +22,7 @@ from torch.nn import functional as F
 from torch.nn.init import normal_
 
 from .msda import MSDeformAttn, attach_host_shapes
-from . import linear_ops
+from . import conv_ops, linear_ops
 from .norm_ops import add_layernorm
 from .position_encoding import PositionEmbeddingSine
 from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill, configurable, get_norm
@@ -266,7 +266,8 @@ class MSDeformAttnPixelDecoder(nn.Module):
         srcs, pos = [], []
         for idx, f in enumerate(self.transformer_in_features[::-1]):
             x = features[f].float()
-            srcs.append(self.input_proj[idx](x))
+            proj = self.input_proj[idx]
+            srcs.append(proj[1](conv_ops.conv2d(x, proj[0])))   # 1x1 conv (x3 kernels) + GroupNorm
             pos.append(self.pe_layer(x))
 
         y, spatial_shapes, level_start_index = self.transformer(srcs, pos)
@@ -277,9 +278,9 @@ class MSDeformAttnPixelDecoder(nn.Module):
 
         for idx, f in enumerate(self.in_features[:self.num_fpn_levels][::-1]):
             x = features[f].float()
-            cur_fpn = self.lateral_convs[idx](x)
+            cur_fpn = conv_ops.conv_norm_act(x, self.lateral_convs[idx])
             y = cur_fpn + F.interpolate(out[-1], size=cur_fpn.shape[-2:], mode="bilinear", align_corners=False)
-            out.append(self.output_convs[idx](y))
+            out.append(conv_ops.conv_norm_act(y, self.output_convs[idx]))
 
         multi_scale_features = out[:self.maskformer_num_feature_levels]
-        return self.mask_features(out[-1]), out[0], multi_scale_features
+        return conv_ops.conv_norm_act(out[-1], self.mask_features), out[0], multi_scale_features

@@ -205,6 +205,21 @@ int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, int64_t ldb, 
                       float* colsum, int M, int N1, int N2, void* workspace, int64_t workspace_bytes,
                       void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * fp32 convolutions on the x3 engine (NCHW, stride 1, 1x1 or 3x3 with "same" padding, no groups):
+ * the pixel decoder's input_proj / adapter / layer / mask_features convs (msdeformattn.py:213-292),
+ * replacing cuDNN/MIOpen calls of F.conv2d.  Needs channels % 16 == 0, H*W % 128 == 0, W % 8 == 0.
+ * m2f_conv_f32x3: mode 0 O[N][Co][H][W] = conv(I[N][Ci][H][W], W[Co][Ci][k][k]) (+ bias[Co]);
+ *                 mode 1 O[N][Ci][H][W] = input gradient of I = grad_out[N][Co][H][W] (no bias).
+ * m2f_conv_f32x3_wgrad: dW_tck[k*k][Ci][Co] (tap-major: the caller permutes to [Co][Ci][k][k]) and,
+ *                 if dbias, dbias[Co]; split over pixels, slabs summed in a fixed order.
+ * All three take m2f_conv_f32x3_workspace() bytes (16-byte aligned). */
+int m2f_conv_f32x3_workspace(int N, int Ci, int Co, int H, int W, int ksize, int64_t* workspace_bytes);
+int m2f_conv_f32x3(const float* I, const float* W, const float* bias, float* O, int N, int Ci, int Co, int H, int Wd,
+                   int ksize, int mode, void* workspace, int64_t workspace_bytes, void* stream);
+int m2f_conv_f32x3_wgrad(const float* grad_out, const float* I, float* dW_tck, float* dbias, int N, int Ci, int Co,
+                         int H, int Wd, int ksize, void* workspace, int64_t workspace_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

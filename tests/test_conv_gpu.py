@@ -1,0 +1,45 @@
+"""x3 fp32 convolutions (csrc/conv_x3.hip, conv_ops.py) against fp64 F.conv2d: forward, input, weight and
+bias gradients, for the pixel decoder's conv shapes (msdeformattn.py:213-292) at reduced batch/size."""
+import pytest
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from bm2f_amd import conv_ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("N,Ci,Co,H,W,k,bias", [(2, 256, 256, 32, 32, 3, False), (1, 256, 256, 16, 24, 3, True),
+                                                (2, 512, 256, 16, 16, 1, True), (1, 2048, 256, 8, 16, 1, True),
+                                                (3, 256, 256, 8, 16, 1, False), (1, 32, 48, 8, 16, 3, True)])
+def test_conv_x3_vs_fp64(device, N, Ci, Co, H, W, k, bias):
+    torch.manual_seed(Ci + Co + H)
+    conv = nn.Conv2d(Ci, Co, k, padding=k // 2, bias=bias).to(device)
+    x = torch.randn(N, Ci, H, W, device=device, requires_grad=True)
+    assert conv_ops.eligible(x, conv)
+    y = conv_ops.conv2d(x, conv)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xd = x.detach().double().requires_grad_()
+    wd = conv.weight.detach().double().requires_grad_()
+    bd = conv.bias.detach().double().requires_grad_() if bias else None
+    yd = F.conv2d(xd, wd, bd, padding=k // 2)
+    yd.backward(g.double())
+    assert _rel(y, yd) < 2e-6
+    assert _rel(x.grad, xd.grad) < 2e-6
+    assert _rel(conv.weight.grad, wd.grad) < 2e-6
+    if bias:
+        assert _rel(conv.bias.grad, bd.grad) < 2e-6
+
+
+def test_conv_x3_fallback_shapes(device):
+    conv = nn.Conv2d(256, 256, 3, padding=1, stride=2).to(device)
+    x = torch.randn(1, 256, 16, 16, device=device)
+    assert not conv_ops.eligible(x, conv)
+    torch.testing.assert_close(conv_ops.conv2d(x, conv), conv(x))
