@@ -27,7 +27,8 @@ PIXEL_STD = (58.395, 57.120, 57.375)
 
 
 class FrozenBNConv(nn.Module):
-    """conv (no bias) + FrozenBatchNorm2d, applied as one conv with folded weights."""
+    """conv (no bias) + FrozenBatchNorm2d: the BN scale is folded into the conv weights on the fly, the BN
+    shift is returned for the fused bias(+shortcut)+ReLU that follows (:func:`bias_act`)."""
 
     def __init__(self, cin, cout, k, stride=1, padding=0):
         super().__init__()
@@ -39,11 +40,50 @@ class FrozenBNConv(nn.Module):
         self.register_buffer("running_var", torch.ones(cout))
         self.eps = 1e-5
 
-    def forward(self, x):
+    def conv_shift(self, x):
+        """(conv(x) with the BN scale folded into the weights, per-channel BN shift)."""
         scale = self.weight * (self.running_var + self.eps).rsqrt()
         shift = self.bias - self.running_mean * scale
         w = self.conv.weight * scale.view(-1, 1, 1, 1)
-        return F.conv2d(x, w, shift, self.conv.stride, self.conv.padding)
+        return F.conv2d(x, w, None, self.conv.stride, self.conv.padding), shift
+
+    def forward(self, x):
+        y, shift = self.conv_shift(x)
+        return y + shift.view(1, -1, 1, 1).to(y.dtype)
+
+
+class _BiasAct(torch.autograd.Function):
+    """y = relu(x + r + bias[c]) in place on x (bias: frozen BN shift, no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, r, bias):
+        from . import _native
+        code = {torch.bfloat16: 2, torch.float32: 0}[x.dtype]
+        _native.call("m2f_bias_act_nchw", x.data_ptr(), r.data_ptr() if r is not None else None,
+                     bias.data_ptr(), x.shape[0], x.shape[1], x.shape[2] * x.shape[3], code,
+                     torch.cuda.current_stream(x.device).cuda_stream)
+        ctx.mark_dirty(x)
+        ctx.save_for_backward(x)
+        ctx.has_r = r is not None
+        return x
+
+    @staticmethod
+    def backward(ctx, grad):
+        (y,) = ctx.saved_tensors
+        g = torch.ops.aten.threshold_backward(grad, y, 0)  # ReLU's own backward: one pass
+        return g, (g if ctx.has_r else None), None
+
+
+def bias_act(x, bias, residual=None):
+    """relu(x + residual + bias[c]) (NCHW); one fused pass on a HIP device."""
+    hw = x.shape[2] * x.shape[3]
+    if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.is_contiguous() and hw % 8 == 0
+            and (residual is None or (residual.is_contiguous() and residual.dtype == x.dtype))):
+        return _BiasAct.apply(x, residual, bias.float().contiguous())
+    y = x + bias.view(1, -1, 1, 1).to(x.dtype)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y)
 
 
 class Bottleneck(nn.Module):
@@ -55,11 +95,15 @@ class Bottleneck(nn.Module):
         self.conv3 = FrozenBNConv(cb, cout, 1, 1)
 
     def forward(self, x):
-        out = F.relu_(self.conv1(x))
-        out = F.relu_(self.conv2(out))
-        out = self.conv3(out)
-        sc = self.shortcut(x) if self.shortcut is not None else x
-        return F.relu_(out + sc)
+        out = bias_act(*self.conv1.conv_shift(x))
+        out = bias_act(*self.conv2.conv_shift(out))
+        out, shift = self.conv3.conv_shift(out)
+        if self.shortcut is not None:
+            sc, sc_shift = self.shortcut.conv_shift(x)
+            shift = shift + sc_shift
+        else:
+            sc = x
+        return bias_act(out, shift, sc)
 
 
 class ResNet50(nn.Module):
@@ -82,7 +126,7 @@ class ResNet50(nn.Module):
         return {k: ShapeSpec(channels=ch[k], stride=st[k]) for k in self.stage_names}
 
     def forward(self, x):
-        x = F.relu_(self.stem(x))
+        x = bias_act(*self.stem.conv_shift(x))
         x = F.max_pool2d(x, kernel_size=3, stride=2, padding=1)
         out = {}
         for name in self.stage_names:
