@@ -329,7 +329,7 @@ template <int P, int LT, bool FUSED, int TPB>
 __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
-    float* __restrict__ gloc, float* __restrict__ gattn) {
+    float* __restrict__ gloc, float* __restrict__ gattn, float* __restrict__ scratch, int* __restrict__ wtab) {
   constexpr int D = 32;
   constexpr int PB = TPB <= 768 ? 4 : 1;  // points per gather batch (1024 threads: 128 VGPRs, no room)
   static_assert(P % PB == 0, "batches cover the points");
@@ -490,6 +490,19 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
   const int rows_total = ts.woff[L];
   const float fscale = ts.scale;
   for (int i = tid; i < rows_total; i += blockDim.x) head[i] = -1;
+  const int64_t wg = (static_cast<int64_t>(n) * M + m) * (geo.nty * geo.ntx) + tile;
+  if (scratch && tid == 0) {  // the window of this workgroup, for the combine pass
+    int* wt = wtab + wg * kWtab;
+    for (int l = 0; l < kTileMaxL; ++l) {
+      const bool on = l < L;
+      wt[5 * l + 0] = on ? ts.wy0[l] : 0;
+      wt[5 * l + 1] = on ? ts.wx0[l] : 0;
+      wt[5 * l + 2] = on ? ts.wh[l] : 0;
+      wt[5 * l + 3] = on ? ts.ww[l] : 0;
+      wt[5 * l + 4] = on ? ts.woff[l] : 0;
+    }
+    wt[20] = rows_total;
+  }
   __syncthreads();
 
   // ---- phase 2: gradients; grad_value into the windows --------------------------------------------
@@ -631,26 +644,36 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
   }
   __syncthreads();
 
-  // ---- phase 3: per window row, an 8-lane group walks its list and adds the row to HBM once -------
+  // ---- phase 3: per window row, an 8-lane group walks its list; the row goes to HBM once: as a partial
+  // row in this workgroup's scratch slot (plain stores, summed by msda_gv_combine) or, without scratch,
+  // added to grad_value with row-contiguous atomics -----------------------------------------------------
   if (!(geo.ablate & 2)) {
     const double unscale = ts.unscale;
     const float inv_lp4 = 1.f / static_cast<float>(LP4);
     const int ngroups = blockDim.x >> 3;
     for (int row = tid >> 3; row < rows_total; row += ngroups) {
       int id = head[row];
-      if (id < 0) continue;  // the 8 lanes of a group share the row
+      if (id < 0 && !scratch) continue;  // the 8 lanes of a group share the row
       // every term is an integer (fixed point, |sum| < 2^52): the f64 adds are exact, so the result does
       // not depend on the list order
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-      while (id != 0xffff) {
-        const float c = coef[id] * fscale;
-        const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
-        const f4 g = *reinterpret_cast<const f4*>(gsh + q * D + 4 * j);
-        a0 += static_cast<double>(rintf(c * g.x));
-        a1 += static_cast<double>(rintf(c * g.y));
-        a2 += static_cast<double>(rintf(c * g.z));
-        a3 += static_cast<double>(rintf(c * g.w));
-        id = nxt[id];
+      if (id >= 0) {
+        while (id != 0xffff) {
+          const float c = coef[id] * fscale;
+          const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
+          const f4 g = *reinterpret_cast<const f4*>(gsh + q * D + 4 * j);
+          a0 += static_cast<double>(rintf(c * g.x));
+          a1 += static_cast<double>(rintf(c * g.y));
+          a2 += static_cast<double>(rintf(c * g.z));
+          a3 += static_cast<double>(rintf(c * g.w));
+          id = nxt[id];
+        }
+      }
+      if (scratch) {
+        const f4 v = {static_cast<float>(a0 * unscale), static_cast<float>(a1 * unscale),
+                      static_cast<float>(a2 * unscale), static_cast<float>(a3 * unscale)};
+        *reinterpret_cast<f4*>(scratch + (wg * geo.wrows + row) * D + 4 * j) = v;
+        continue;
       }
       int l = 0;
       while (row >= ts.woff[l + 1]) ++l;
@@ -663,6 +686,40 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
       if (a3 != 0.0) atomicAdd(dst + 3, static_cast<float>(a3 * unscale));
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Combine pass of the tiled backward with scratch: every grad_value row (n, pixel s, head m) adds the
+// partial rows that the workgroups whose windows cover it left in scratch, in a fixed neighbour order
+// (deterministic), to what the out-of-window atomics put there.  One 8-lane group per row, float4 per
+// lane; only tiles within the halo of the pixel can cover it.
+// ------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) msda_gv_combine(const float* __restrict__ scratch, const int* __restrict__ wtab,
+                                                       TileGeom geo, int S, int M, float* __restrict__ gvalue) {
+  constexpr int D = 32;
+  const int s = blockIdx.x * 32 + (threadIdx.x >> 3), j = threadIdx.x & 7;
+  const int m = blockIdx.y, n = blockIdx.z;
+  if (s >= S) return;
+  int l = 0;
+  while (l + 1 < geo.L && s >= geo.start[l + 1]) ++l;
+  const int H = geo.H[l], W = geo.W[l];
+  const int y = (s - geo.start[l]) / W, x = (s - geo.start[l]) % W;
+  const int h = geo.max_halo;
+  const int ty0 = tile_of(max(y - h, 0), H, geo.nty), ty1 = tile_of(min(y + h, H - 1), H, geo.nty);
+  const int tx0 = tile_of(max(x - h, 0), W, geo.ntx), tx1 = tile_of(min(x + h, W - 1), W, geo.ntx);
+  const int64_t wg0 = (static_cast<int64_t>(n) * M + m) * (geo.nty * geo.ntx);
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int ty = ty0; ty <= ty1; ++ty)
+    for (int tx = tx0; tx <= tx1; ++tx) {
+      const int64_t wg = wg0 + ty * geo.ntx + tx;
+      const int* wt = wtab + wg * kWtab + 5 * l;
+      const int wy0 = wt[0], wx0 = wt[1], wh = wt[2], ww = wt[3], woff = wt[4];
+      if (y < wy0 || y >= wy0 + wh || x < wx0 || x >= wx0 + ww) continue;
+      const int row = woff + (y - wy0) * ww + (x - wx0);
+      acc += *reinterpret_cast<const f4*>(scratch + (wg * geo.wrows + row) * D + 4 * j);
+    }
+  f4* dst = reinterpret_cast<f4*>(gvalue + ((static_cast<int64_t>(n) * S + s) * M + m) * D + 4 * j);
+  *dst = *dst + acc;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -834,6 +891,12 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     qt += th * tw;
   }
   geo.max_qt = qt;
+  int wrows = 0;  // the largest window any workgroup can choose: tile +- max_halo, clipped to the level
+  for (int l = 0; l < d.L; ++l) {
+    const int th = (geo.H[l] + geo.nty - 1) / geo.nty, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx;
+    wrows += std::min(geo.H[l], th + 2 * geo.max_halo) * std::min(geo.W[l], tw + 2 * geo.max_halo);
+  }
+  geo.wrows = std::min(wrows, geo.max_rows);
   const int lp4 = d.L * d.P * 4;
   if (own > geo.max_rows || static_cast<int64_t>(qt) * lp4 >= 0xffff) return false;
   lds = static_cast<size_t>(qt) * 32 * 4 + static_cast<size_t>(qt) * lp4 * 4 +
@@ -844,7 +907,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
 template <int P, int LT, bool FUSED, int TPB>
 void launch_tiled_t(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
                     const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                    hipStream_t st) {
+                    hipStream_t st, float* scratch, int* wtab) {
   static bool attr = false;  // one flag per instantiation
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<P, LT, FUSED, TPB>),
@@ -852,20 +915,25 @@ void launch_tiled_t(const float* value, const float* loc, const float* attn, con
     attr = true;
   }
   const dim3 grid(geo.nty * geo.ntx, d.M, d.N);
-  msda_bwd_f32_tiled<P, LT, FUSED, TPB><<<grid, threads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+  msda_bwd_f32_tiled<P, LT, FUSED, TPB><<<grid, threads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga,
+                                                                    scratch, wtab);
+  if (scratch) {
+    const dim3 cgrid((d.S + 31) / 32, d.M, d.N);
+    msda_gv_combine<<<cgrid, 256, 0, st>>>(scratch, wtab, geo, d.S, d.M, gv);
+  }
 }
 
 // the register budget follows the block size: <= 512 threads get 2 waves/SIMD worth, 768 three, 1024 four
 template <int P, int LT, bool FUSED>
 void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
                   const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                  hipStream_t st) {
+                  hipStream_t st, float* scratch = nullptr, int* wtab = nullptr) {
   if (threads <= 512)
-    launch_tiled_t<P, LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st);
+    launch_tiled_t<P, LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st, scratch, wtab);
   else if (threads <= 768)
-    launch_tiled_t<P, LT, FUSED, 768>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st);
+    launch_tiled_t<P, LT, FUSED, 768>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st, scratch, wtab);
   else
-    launch_tiled_t<P, LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st);
+    launch_tiled_t<P, LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st, scratch, wtab);
 }
 
 bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,
@@ -1016,11 +1084,38 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
   return m2f::check_launch(fn);
 }
 
+namespace {
+// scratch partial rows (wrows x 32 fp32 per workgroup) + window tables, 256-byte aligned pieces
+void fused_ws_layout(const Dims& d, const TileGeom& geo, int64_t& scratch_bytes, int64_t& total) {
+  const int64_t nwg = static_cast<int64_t>(geo.nty) * geo.ntx * d.M * d.N;
+  scratch_bytes = (nwg * geo.wrows * 32 * 4 + 255) / 256 * 256;
+  total = scratch_bytes + (nwg * kWtab * 4 + 255) / 256 * 256;
+}
+}  // namespace
+
+extern "C" int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, int batch, int spatial_size,
+                                            int num_heads, int channels, int num_levels, int num_point,
+                                            int64_t* workspace_bytes) {
+  const char* fn = "m2f_msda_fused_bwd_workspace";
+  const Dims d{batch, spatial_size, num_heads, channels, num_levels, spatial_size, num_point};
+  if (!host_spatial_shapes || !workspace_bytes) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  TileGeom geo;
+  size_t lds;
+  int threads;
+  if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout", fn);
+  int64_t sb, total;
+  fused_ws_layout(d, geo, sb, total);
+  *workspace_bytes = total;
+  return m2f::ok();
+}
+
 extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
                                       int64_t ref_batch_stride, const int64_t* host_spatial_shapes,
                                       const float* grad_output, int batch, int spatial_size, int num_heads,
                                       int channels, int num_levels, int num_query, int num_point,
-                                      float* grad_value, float* grad_proj, void* stream) {
+                                      float* grad_value, float* grad_proj, void* workspace, int64_t workspace_bytes,
+                                      void* stream) {
   const char* fn = "m2f_msda_fused_bwd_f32";
   const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
   TileGeom geo0;
@@ -1033,16 +1128,27 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
   int threads;
   if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout (num_query == spatial_size)", fn);
+  float* scratch = nullptr;
+  int* wtab = nullptr;
+  if (workspace) {  // partial rows + combine pass (no flush atomics); without a workspace: atomic flush
+    int64_t sb, total;
+    fused_ws_layout(d, geo, sb, total);
+    if (workspace_bytes < total || !m2f::aligned(workspace, 16))
+      return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld bytes", fn, static_cast<long long>(workspace_bytes),
+                       static_cast<long long>(total));
+    scratch = static_cast<float*>(workspace);
+    wtab = reinterpret_cast<int*>(static_cast<char*>(workspace) + sb);
+  }
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t gv_bytes = static_cast<size_t>(d.N) * d.S * d.M * d.D * sizeof(float);
   hipError_t e = hipMemsetAsync(grad_value, 0, gv_bytes, st);
   if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
   const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
   switch (d.L) {
-    case 1: launch_tiled<4, 1, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st); break;
-    case 2: launch_tiled<4, 2, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st); break;
-    case 3: launch_tiled<4, 3, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st); break;
-    default: launch_tiled<4, 4, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st); break;
+    case 1: launch_tiled<4, 1, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st, scratch, wtab); break;
+    case 2: launch_tiled<4, 2, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st, scratch, wtab); break;
+    case 3: launch_tiled<4, 3, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st, scratch, wtab); break;
+    default: launch_tiled<4, 4, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st, scratch, wtab); break;
   }
   return m2f::check_launch(fn);
 }

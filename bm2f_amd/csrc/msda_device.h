@@ -59,10 +59,21 @@ struct TileGeom {
   int max_halo;   // windows never extend more than this many pixels past the tile
   int max_qt;     // queries of the largest tile (sizes the LDS carve-up)
   int bbox;       // 1: shrink the window to the bounding box of the touched corners (phase 0 pass)
+  int wrows;      // scratch rows per workgroup (>= any window) when partial rows go to a scratch buffer
   int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no list inserts, 2 no flush, 4 no spill atomics
 };
 
 __device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
+
+// the tile t with tile_lo(t) <= y < tile_lo(t + 1)
+__device__ __forceinline__ int tile_of(int y, int n, int nt) {
+  int t = (y * nt + nt - 1) / n;
+  while (t > 0 && tile_lo(t, n, nt) > y) --t;
+  while (t + 1 < nt && tile_lo(t + 1, n, nt) <= y) ++t;
+  return t;
+}
+
+constexpr int kWtab = 24;  // window table ints per workgroup: (wy0, wx0, wh, ww, woff) x 4 levels, rows
 
 // Sum over each aligned group of 8 lanes with DPP moves (VALU, no LDS crossbar): xor 1, xor 2 within
 // quads, then row_half_mirror (lane i <-> 7-i) pairs the two quads.

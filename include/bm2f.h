@@ -109,11 +109,16 @@ int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int proj_ld, c
                            int spatial_size, int num_heads, int channels, int num_levels, int num_query,
                            int num_point, float* output, void* stream);
 
+/* workspace (optional, m2f_msda_fused_bwd_workspace() bytes, 16-byte aligned): with it every workgroup
+ * leaves its window's grad_value partial rows in the workspace and a combine pass adds them in a fixed
+ * order (plain stores, deterministic); without it (NULL) the rows are added with float atomics. */
+int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, int batch, int spatial_size, int num_heads,
+                                 int channels, int num_levels, int num_point, int64_t* workspace_bytes);
 int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
                            int64_t ref_batch_stride, const int64_t* host_spatial_shapes,
                            const float* grad_output, int batch, int spatial_size, int num_heads, int channels,
                            int num_levels, int num_query, int num_point, float* grad_value, float* grad_proj,
-                           void* stream);
+                           void* workspace, int64_t workspace_bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Masked-attention decoder (mask2former_transformer_decoder.py).

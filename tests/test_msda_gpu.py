@@ -263,3 +263,41 @@ def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5)
     for a, b in zip(grads[0], grads[1]):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * max(b.abs().max().item(), 1e-6))
+
+
+@pytest.mark.parametrize("shapes,halo", [([(4, 4), (8, 8), (16, 16)], 8), ([(6, 10), (12, 20), (24, 40)], 3),
+                                         ([(16, 16), (32, 32), (64, 64)], 8)])
+def test_fused_backward_scratch_combine(device, monkeypatch, shapes, halo):
+    """Partial rows in scratch + the ordered combine pass == the atomic flush, and bitwise repeatable when
+    every sample lands in a window (halo 8 here; with halo 3 some go through fp32 atomics)."""
+    from bm2f_amd.msda import MSDeformAttn, attach_host_shapes
+    monkeypatch.setenv("M2F_MSDA_HALO", str(halo))
+    torch.manual_seed(1)
+    L = len(shapes)
+    m = MSDeformAttn(256, L, 8, 4).to(device)
+    with torch.no_grad():
+        m.sampling_offsets.weight.normal_(0, 0.05)
+        m.attention_weights.weight.normal_(0, 0.05)
+    st = torch.tensor(shapes, dtype=torch.int64, device=device)
+    attach_host_shapes(st, shapes)
+    lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
+    S = int(st.prod(1).sum())
+    refs = []
+    for h, w in shapes:
+        ys, xs = torch.meshgrid(torch.linspace(0.5, h - 0.5, h), torch.linspace(0.5, w - 0.5, w), indexing="ij")
+        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
+    ref = torch.cat(refs, 0).to(device)[None, :, None, :].expand(2, S, L, 2)
+    src = torch.randn(2, S, 256, device=device)
+    grads = []
+    for scratch in ("1", "1", "0"):
+        monkeypatch.setenv("M2F_MSDA_SCRATCH", scratch)
+        m.zero_grad()
+        x = src.clone().requires_grad_()
+        out = m(x, ref, x, st, lsi)
+        out.backward(torch.ones_like(out) * 0.01 + out.detach() * 0.1)
+        grads.append([x.grad.clone()] + [p.grad.clone() for p in m.parameters()])
+    if halo == 8:
+        for a, b in zip(grads[0], grads[1]):
+            assert torch.equal(a, b)
+    for a, b in zip(grads[0], grads[2]):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * max(b.abs().max().item(), 1e-6))
