@@ -540,8 +540,10 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
       float2 rf = make_float2(0.f, 0.f);
       if constexpr (FUSED) rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
       // points in batches of PB: every corner load of a batch is issued before any of its math, so a
-      // wave keeps 4*PB row gathers in flight (the kernel is gather-latency bound)
-#pragma unroll
+      // wave keeps 4*PB row gathers in flight (the kernel is gather-latency bound).  With PB = 1 (the
+      // 128-VGPR budget of 1024-thread blocks) the point loop stays rolled: unrolled it spilled
+      constexpr int PUNROLL = PB == 1 ? 1 : P / PB;
+#pragma unroll PUNROLL
       for (int p0 = 0; p0 < P; p0 += PB) {
         Corners kb[PB];
         float ab[PB];
