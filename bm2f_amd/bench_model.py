@@ -12,6 +12,7 @@ function, one op fewer per conv).  Optimizer: AdamW + full-model grad-norm clipp
 """
 from __future__ import annotations
 
+import os
 import types
 
 import torch
@@ -59,8 +60,9 @@ class _BiasAct(torch.autograd.Function):
     def forward(ctx, x, r, bias):
         from . import _native
         code = {torch.bfloat16: 2, torch.float32: 0}[x.dtype]
+        cl = 0 if x.is_contiguous() else 1
         _native.call("m2f_bias_act_nchw", x.data_ptr(), r.data_ptr() if r is not None else None,
-                     bias.data_ptr(), x.shape[0], x.shape[1], x.shape[2] * x.shape[3], code,
+                     bias.data_ptr(), x.shape[0], x.shape[1], x.shape[2] * x.shape[3], code, cl,
                      torch.cuda.current_stream(x.device).cuda_stream)
         ctx.mark_dirty(x)
         ctx.save_for_backward(x)
@@ -77,8 +79,12 @@ class _BiasAct(torch.autograd.Function):
 def bias_act(x, bias, residual=None):
     """relu(x + residual + bias[c]) (NCHW); one fused pass on a HIP device."""
     hw = x.shape[2] * x.shape[3]
-    if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.is_contiguous() and hw % 8 == 0
-            and (residual is None or (residual.is_contiguous() and residual.dtype == x.dtype))):
+    cl = torch.channels_last
+    ok = ((x.is_contiguous() and hw % 8 == 0 and (residual is None or residual.is_contiguous()))
+          or (x.is_contiguous(memory_format=cl) and x.shape[1] % 8 == 0
+              and (residual is None or residual.is_contiguous(memory_format=cl))))
+    if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and ok
+            and (residual is None or residual.dtype == x.dtype)):
         return _BiasAct.apply(x, residual, bias.float().contiguous())
     y = x + bias.view(1, -1, 1, 1).to(x.dtype)
     if residual is not None:
@@ -169,6 +175,10 @@ class MaskFormerR50(nn.Module):
         self.sem_seg_head = MaskFormerHead(cfg, self.backbone.output_shape())
         self.register_buffer("pixel_mean", torch.tensor(PIXEL_MEAN).view(-1, 1, 1), False)
         self.register_buffer("pixel_std", torch.tensor(PIXEL_STD).view(-1, 1, 1), False)
+        # backbone memory format: NHWC lets MIOpen run its NHWC kernels without NCHW<->NHWC transposes
+        self.channels_last = os.environ.get("M2F_CHANNELS_LAST", "0") == "1"
+        if self.channels_last:
+            self.backbone.to(memory_format=torch.channels_last)
 
     @property
     def pixel_decoder(self):
@@ -180,6 +190,8 @@ class MaskFormerR50(nn.Module):
 
     def forward(self, images):
         x = (images - self.pixel_mean) / self.pixel_std
+        if self.channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
         return self.sem_seg_head(self.backbone(x))
 
 

@@ -226,10 +226,11 @@ int m2f_conv_f32x3_wgrad(const float* grad_out, const float* I, float* dW_tck, f
                          int H, int Wd, int ksize, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Fused per-channel bias (+ residual) + ReLU in place over an NCHW activation (dtype M2F_BF16 or
- * M2F_F32): x = max(x + residual + bias[c], 0).  The benchmark backbone's FrozenBN shift + shortcut +
- * ReLU in one pass (not on the reference's hot path).  H*W % 8 (bf16) / % 4 (fp32), 16-byte aligned. */
+ * M2F_F32), memory NCHW or (channels_last != 0) NHWC: x = max(x + residual + bias[c], 0).  The
+ * benchmark backbone's FrozenBN shift + shortcut + ReLU in one pass (not on the reference's hot path).
+ * H*W (NCHW) or C (NHWC) % 8 (bf16) / % 4 (fp32), 16-byte aligned. */
 int m2f_bias_act_nchw(void* x, const void* residual, const float* bias, int64_t N, int C, int64_t HW, int dtype,
-                      void* stream);
+                      int channels_last, void* stream);
 
 #ifdef __cplusplus
 }
