@@ -305,7 +305,7 @@ struct TileState {
   int bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
   unsigned int gmax, amax;
   float scale;
-  double unscale;
+  double unscale, rscale;  // rscale = 2^e: fp32 partial sums re-expressed in fixed-point units
   int wy0[kTileMaxL], wx0[kTileMaxL], wh[kTileMaxL], ww[kTileMaxL], woff[kTileMaxL + 1];
   int qc[kTileMaxL + 1], qy0[kTileMaxL], qx0[kTileMaxL], qw[kTileMaxL];
 };
@@ -460,6 +460,7 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
     const int e = use_lds ? 52 - cnt_bits - static_cast<int>(ceilf(log2f(bound))) : 0;
     ts.scale = use_lds ? ldexpf(1.f, e) : 0.f;
     ts.unscale = use_lds ? ldexp(1.0, -e) : 0.0;
+    ts.rscale = use_lds ? ldexp(1.0, e) : 0.0;
     for (int halo = use_lds ? geo.max_halo : -1; halo >= 0; --halo) {
       int total = 0;
       for (int l = 0; l < L; ++l) {
@@ -659,7 +660,7 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
       // every term is an integer (fixed point, |sum| < 2^52): the f64 adds are exact, so the result does
       // not depend on the list order
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-      if (id >= 0) {
+      if (id >= 0 && geo.exact) {
         while (id != 0xffff) {
           const float c = coef[id] * fscale;
           const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
@@ -670,11 +671,29 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
           a3 += static_cast<double>(rintf(c * g.w));
           id = nxt[id];
         }
+      } else if (id >= 0) {
+        // fp32 accumulation in list order: as accurate as the reference's fp32 atomics and, like them,
+        // not bitwise repeatable (M2F_MSDA_DETERMINISTIC=0; the default is the exact branch above)
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+        while (id != 0xffff) {
+          const float c = coef[id];
+          const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
+          acc += c * *reinterpret_cast<const f4*>(gsh + q * D + 4 * j);
+          id = nxt[id];
+        }
+        a0 = static_cast<double>(acc.x) * ts.rscale;
+        a1 = static_cast<double>(acc.y) * ts.rscale;
+        a2 = static_cast<double>(acc.z) * ts.rscale;
+        a3 = static_cast<double>(acc.w) * ts.rscale;
       }
       if (scratch) {
         const f4 v = {static_cast<float>(a0 * unscale), static_cast<float>(a1 * unscale),
                       static_cast<float>(a2 * unscale), static_cast<float>(a3 * unscale)};
         *reinterpret_cast<f4*>(scratch + (wg * geo.wrows + row) * D + 4 * j) = v;
+        continue;
+      }
+      if (geo.ablate & 8) {  // timing experiment: walk the lists, skip the HBM adds
+        if (a0 == 12345.0) gvalue[0] = 0.f;
         continue;
       }
       int l = 0;
@@ -884,6 +903,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   geo.max_halo = env_int("M2F_MSDA_HALO", 8);
   geo.ablate = env_int("M2F_MSDA_ABLATE", 0);
   geo.bbox = env_int("M2F_MSDA_BBOX", 1);
+  geo.exact = env_int("M2F_MSDA_DETERMINISTIC", 1);  // default: bitwise-repeatable gradients (+0.17 ms per launch)
   // the index budget must hold every level's share of one tile (halo 0); tiles span at most
   // ceil(n / nt) pixels per axis (tile_lo)
   int own = 0, qt = 0;

@@ -60,7 +60,9 @@ struct TileGeom {
   int max_qt;     // queries of the largest tile (sizes the LDS carve-up)
   int bbox;       // 1: shrink the window to the bounding box of the touched corners (phase 0 pass)
   int wrows;      // scratch rows per workgroup (>= any window) when partial rows go to a scratch buffer
-  int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no list inserts, 2 no flush, 4 no spill atomics
+  int exact;      // 1: exact integer-valued f64 row sums (bitwise repeatable); 0: fp32 sums in list order
+  int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no list inserts, 2 no phase 3, 4 no spill
+                  // atomics, 8 phase 3 without its HBM adds
 };
 
 __device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
