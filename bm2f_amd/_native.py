@@ -51,6 +51,13 @@ _SIGNATURES = {
     "m2f_add_layernorm_workspace": [_l, _i, _p],
     "m2f_add_layernorm_fwd_f32": [_p, _p, _p, _p, _l, _i, _f, _p, _p, _p, _p],
     "m2f_add_layernorm_bwd_f32": [_p, _p, _p, _p, _p, _p, _l, _i, _p, _p, _p, _p, _l, _p],
+    "m2f_lsap_batched": [_p, _i, _i, _i, _l, _p, _p, _p, _p, _p],
+    "m2f_pairwise_tiles": [_i, _i],
+    "m2f_pairwise_rows": [_p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p],
+    "m2f_pairwise_rows_bwd": [_p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
+    "m2f_threshold_bits": [_p, _i, _l, _f, _p, _p],
+    "m2f_weaksup_lab": [_p, _i, _i, _i, _i, _p, _p],
+    "m2f_color_similarity": [_p, _p, _i, _i, _i, _i, _p, _p],
 }
 
 

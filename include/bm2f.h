@@ -232,6 +232,48 @@ int m2f_conv_f32x3_wgrad(const float* grad_out, const float* I, float* dW_tck, f
 int m2f_bias_act_nchw(void* x, const void* residual, const float* bias, int64_t N, int C, int64_t HW, int dtype,
                       int channels_last, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Weak-supervision criterion (SUP_TYPE "mask_projection_and_pairwise"), SURVEY 8(f) ranks 1 and 3.
+ * ------------------------------------------------------------------------------------------- */
+
+/* Batched linear sum assignment, replacing scipy.optimize.linear_sum_assignment on C.cpu()
+ * (mask2former/modeling/matcher.py:309-311; same shortest-augmenting-path algorithm and tie rule,
+ * in fp64).  Problem b is cost[b*batch_stride + r*max_cols + c] for r < rows[b], c < cols[b]
+ * (cols == NULL: max_cols).  match[b*max_rows + r] = matched column or -1.  status[b] = 0 ok,
+ * 1 infeasible, 2 too large, 3 NaN / -inf entry (scipy raises ValueError for 1 and 3).
+ * Limits per problem: min(rows, cols) <= 256, max(rows, cols) <= 1024.  One wavefront per problem. */
+int m2f_lsap_batched(const float* cost, int batch, int max_rows, int max_cols, int64_t batch_stride,
+                     const int* rows, const int* cols, int* match, int* status, void* stream);
+
+/* Pairwise affinity term s(p,q) = -log(sig(x_p)sig(x_q) + sig(-x_p)sig(-x_q)) over the 8 dilated
+ * neighbours of each pixel (criterion.py:156-181, matcher.py:48-83, weaksup_utils.py:7-31; zero
+ * padding outside the image as F.unfold).  Row r reads mask x[x_row[r]] (H, W) fp32, neighbour
+ * bits[t_row[r]] (H*W bytes, bit k = similarity_k >= thresh) and weight box[box_row[r]] (or 1).
+ * NULL index arrays mean identity.  mode 0: out[r, p] = sum_k bit_k s_k;  mode 1: per-tile
+ * partials out[r, t] = sum_p w sum_k bit_k s_k and out_den[r, t] = sum_p w popcount(bits), with
+ * t < m2f_pairwise_tiles(H, W);  mode 2: out[r, k, p] = s_k (bits unused).  1 <= dilation <= 8,
+ * R <= 65535. */
+int m2f_pairwise_tiles(int H, int W);
+int m2f_pairwise_rows(const float* x, const int* x_row, int R, int H, int W, int dilation, const uint8_t* bits,
+                      const int* t_row, const float* box, const int* box_row, int mode, float* out, float* out_den,
+                      void* stream);
+/* Gradient of sum_r grad_scale[r] * (mode-1 numerator of row r) w.r.t. x[x_row[r]], written to
+ * grad[r] (R, H, W) (not accumulated). */
+int m2f_pairwise_rows_bwd(const float* x, const int* x_row, int R, int H, int W, int dilation, const uint8_t* bits,
+                          const int* t_row, const float* box, const int* box_row, const float* grad_scale,
+                          float* grad, void* stream);
+/* bits[n, p] = sum_k (sim[n, k, p] >= thr) << k for an (N, 8, HW) similarity. */
+int m2f_threshold_bits(const float* sim, int N, int64_t HW, float thr, uint8_t* bits, void* stream);
+
+/* Target preparation (maskformer_model.py:417-440): images (B, 3, Hp, Wp) fp32 in 0..255 (zero
+ * padded) -> lab (B, 3, Hp/stride, Wp/stride): stride x stride average pool, Tensor.byte(),
+ * skimage.color.rgb2lab (D65/2deg, double precision) -> fp32. */
+int m2f_weaksup_lab(const float* images, int B, int Hp, int Wp, int stride, float* lab, void* stream);
+/* sim (B, 8, h, w) = exp(-0.5 * ||lab_p - lab_q||) * mask_q, q = p + dilation * tap_k (0 outside),
+ * get_images_color_similarity (weaksup_utils.py:34-57) batched over images. */
+int m2f_color_similarity(const float* lab, const float* mask, int B, int h, int w, int dilation, float* sim,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif
