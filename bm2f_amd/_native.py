@@ -54,6 +54,7 @@ _SIGNATURES = {
     "m2f_lsap_batched": [_p, _i, _i, _i, _l, _p, _p, _p, _p, _p],
     "m2f_pairwise_tiles": [_i, _i],
     "m2f_pairwise_rows": [_p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p],
+    "m2f_pairwise_match_cost": [_p, _i, _i, _i, _i, _i, _p, _p, _p, _p, _i, _p, _p, _p, _p],
     "m2f_pairwise_rows_bwd": [_p, _p, _i, _i, _i, _i, _p, _p, _p, _p, _p, _p, _p],
     "m2f_threshold_bits": [_p, _i, _l, _f, _p, _p],
     "m2f_weaksup_lab": [_p, _i, _i, _i, _i, _p, _p],

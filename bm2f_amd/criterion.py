@@ -97,14 +97,31 @@ class WeakTargets:
             sim_all = torch.cat(self.sim_list)
             self.bits = ws.threshold_bits(sim_all, thresh) if sim_all.shape[0] else None       # (T, H, W)
         self.thresh = thresh
+        self.device = device
         self._padded = None
+        self._match_aux = None
 
     def padded(self):
         if self._padded is None:
             labels = pad_sequence([l.long() for l in self.labels], batch_first=True)                # (B, Gm)
-            box = pad_sequence(self.box_list, batch_first=True)                                  # (B, Gm, H, W)
+            box = pad_sequence(self.box_list, batch_first=True).contiguous()                     # (B, Gm, H, W)
             self._padded = (labels, box)
         return self._padded
+
+    def match_aux(self):
+        """Matcher-side constants of the targets: box axis projections, the pairwise normaliser
+        sum_p box_g(p) popcount(bits(p)) (shared similarity) and the per-image target counts."""
+        if self._match_aux is None:
+            _, box = self.padded()
+            B, Gm = box.shape[:2]
+            aux = {"box_x": box.amax(3), "box_y": box.amax(2), "gcount": ws.h2d(self.G, self.device),
+                   "extents": ws.box_extents(box)}
+            if self.shared:
+                k = torch.arange(8, device=box.device, dtype=torch.uint8)
+                tsum = ((self.bits.view(B, -1, 1) >> k) & 1).sum(-1, dtype=torch.float32)       # (B, HW)
+                aux["pair_den"] = (box.view(B, Gm, -1) * tsum[:, None]).sum(-1).clamp(min=1.0)  # (B, Gm)
+            self._match_aux = aux
+        return self._match_aux
 
 
 class HungarianMatcherProjPair(nn.Module):
@@ -137,28 +154,30 @@ class HungarianMatcherProjPair(nn.Module):
         B, Q = logits.shape[:2]
         H, W = masks.shape[-2:]
         labels, box = tg.padded()
+        aux = tg.match_aux()
         Gm = tg.Gm
         prob = logits.float().softmax(-1)
         c_class = -torch.gather(prob, 2, labels[:, None, :].expand(B, Q, Gm))
-        x = masks.float()
-        c_proj = _dice_cost(x.amax(3), box.amax(3)) + _dice_cost(x.amax(2), box.amax(2))
+        x = masks.float().contiguous()
+        pair = None
+        if tg.shared:
+            # one pass over the masks: pairwise numerators and both axis projections
+            num, sx, sy = ws.match_cost(x, tg.bits, box, aux["gcount"], self.pairwise_dilation, aux["extents"])
+            pair = num / aux["pair_den"][:, None, :]
+        else:
+            sx, sy = x.amax(3), x.amax(2)
+        c_proj = _dice_cost(sx, aux["box_x"]) + _dice_cost(sy, aux["box_y"])
         C = self.cost_class * c_class + self.cost_projection * c_proj
         if self.cost_pairwise != 0 and warm != 0:
-            C = C + self.cost_pairwise * (self._pairwise_cost(x, tg, box) * warm)
+            if pair is None:
+                pair = self._pairwise_cost_general(x, tg)
+            C = C + self.cost_pairwise * (pair * warm)
         return C
 
-    def _pairwise_cost(self, x, tg, box):
+    def _pairwise_cost_general(self, x, tg):
+        """Per-target similarity maps: s (Q, 8HW) x T (8HW, G) per image (matcher.py:23-35, :48-83)."""
         B, Q, H, W = x.shape
         d = self.pairwise_dilation
-        if tg.shared:
-            t_row = torch.arange(B * Q, device=x.device, dtype=torch.int32) // Q
-            A = ws.pairwise_map(x.reshape(B * Q, H, W).contiguous(), tg.bits, t_row, d).view(B, Q, H * W)
-            boxf = box.reshape(B, tg.Gm, H * W)
-            num = torch.bmm(A, boxf.transpose(1, 2))                                          # (B, Q, Gm)
-            k = torch.arange(8, device=x.device, dtype=torch.uint8)
-            tsum = ((tg.bits.view(B, H * W, 1) >> k) & 1).sum(-1, dtype=torch.float32)        # (B, HW)
-            den = torch.bmm(boxf, tsum[:, :, None])[..., 0]                                   # (B, Gm)
-            return num / den.clamp(min=1.0)[:, None, :]
         out = x.new_zeros((B, Q, tg.Gm))
         for b in range(B):
             G = tg.G[b]
@@ -227,6 +246,7 @@ class SetCriterionProjPair(nn.Module):
         self.check_matching = os.environ.get("M2F_LSAP_CHECK", "1") != "0"
         self._tg = self._tg_key = None
         self._status = []
+        self._gathered = {}
 
     # -- losses --------------------------------------------------------------------------------------
     def loss_labels(self, outputs, targets, indices, num_masks):
@@ -239,9 +259,16 @@ class SetCriterionProjPair(nn.Module):
         return {"loss_ce": F.cross_entropy(src_logits.transpose(1, 2), target_classes, self.empty_weight)}
 
     def _matched(self, outputs, targets, indices):
+        """Matched masks (N, H, W) and flat target rows, gathered once per head for both mask losses
+        (one IndexBackward, so one full-size gradient buffer per head)."""
         tg = self._targets(targets, outputs["pred_masks"].device)
+        key = (id(outputs["pred_masks"]), id(indices))
+        hit = self._gathered.get(key)
+        if hit is not None and hit[0] is outputs["pred_masks"] and hit[1] is indices:
+            return tg, hit[2], hit[3]
         src = outputs["pred_masks"][self._get_src_permutation_idx(indices)].float().contiguous()   # (N, H, W)
         flat = torch.cat([j + tg.offsets[b] for b, (_, j) in enumerate(indices)])                # target rows
+        self._gathered[key] = (outputs["pred_masks"], indices, src, flat)
         return tg, src, flat
 
     def loss_projection_masks(self, outputs, targets, indices, num_masks):
@@ -310,6 +337,7 @@ class SetCriterionProjPair(nn.Module):
         self._iter_host.step(self._iter)
         self._tg = self._tg_key = None
         self._status = []
+        self._gathered = {}
         try:
             outputs_without_aux = {k: v for k, v in outputs.items() if k != "aux_outputs"}
             indices = self._match(outputs_without_aux, targets)
@@ -336,6 +364,7 @@ class SetCriterionProjPair(nn.Module):
         finally:
             self._tg = self._tg_key = None
             self._status = []
+            self._gathered = {}
 
     def __repr__(self):
         head = "Criterion " + self.__class__.__name__

@@ -10,11 +10,11 @@
 //   loss          criterion.py:156-181 + 257-323: the same s on the matched masks, sum(s*T)/sum(T)/num_masks.
 //
 // The reference materialises (rows, 8, H, W) log-probability unfolds for each of them.  Here a workgroup
-// owns a 16x64 pixel tile of one mask row, stages logsigmoid(+-x) of the tile plus its dilation halo in
-// LDS, and evaluates the 8 neighbour terms per pixel in registers; the thresholded similarity is read as
-// one byte of neighbour bits per pixel (bit k = sim[k] >= thr).  Out-of-image neighbours see the zero
-// padding of F.unfold exactly as in the reference.  Sums are per-tile partials (deterministic; reduced
-// by the caller).
+// owns a 16x64 pixel tile of one mask row, stages x and logsigmoid(x) of the tile plus its dilation halo
+// in LDS, and evaluates the 8 neighbour terms per pixel in registers with one softplus each (hardware
+// exp/log); the thresholded similarity is read as one byte of neighbour bits per pixel (bit k = sim[k] >=
+// thr).  Out-of-image neighbours contribute 0, as F.unfold's zero padding of the log-probabilities makes
+// them in the reference.  Sums are per-tile partials (deterministic; reduced by the caller).
 #include "bm2f.h"
 #include "common.h"
 
@@ -24,9 +24,10 @@
 
 namespace {
 
-constexpr int TH = 16, TW = 64, NT = 256;  // tile rows, cols, threads (4 pixels per thread, one column)
-constexpr int kMaxDil = 8;
-constexpr int LW = TW + 2 * kMaxDil;  // LDS row pitch (fixed so the halo of any dilation <= 8 fits)
+constexpr int TH = 16, TW = 64, NT = 256;  // tile rows, cols, threads
+constexpr int PPT = TH * TW / NT;           // pixels per thread: PPT consecutive rows of one column
+constexpr int kMaxDil = 4;
+constexpr int LW = TW + 2 * kMaxDil;  // LDS row pitch (fixed so the halo of any dilation <= 4 fits)
 constexpr int LH = TH + 2 * kMaxDil;
 
 // unfold_wo_center order: 3x3 taps row-major minus the centre; tap 7-k is the mirror of tap k
@@ -36,24 +37,34 @@ __device__ __forceinline__ int tap_dx(int k) {
   return t % 3 - 1;
 }
 
+constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+
+// log(1 + exp(t)) for t <= 0 on the raw hardware exp2/log2 (one v_exp_f32 + one v_log_f32; 1 + e lies in
+// [1, 2], so no denormal range fix-ups are needed)
+__device__ __forceinline__ float softplus_neg(float t) {
+  return kLn2 * __builtin_amdgcn_logf(1.f + __builtin_amdgcn_exp2f(t * kLog2e));
+}
+
 __device__ __forceinline__ float log_sigmoid(float x) {  // F.logsigmoid: min(x,0) - log1p(exp(-|x|))
-  return fminf(x, 0.f) - log1pf(expf(-fabsf(x)));
+  return fminf(x, 0.f) - softplus_neg(-fabsf(x));
 }
 
-// -log(sig(a)sig(b) + sig(-a)sig(-b)) from the log-probabilities, as criterion.py:175-179 evaluates it
-__device__ __forceinline__ float pair_term(float fa, float ba, float fb, float bb) {
-  const float u = fa + fb, v = ba + bb;
-  const float m = fmaxf(u, v);
-  return -(logf(expf(u - m) + expf(v - m)) + m);
+// s(a,b) = -log(sig(a)sig(b) + sig(-a)sig(-b)) = -(logsig(a) + logsig(b) + softplus(-(a+b))): the
+// reference's log-space form (criterion.py:175-179, with logsig(-x) = logsig(x) - x) reduced to one
+// softplus per pair.  Pairs reaching outside the image are 0, as F.unfold's zero log-prob padding gives.
+__device__ __forceinline__ float pair_term(float a, float fa, float b, float fb) {
+  const float z = a + b;
+  return -(fa + fb + fmaxf(-z, 0.f) + softplus_neg(-fabsf(z)));
 }
 
-// d pair_term / d a (a = centre logit): -(w_u sig(-a) - w_v sig(a)), w = softmax(u, v)
-__device__ __forceinline__ float pair_grad(float fa, float ba, float fb, float bb) {
-  const float u = fa + fb, v = ba + bb;
-  const float m = fmaxf(u, v);
-  const float eu = expf(u - m), ev = expf(v - m);
-  return -(eu * expf(ba) - ev * expf(fa)) / (eu + ev);
+__device__ __forceinline__ float sigmoid_neg(float t) {  // sig(-t), accurate in both tails
+  const float e = __builtin_amdgcn_exp2f(-fabsf(t) * kLog2e);
+  const float r = __builtin_amdgcn_rcpf(1.f + e);
+  return t >= 0.f ? e * r : r;
 }
+
+// d s(a, b) / d a = sig(-(a+b)) - sig(-a)
+__device__ __forceinline__ float pair_grad(float a, float sna, float b) { return sigmoid_neg(a + b) - sna; }
 
 struct Tile {
   int ty0, tx0;
@@ -64,25 +75,36 @@ __device__ __forceinline__ Tile tile_of(int W) {
   return {static_cast<int>(blockIdx.x / ntx) * TH, static_cast<int>(blockIdx.x % ntx) * TW};
 }
 
-// stage logsigmoid(x), logsigmoid(-x) of the tile + halo (zero outside the image: F.unfold's padding)
-__device__ __forceinline__ void stage_logprobs(const float* __restrict__ xr, int H, int W, int d, Tile t, float* lf,
-                                               float* lb) {
-  const int hh = TH + 2 * d, ww = TW + 2 * d;
-  for (int i = threadIdx.x; i < hh * ww; i += NT) {
-    const int yy = i / ww, xx = i % ww;
+// stage x and logsigmoid(x) of the tile + halo (values outside the image are never read)
+__device__ __forceinline__ void stage_logits(const float* __restrict__ xr, int H, int W, int d, Tile t, float* lx,
+                                             float* lf) {
+  const int hh = TH + 2 * d;
+  for (int i = threadIdx.x; i < hh * LW; i += NT) {
+    const int yy = i / LW, xx = i % LW;  // LW is a constant: multiply-shift, no division
     const int gy = t.ty0 - d + yy, gx = t.tx0 - d + xx;
-    float f = 0.f, b = 0.f;
-    if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-      const float v = xr[static_cast<int64_t>(gy) * W + gx];
-      f = log_sigmoid(v);
-      b = log_sigmoid(-v);
-    }
-    lf[yy * LW + xx] = f;
-    lb[yy * LW + xx] = b;
+    float v = 0.f;
+    if (xx < TW + 2 * d && gy >= 0 && gy < H && gx >= 0 && gx < W) v = xr[static_cast<int64_t>(gy) * W + gx];
+    lx[i] = v;
+    lf[i] = log_sigmoid(v);
   }
 }
 
-// MODE 0: out[r, p] = sum_k bit_k(p) s_k(p)                          (matcher, image-shared similarity)
+__device__ __forceinline__ bool inside(int y, int x, int H, int W) { return y >= 0 && y < H && x >= 0 && x < W; }
+
+// bit k set when neighbour k of (y, x) lies in the image
+__device__ __forceinline__ unsigned neighbours_inside(int y, int x, int H, int W, int d) {
+  unsigned m = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) m |= (inside(y + tap_dy(k) * d, x + tap_dx(k) * d, H, W) ? 1u : 0u) << k;
+  return m;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// MODE 0: out[r, p] = sum_k bit_k(p) s_k(p)                          (image-shared similarity map)
 // MODE 1: part_num[r, tile] = sum_p w(p) sum_k bit_k s_k; part_den = sum_p w(p) popcount(bits(p))   (loss)
 // MODE 2: out[r, k, p] = s_k(p)                                      (matcher, per-target similarity)
 template <int MODE>
@@ -91,35 +113,37 @@ __global__ void __launch_bounds__(NT) pairwise_rows_kernel(const float* __restri
                                                            const int* __restrict__ t_row, const float* __restrict__ box,
                                                            const int* __restrict__ box_row, float* __restrict__ out,
                                                            float* __restrict__ part_den) {
-  __shared__ float lf[LH * LW], lb[LH * LW];
+  __shared__ float lx[LH * LW], lf[LH * LW];
   __shared__ float red[2][NT / 64];
   const int r = blockIdx.y;
   const int64_t HW = static_cast<int64_t>(H) * W;
   const Tile t = tile_of(W);
-  stage_logprobs(x + static_cast<int64_t>(x_row ? x_row[r] : r) * HW, H, W, d, t, lf, lb);
+  stage_logits(x + static_cast<int64_t>(x_row ? x_row[r] : r) * HW, H, W, d, t, lx, lf);
   __syncthreads();
   const uint8_t* br = MODE == 2 ? nullptr : bits + static_cast<int64_t>(t_row ? t_row[r] : r) * HW;
   const float* wr = (MODE == 1 && box) ? box + static_cast<int64_t>(box_row ? box_row[r] : r) * HW : nullptr;
-  const int tx = threadIdx.x % TW, ty_base = (threadIdx.x / TW) * 4;
+  const int tx = threadIdx.x % TW, ty_base = (threadIdx.x / TW) * PPT;
   float num = 0.f, den = 0.f;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < PPT; ++i) {
     const int ly = ty_base + i, gy = t.ty0 + ly, gx = t.tx0 + tx;
     if (gy >= H || gx >= W) continue;
     const int64_t p = static_cast<int64_t>(gy) * W + gx;
     const int c = (ly + d) * LW + (tx + d);
-    const float fa = lf[c], ba = lb[c];
+    const float a = lx[c], fa = lf[c];
     const unsigned bm = MODE == 2 ? 0xffu : br[p];
+    const unsigned on = (MODE == 2 ? 0xffu : bm) & neighbours_inside(gy, gx, H, W, d);
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int q = c + tap_dy(k) * d * LW + tap_dx(k) * d;
-      const float s = pair_term(fa, ba, lf[q], lb[q]);
-      if (MODE == 2) {
-        out[(static_cast<int64_t>(r) * 8 + k) * HW + p] = s;
-      } else if ((bm >> k) & 1u) {
-        acc += s;
-      }
+      // evaluated for every neighbour and masked by a multiply: straight-line code, no per-tap branches
+      // (staged values are finite for finite logits, out-of-image taps read the zero halo)
+      const float sk = static_cast<float>((on >> k) & 1u) * pair_term(a, fa, lx[q], lf[q]);
+      if (MODE == 2)
+        out[(static_cast<int64_t>(r) * 8 + k) * HW + p] = sk;
+      else
+        acc += sk;
     }
     if (MODE == 0) out[static_cast<int64_t>(r) * HW + p] = acc;
     if (MODE == 1) {
@@ -129,10 +153,8 @@ __global__ void __launch_bounds__(NT) pairwise_rows_kernel(const float* __restri
     }
   }
   if (MODE == 1) {
-    for (int off = 32; off > 0; off >>= 1) {
-      num += __shfl_xor(num, off);
-      den += __shfl_xor(den, off);
-    }
+    num = wave_sum(num);
+    den = wave_sum(den);
     if ((threadIdx.x & 63) == 0) {
       red[0][threadIdx.x >> 6] = num;
       red[1][threadIdx.x >> 6] = den;
@@ -150,54 +172,144 @@ __global__ void __launch_bounds__(NT) pairwise_rows_kernel(const float* __restri
   }
 }
 
+// The matcher's whole per-mask pass in one read of the mask logits (matcher.py:42-83): for row r (query q
+// of image b = img[r]) and this tile,
+//   part_cost[r, tile, g] = sum_p box[b, g, p] sum_k bit_k(p) s_k(p)      g < gcount[b]  (0 for g >= it)
+//   rowmax[r, y, tile_x]  = max over the tile's columns of x (the W-axis projection)
+//   colmax[r, tile_y, x]  = max over the tile's rows of x    (the H-axis projection)
+constexpr int kMaxG = 256;
+__global__ void __launch_bounds__(NT) match_cost_kernel(const float* __restrict__ x, int H, int W, int d, int Q,
+                                                        const uint8_t* __restrict__ bits, const float* __restrict__ box,
+                                                        const int* __restrict__ gcount, const int* __restrict__ gbox,
+                                                        int Gm, float* __restrict__ part_cost, float* __restrict__ rowmax,
+                                                        float* __restrict__ colmax) {
+  __shared__ float lx[LH * LW], lf[LH * LW];
+  __shared__ float red[NT / 64][kMaxG];
+  __shared__ float cmax[NT / 64][TW];
+  const int r = blockIdx.y, b = r / Q;
+  const int64_t HW = static_cast<int64_t>(H) * W;
+  const Tile t = tile_of(W);
+  const int ntx = (W + TW - 1) / TW, nty = (H + TH - 1) / TH;
+  stage_logits(x + static_cast<int64_t>(r) * HW, H, W, d, t, lx, lf);
+  __syncthreads();
+  const uint8_t* br = bits + static_cast<int64_t>(b) * HW;
+  const int tx = threadIdx.x % TW, wave = threadIdx.x / TW, ty_base = wave * PPT;
+  const int gx = t.tx0 + tx;
+  float A[PPT];
+  int64_t P[PPT];
+  float cm = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < PPT; ++i) {
+    const int ly = ty_base + i, gy = t.ty0 + ly;
+    A[i] = 0.f;
+    P[i] = -1;
+    float rv = -INFINITY;
+    if (gy < H && gx < W) {
+      const int64_t p = static_cast<int64_t>(gy) * W + gx;
+      P[i] = p;
+      const int c = (ly + d) * LW + (tx + d);
+      const float a = lx[c], fa = lf[c];
+      rv = a;
+      cm = fmaxf(cm, a);
+      const unsigned on = br[p] & neighbours_inside(gy, gx, H, W, d);
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int q = c + tap_dy(k) * d * LW + tap_dx(k) * d;
+        acc = fmaf(static_cast<float>((on >> k) & 1u), pair_term(a, fa, lx[q], lf[q]), acc);
+      }
+      A[i] = acc;
+    }
+    // row max over this wave's 64 columns
+    for (int off = 32; off > 0; off >>= 1) rv = fmaxf(rv, __shfl_xor(rv, off));
+    if (tx == 0 && gy < H) rowmax[(static_cast<int64_t>(r) * H + gy) * ntx + blockIdx.x % ntx] = rv;
+  }
+  cmax[wave][tx] = cm;
+  // box-weighted sums, one wave reduction per target whose nonzero bounding box meets this tile
+  const int G = gcount[b];
+  const float* bb = box + static_cast<int64_t>(b) * Gm * HW;
+  for (int g = 0; g < G; ++g) {
+    const int* bx = gbox + (static_cast<int64_t>(b) * Gm + g) * 4;  // [y0, y1) x [x0, x1)
+    if (bx[0] >= min(t.ty0 + TH, H) || bx[1] <= t.ty0 || bx[2] >= min(t.tx0 + TW, W) || bx[3] <= t.tx0) {
+      if (threadIdx.x % TW == 0) red[wave][g] = 0.f;
+      continue;
+    }
+    const float* bg = bb + static_cast<int64_t>(g) * HW;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i)
+      if (P[i] >= 0) v += A[i] * bg[P[i]];
+    v = wave_sum(v);
+    if (tx == 0) red[wave][g] = v;
+  }
+  __syncthreads();
+  float* pc = part_cost + (static_cast<int64_t>(r) * gridDim.x + blockIdx.x) * Gm;
+  for (int g = threadIdx.x; g < Gm; g += NT) {
+    float v = 0.f;
+    if (g < G)
+      for (int w = 0; w < NT / 64; ++w) v += red[w][g];
+    pc[g] = v;
+  }
+  if (threadIdx.x < TW && gx < W) {
+    float m = cmax[0][threadIdx.x];
+    for (int w = 1; w < NT / 64; ++w) m = fmaxf(m, cmax[w][threadIdx.x]);
+    colmax[(static_cast<int64_t>(r) * nty + blockIdx.x / ntx) * W + gx] = m;
+  }
+}
+
 // grad_x[r, p] = g[r] * sum_k D(x_p, x_q) (w(p) bit_k(p) + w(q) bit_{7-k}(q)),  q = p + off_k in the image
 __global__ void __launch_bounds__(NT) pairwise_bwd_kernel(const float* __restrict__ x, const int* __restrict__ x_row,
                                                           int H, int W, int d, const uint8_t* __restrict__ bits,
                                                           const int* __restrict__ t_row, const float* __restrict__ box,
                                                           const int* __restrict__ box_row, const float* __restrict__ g,
                                                           float* __restrict__ grad) {
-  __shared__ float lf[LH * LW], lb[LH * LW], lw[LH * LW];
+  __shared__ float lx[LH * LW], lw[LH * LW];
   __shared__ uint8_t lbits[LH * LW];
   const int r = blockIdx.y;
   const int64_t HW = static_cast<int64_t>(H) * W;
   const Tile t = tile_of(W);
-  stage_logprobs(x + static_cast<int64_t>(x_row ? x_row[r] : r) * HW, H, W, d, t, lf, lb);
+  const float* xr = x + static_cast<int64_t>(x_row ? x_row[r] : r) * HW;
   const uint8_t* br = bits + static_cast<int64_t>(t_row ? t_row[r] : r) * HW;
   const float* wr = box ? box + static_cast<int64_t>(box_row ? box_row[r] : r) * HW : nullptr;
   const int hh = TH + 2 * d, ww = TW + 2 * d;
-  for (int i = threadIdx.x; i < hh * ww; i += NT) {
-    const int yy = i / ww, xx = i % ww;
-    const int gy = t.ty0 - d + yy, gx = t.tx0 - d + xx;
-    uint8_t b = 0;
-    float w = 0.f;
-    if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-      const int64_t p = static_cast<int64_t>(gy) * W + gx;
-      b = br[p];
-      w = wr ? wr[p] : 1.f;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int yy = wave; yy < hh; yy += NT / 64) {
+    for (int xx = lane; xx < ww; xx += 64) {
+      const int gy = t.ty0 - d + yy, gx = t.tx0 - d + xx;
+      uint8_t bv = 0;
+      float w = 0.f, v = 0.f;
+      if (inside(gy, gx, H, W)) {
+        const int64_t p = static_cast<int64_t>(gy) * W + gx;
+        v = xr[p];
+        bv = br[p];
+        w = wr ? wr[p] : 1.f;
+      }
+      lx[yy * LW + xx] = v;
+      lbits[yy * LW + xx] = bv;
+      lw[yy * LW + xx] = w;
     }
-    lbits[yy * LW + xx] = b;
-    lw[yy * LW + xx] = w;
   }
   __syncthreads();
   const float gr = g[r];
-  const int tx = threadIdx.x % TW, ty_base = (threadIdx.x / TW) * 4;
+  const int tx = threadIdx.x % TW, ty_base = (threadIdx.x / TW) * PPT;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < PPT; ++i) {
     const int ly = ty_base + i, gy = t.ty0 + ly, gx = t.tx0 + tx;
     if (gy >= H || gx >= W) continue;
     const int c = (ly + d) * LW + (tx + d);
-    const float fa = lf[c], ba = lb[c], wc = lw[c];
+    const float a = lx[c], wc = lw[c];
+    const float sna = sigmoid_neg(a);
     const unsigned bc = lbits[c];
     float acc = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int dy = tap_dy(k) * d, dx = tap_dx(k) * d;
+      if (!inside(gy + dy, gx + dx, H, W)) continue;
       const int q = c + dy * LW + dx;
-      const bool inside = gy + dy >= 0 && gy + dy < H && gx + dx >= 0 && gx + dx < W;
       // the centre's own term k, and the neighbour's mirrored term 7-k (which reads x_p as its neighbour)
       float wt = ((bc >> k) & 1u) ? wc : 0.f;
-      if (inside && ((lbits[q] >> (7 - k)) & 1u)) wt += lw[q];
-      if (wt != 0.f) acc += wt * pair_grad(fa, ba, lf[q], lb[q]);
+      if ((lbits[q] >> (7 - k)) & 1u) wt += lw[q];
+      if (wt != 0.f) acc += wt * pair_grad(a, sna, lx[q]);
     }
     grad[static_cast<int64_t>(r) * HW + static_cast<int64_t>(gy) * W + gx] = gr * acc;
   }
@@ -320,6 +432,20 @@ extern "C" int m2f_pairwise_rows(const float* x, const int* x_row, int R, int H,
     pairwise_rows_kernel<1><<<grid, NT, 0, st>>>(x, x_row, H, W, dilation, bits, t_row, box, box_row, out, out_den);
   else
     pairwise_rows_kernel<2><<<grid, NT, 0, st>>>(x, x_row, H, W, dilation, bits, t_row, box, box_row, out, out_den);
+  return m2f::check_launch(fn);
+}
+
+extern "C" int m2f_pairwise_match_cost(const float* x, int B, int Q, int H, int W, int dilation, const uint8_t* bits,
+                                       const float* box, const int* gcount, const int* gbox, int Gm, float* part_cost,
+                                       float* rowmax, float* colmax, void* stream) {
+  const char* fn = "m2f_pairwise_match_cost";
+  if (int e = check_rows(fn, x, B * Q, H, W, dilation)) return e;
+  if (Gm < 0 || Gm > kMaxG) return m2f::fail(M2F_EUNSUPPORTED, "%s: %d targets > %d", fn, Gm, kMaxG);
+  if (B * Q > 0 && H > 0 && W > 0 && (!bits || !gcount || !rowmax || !colmax || (Gm > 0 && (!box || !gbox || !part_cost))))
+    return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  if (B * Q == 0 || H == 0 || W == 0) return m2f::ok();
+  match_cost_kernel<<<dim3(n_tiles(H, W), B * Q), NT, 0, static_cast<hipStream_t>(stream)>>>(
+      x, H, W, dilation, Q, bits, box, gcount, gbox, Gm, part_cost, rowmax, colmax);
   return m2f::check_launch(fn);
 }
 

@@ -116,8 +116,8 @@ def _rows_args(x, bits, t_row, box, box_row, dilation):
         raise ValueError("box must be contiguous fp32")
     if bits is not None and (bits.dtype != torch.uint8 or not bits.is_contiguous()):
         raise ValueError("bits must be contiguous uint8")
-    if dilation < 1 or dilation > 8:
-        raise ValueError("pairwise_dilation must be in [1, 8]")
+    if dilation < 1 or dilation > 4:
+        raise ValueError("pairwise_dilation must be in [1, 4]")
 
 
 def pairwise_map(x: torch.Tensor, bits: torch.Tensor, t_row: torch.Tensor, dilation: int) -> torch.Tensor:
@@ -138,6 +138,48 @@ def pairwise_planes(x: torch.Tensor, dilation: int) -> torch.Tensor:
     _native.call("m2f_pairwise_rows", x.data_ptr(), None, N, H, W, dilation, None, None, None, None, 2, out.data_ptr(),
                  None, _stream(x))
     return out
+
+
+def box_extents(box: torch.Tensor) -> torch.Tensor:
+    """(B, G, H, W) masks -> (B, G, 4) int32 [y0, y1, x0, x1) bounding every nonzero pixel (empty: y0 = H)."""
+    B, G, H, W = box.shape
+    rows = box.ne(0).any(3)                                    # (B, G, H)
+    cols = box.ne(0).any(2)                                    # (B, G, W)
+    ar_h = torch.arange(H, device=box.device)
+    ar_w = torch.arange(W, device=box.device)
+    y0 = torch.where(rows, ar_h, H).amin(2)
+    y1 = torch.where(rows, ar_h + 1, 0).amax(2)
+    x0 = torch.where(cols, ar_w, W).amin(2)
+    x1 = torch.where(cols, ar_w + 1, 0).amax(2)
+    return torch.stack([y0, y1, x0, x1], -1).to(torch.int32).contiguous()
+
+
+def match_cost(x: torch.Tensor, bits: torch.Tensor, box: torch.Tensor, gcount: torch.Tensor, dilation: int,
+               extents: torch.Tensor | None = None):
+    """The matcher's fused pass (``m2f_pairwise_match_cost``) over mask logits x (B, Q, H, W):
+
+    returns num (B, Q, Gm) = sum_p box[b, g, p] sum_k bit_k(p) s_k(p) (0 for g >= gcount[b]), and the axis
+    projections x.amax(3) (B, Q, H), x.amax(2) (B, Q, W) -- one read of x instead of three.  ``extents``
+    (from :func:`box_extents`) lets the kernel skip tiles a target's mask does not touch."""
+    _need_cuda(x, bits, box, gcount)
+    if extents is None:
+        extents = box_extents(box)
+    if x.dtype != torch.float32 or not x.is_contiguous() or x.dim() != 4:
+        raise ValueError("x must be a contiguous fp32 (B, Q, H, W) tensor")
+    if box.dtype != torch.float32 or not box.is_contiguous() or gcount.dtype != torch.int32:
+        raise ValueError("box must be contiguous fp32 (B, Gm, H, W), gcount int32")
+    B, Q, H, W = x.shape
+    Gm = box.shape[1]
+    lib = _native.load()
+    tiles = lib.m2f_pairwise_tiles(H, W)
+    ntx, nty = (W + 63) // 64, (H + 15) // 16
+    part = torch.empty((B * Q, tiles, Gm), dtype=torch.float32, device=x.device)
+    rmax = torch.empty((B * Q, H, ntx), dtype=torch.float32, device=x.device)
+    cmax = torch.empty((B * Q, nty, W), dtype=torch.float32, device=x.device)
+    _native.call("m2f_pairwise_match_cost", x.data_ptr(), B, Q, H, W, dilation, bits.data_ptr(), box.data_ptr(),
+                 gcount.data_ptr(), extents.data_ptr(), Gm, part.data_ptr(), rmax.data_ptr(), cmax.data_ptr(),
+                 _stream(x))
+    return (part.sum(1).view(B, Q, Gm), rmax.amax(2).view(B, Q, H), cmax.amax(1).view(B, Q, W))
 
 
 class PairwiseSums(Function):

@@ -251,12 +251,21 @@ int m2f_lsap_batched(const float* cost, int batch, int max_rows, int max_cols, i
  * bits[t_row[r]] (H*W bytes, bit k = similarity_k >= thresh) and weight box[box_row[r]] (or 1).
  * NULL index arrays mean identity.  mode 0: out[r, p] = sum_k bit_k s_k;  mode 1: per-tile
  * partials out[r, t] = sum_p w sum_k bit_k s_k and out_den[r, t] = sum_p w popcount(bits), with
- * t < m2f_pairwise_tiles(H, W);  mode 2: out[r, k, p] = s_k (bits unused).  1 <= dilation <= 8,
+ * t < m2f_pairwise_tiles(H, W);  mode 2: out[r, k, p] = s_k (bits unused).  1 <= dilation <= 4,
  * R <= 65535. */
 int m2f_pairwise_tiles(int H, int W);
 int m2f_pairwise_rows(const float* x, const int* x_row, int R, int H, int W, int dilation, const uint8_t* bits,
                       const int* t_row, const float* box, const int* box_row, int mode, float* out, float* out_den,
                       void* stream);
+/* The matcher's fused pass over the (B*Q, H, W) mask logits x (query q of image b is row b*Q+q):
+ * part_cost[r, t, g] = sum_{p in tile t} box[b, g, p] sum_k bit_k s_k (bits[b]: the image's neighbour
+ * bits; box (B, Gm, H, W); 0 for g >= gcount[b]), rowmax[r, y, tx] / colmax[r, ty, x] = per-tile maxima
+ * of x along W / H (tiles: 16 rows x 64 columns, t = ty * ceil(W/64) + tx).  gbox (B, Gm, 4) int32
+ * [y0, y1, x0, x1) must contain every nonzero pixel of box[b, g] (tiles outside it are skipped).
+ * Gm <= 256. */
+int m2f_pairwise_match_cost(const float* x, int B, int Q, int H, int W, int dilation, const uint8_t* bits,
+                            const float* box, const int* gcount, const int* gbox, int Gm, float* part_cost,
+                            float* rowmax, float* colmax, void* stream);
 /* Gradient of sum_r grad_scale[r] * (mode-1 numerator of row r) w.r.t. x[x_row[r]], written to
  * grad[r] (R, H, W) (not accumulated). */
 int m2f_pairwise_rows_bwd(const float* x, const int* x_row, int R, int H, int W, int dilation, const uint8_t* bits,

@@ -116,6 +116,24 @@ def test_pairwise_kernels_vs_oracle(device, N, H, W, d):
     torch.testing.assert_close(xg.grad.cpu().double(), xd.grad, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("B,Q,H,W,G", [(2, 5, 32, 32, 3), (3, 7, 45, 130, 9), (1, 4, 16, 20, 0)])
+def test_match_cost_kernel_vs_oracle(device, B, Q, H, W, G):
+    g = torch.Generator().manual_seed(B * 100 + W)
+    x = torch.randn(B, Q, H, W, generator=g) * 4
+    sim = torch.rand(B, 8, H, W, generator=g)
+    box = (torch.rand(B, max(G, 1), H, W, generator=g) < 0.4).float()[:, :G]
+    gcount = torch.tensor([G] * (B - 1) + [max(G - 2, 0)], dtype=torch.int32)
+    bits = weaksup.threshold_bits(sim.to(device), 0.3)
+    num, sx, sy = weaksup.match_cost(x.to(device), bits, box.to(device).contiguous(), gcount.to(device), 2)
+    assert torch.equal(sx.cpu(), x.amax(3)) and torch.equal(sy.cpu(), x.amax(2))
+    s_ref = ref.pred_similarity(x.double().view(B * Q, H, W), 2).view(B, Q, 8, H, W)
+    A = (s_ref * (sim >= 0.3)[:, None].double()).sum(2)                               # (B, Q, H, W)
+    want = torch.einsum("bqhw,bghw->bqg", A, box.double())
+    for b in range(B):
+        want[b, :, int(gcount[b]):] = 0
+    torch.testing.assert_close(num.cpu().double(), want, rtol=1e-5, atol=1e-4)
+
+
 def test_target_prep_vs_reference(device, gold):
     z = gold
     B = len(z["heights"])
