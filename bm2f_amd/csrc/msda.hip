@@ -301,6 +301,8 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // that projection: d offset = sum_c dval/dloc * g * a / (W, H) * (W, H) (the level scale cancels) and
 // d logit = a * (d attn - sum_k a_k d attn_k) (softmax backward over the L*P logits of the pair).
 // ------------------------------------------------------------------------------------------------
+constexpr int kWalkLanes = 4;  // phase-3 lanes per window row (4: 3.96 ms; 8: 4.10; 2: 4.15 at config 2)
+
 struct TileState {
   int bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
   unsigned int gmax, amax;
@@ -647,64 +649,99 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
   }
   __syncthreads();
 
-  // ---- phase 3: per window row, an 8-lane group walks its list; the row goes to HBM once: as a partial
-  // row in this workgroup's scratch slot (plain stores, summed by msda_gv_combine) or, without scratch,
-  // added to grad_value with row-contiguous atomics -----------------------------------------------------
+  // ---- phase 3: per window row, an LPR-lane group (32/LPR channels per lane) walks its list; the row
+  // goes to HBM once: as a partial row in this workgroup's scratch slot (plain stores, summed by
+  // msda_gv_combine) or, without scratch, added to grad_value with atomics.  Few lanes per row means many
+  // independent list walks per wave: the walk is one dependent LDS round trip per record, so more chains
+  // in flight hide more of that latency.
   if (!(geo.ablate & 2)) {
+    constexpr int LPR = kWalkLanes, CPL = D / LPR, RPW = 64 / LPR;  // lanes per row, channels per lane, rows per wave
     const double unscale = ts.unscale;
     const float inv_lp4 = 1.f / static_cast<float>(LP4);
-    const int ngroups = blockDim.x >> 3;
-    for (int row = tid >> 3; row < rows_total; row += ngroups) {
-      int id = head[row];
-      if (id < 0 && !scratch) continue;  // the 8 lanes of a group share the row
-      // every term is an integer (fixed point, |sum| < 2^52): the f64 adds are exact, so the result does
-      // not depend on the list order
-      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    const int jl = tid % LPR;
+    // rows in wave-lockstep batches of RPW (one per group), so the flush can transpose them
+    for (int base = wid * RPW; base < rows_total; base += nwaves * RPW) {
+      const int row = base + lane / LPR;
+      int id = row < rows_total ? head[row] : -1;
+      float v[CPL];
       if (id >= 0 && geo.exact) {
+        // every term is an integer (fixed point, |sum| < 2^52): the f64 adds are exact, so the result
+        // does not depend on the list order
+        double a[CPL];
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) a[k] = 0.0;
         while (id != 0xffff) {
           const float c = coef[id] * fscale;
           const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
-          const f4 g = *reinterpret_cast<const f4*>(gsh + q * D + 4 * j);
-          a0 += static_cast<double>(rintf(c * g.x));
-          a1 += static_cast<double>(rintf(c * g.y));
-          a2 += static_cast<double>(rintf(c * g.z));
-          a3 += static_cast<double>(rintf(c * g.w));
+          f4 g[CPL / 4];
+#pragma unroll
+          for (int k = 0; k < CPL / 4; ++k) g[k] = *reinterpret_cast<const f4*>(gsh + q * D + CPL * jl + 4 * k);
           id = nxt[id];
+#pragma unroll
+          for (int k = 0; k < CPL / 4; ++k) {
+            a[4 * k + 0] += static_cast<double>(rintf(c * g[k].x));
+            a[4 * k + 1] += static_cast<double>(rintf(c * g[k].y));
+            a[4 * k + 2] += static_cast<double>(rintf(c * g[k].z));
+            a[4 * k + 3] += static_cast<double>(rintf(c * g[k].w));
+          }
         }
-      } else if (id >= 0) {
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) v[k] = static_cast<float>(a[k] * unscale);
+      } else {
         // fp32 accumulation in list order: as accurate as the reference's fp32 atomics and, like them,
         // not bitwise repeatable (M2F_MSDA_DETERMINISTIC=0; the default is the exact branch above)
-        f4 acc = {0.f, 0.f, 0.f, 0.f};
-        while (id != 0xffff) {
+        f4 sacc[CPL / 4];
+#pragma unroll
+        for (int k = 0; k < CPL / 4; ++k) sacc[k] = f4{0.f, 0.f, 0.f, 0.f};
+        while (id >= 0 && id != 0xffff) {
           const float c = coef[id];
           const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
-          acc += c * *reinterpret_cast<const f4*>(gsh + q * D + 4 * j);
+#pragma unroll
+          for (int k = 0; k < CPL / 4; ++k) sacc[k] += c * *reinterpret_cast<const f4*>(gsh + q * D + CPL * jl + 4 * k);
           id = nxt[id];
         }
-        a0 = static_cast<double>(acc.x) * ts.rscale;
-        a1 = static_cast<double>(acc.y) * ts.rscale;
-        a2 = static_cast<double>(acc.z) * ts.rscale;
-        a3 = static_cast<double>(acc.w) * ts.rscale;
+#pragma unroll
+        for (int k = 0; k < CPL / 4; ++k) {
+          v[4 * k] = sacc[k].x; v[4 * k + 1] = sacc[k].y; v[4 * k + 2] = sacc[k].z; v[4 * k + 3] = sacc[k].w;
+        }
       }
       if (scratch) {
-        const f4 v = {static_cast<float>(a0 * unscale), static_cast<float>(a1 * unscale),
-                      static_cast<float>(a2 * unscale), static_cast<float>(a3 * unscale)};
-        *reinterpret_cast<f4*>(scratch + (wg * geo.wrows + row) * D + 4 * j) = v;
+        if (row < rows_total) {
+          float* dst = scratch + (wg * geo.wrows + row) * D + CPL * jl;
+#pragma unroll
+          for (int k = 0; k < CPL / 4; ++k)
+            *reinterpret_cast<f4*>(dst + 4 * k) = f4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
+        }
         continue;
       }
       if (geo.ablate & 8) {  // timing experiment: walk the lists, skip the HBM adds
-        if (a0 == 12345.0) gvalue[0] = 0.f;
+        if (v[0] == 12345.f) gvalue[0] = 0.f;
         continue;
       }
-      int l = 0;
-      while (row >= ts.woff[l + 1]) ++l;
-      const int rr = row - ts.woff[l];
-      const int y = ts.wy0[l] + rr / ts.ww[l], x = ts.wx0[l] + rr % ts.ww[l];
-      float* dst = gvalue + ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D + 4 * j;
-      if (a0 != 0.0) atomicAdd(dst + 0, static_cast<float>(a0 * unscale));
-      if (a1 != 0.0) atomicAdd(dst + 1, static_cast<float>(a1 * unscale));
-      if (a2 != 0.0) atomicAdd(dst + 2, static_cast<float>(a2 * unscale));
-      if (a3 != 0.0) atomicAdd(dst + 3, static_cast<float>(a3 * unscale));
+      int64_t off = -1;  // element offset of channel 0 of this group's grad_value row (-1: none)
+      if (row < rows_total && head[row] >= 0) {
+        int l = 0;
+        while (row >= ts.woff[l + 1]) ++l;
+        const int rr = row - ts.woff[l];
+        const int y = ts.wy0[l] + rr / ts.ww[l], x = ts.wx0[l] + rr % ts.ww[l];
+        off = ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D;
+      }
+      // transpose the wave's rows (ds_bpermute) so that each atomic instruction covers two whole
+      // 128-byte rows, one dword per lane: gfx950's L2 takes atomics per request, and this issues 2
+      // requests per row instead of 8 (tools/ubench/global_atomic.hip: 1.6 vs 6.5 ms per 2.1 GB)
+      const int c = lane & 31;
+#pragma unroll
+      for (int i = 0; i < RPW / 2; ++i) {
+        const int src = (2 * i + (lane >> 5)) * LPR + c / CPL;  // lane holding channel c of row 2i + half
+        float val = 0.f;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) {
+          const float xk = __shfl(v[k], src);
+          val = (c % CPL) == k ? xk : val;
+        }
+        const int64_t o = __shfl(off, src);
+        if (o >= 0 && val != 0.f) atomicAdd(gvalue + o + c, val);
+      }
     }
   }
 }
