@@ -204,10 +204,30 @@ def wrap_ddp(model, device=None):
     return torch.nn.parallel.DistributedDataParallel(model, **kw)
 
 
+class _MeanF32(torch.autograd.Function):
+    """``x.float().mean()`` without the fp32 copy: the mean accumulates in fp32 straight from the bf16
+    masks, and the gradient is the same bf16(g / numel) the cast's backward would produce, written as one
+    fill (no fp32 (B, Q, H, W) intermediate in either pass)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.shape, ctx.dtype, ctx.n = x.shape, x.dtype, x.numel()
+        return x.mean(dtype=torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        v = (g.float() / ctx.n).to(ctx.dtype)
+        return torch.empty(ctx.shape, dtype=ctx.dtype, device=g.device).fill_(v)
+
+
+def _mean_f32(x):
+    return _MeanF32.apply(x) if x.requires_grad else x.float().mean()
+
+
 def surrogate_loss(out):
-    """Sum over the 10 heads of mean(pred_logits) + mean(pred_masks)."""
+    """Sum over the 10 heads of mean(pred_logits) + mean(pred_masks), in fp32."""
     heads = [out] + list(out["aux_outputs"])
-    return sum(h["pred_logits"].float().mean() + h["pred_masks"].float().mean() for h in heads)
+    return sum(_mean_f32(h["pred_logits"]) + _mean_f32(h["pred_masks"]) for h in heads)
 
 
 def make_optimizer(model):

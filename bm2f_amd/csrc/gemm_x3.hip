@@ -40,7 +40,7 @@ namespace {
 
 using namespace m2f_x3;
 
-enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4 };
+enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4, kAdd = 8 };  // kAdd: C = A.B (+bias) + D1 (+ D2)
 
 // ---------------------------------------------------------------------------------------------------
 // NT: C[M,N] = A[M,K] . B[N,K]^T.
@@ -92,7 +92,8 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
                                                        const __bf16* __restrict__ Bs, int NP,
                                                        const float* __restrict__ bias,
                                                        const float* __restrict__ mask, int64_t ldm,
-                                                       float* __restrict__ C, int64_t ldc, int M, int N, int K) {
+                                                       const float* D1, const float* D2, int64_t ldd,
+                                                       float* C, int64_t ldc, int M, int N, int K) {
   constexpr int NT = 64 * NW, BM = 32 * NW, TJ = BN / 32;
   constexpr int PIECES = 3 * BN * 2;             // 16-byte pieces of one B chunk
   constexpr int NBL = (PIECES + NT - 1) / NT;    // per thread
@@ -231,11 +232,20 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
           v.x = mk.x > 0.f ? v.x : 0.f; v.y = mk.y > 0.f ? v.y : 0.f;
           v.z = mk.z > 0.f ? v.z : 0.f; v.w = mk.w > 0.f ? v.w : 0.f;
         }
+        if constexpr ((EPI & kAdd) != 0) {
+          // (A.B + bias) + D1 + D2, left to right: the sum autograd would form, one rounding per add
+          v = v + *reinterpret_cast<const f4*>(D1 + static_cast<int64_t>(row) * ldd + col);
+          if (D2) v = v + *reinterpret_cast<const f4*>(D2 + static_cast<int64_t>(row) * ldd + col);
+        }
         *reinterpret_cast<f4*>(C + static_cast<int64_t>(row) * ldc + col) = v;
       } else {
         for (int t = 0; t < 4 && col + t < N; ++t) {
           float x = v[t];
           if constexpr ((EPI & kMask) != 0) x = mask[static_cast<int64_t>(row) * ldm + col + t] > 0.f ? x : 0.f;
+          if constexpr ((EPI & kAdd) != 0) {
+            x += D1[static_cast<int64_t>(row) * ldd + col + t];
+            if (D2) x += D2[static_cast<int64_t>(row) * ldd + col + t];
+          }
           C[static_cast<int64_t>(row) * ldc + col + t] = x;
         }
       }
@@ -248,12 +258,14 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
 
 template <int BN, int NW>
 int launch_nt(int epi, const float* A, int64_t lda, const __bf16* Bs, int NP, const float* bias, const float* mask,
-              int64_t ldm, float* C, int64_t ldc, int M, int N, int K, hipStream_t st) {
+              int64_t ldm, const float* D1, const float* D2, int64_t ldd, float* C, int64_t ldc, int M, int N, int K,
+              hipStream_t st) {
   constexpr int BM = 32 * NW;
   const int64_t nwg = static_cast<int64_t>((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (nwg > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "m2f_gemm_f32x3_nt: too many tiles");
   const dim3 grid(static_cast<unsigned>(nwg)), block(64 * NW);
-#define M2F_X3NT(E) x3_nt_kernel<BN, NW, E><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K)
+#define M2F_X3NT(E) x3_nt_kernel<BN, NW, E><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, \
+                                                       M, N, K)
   switch (epi) {
     case kNone: M2F_X3NT(kNone); break;
     case kBias: M2F_X3NT(kBias); break;
@@ -261,6 +273,8 @@ int launch_nt(int epi, const float* A, int64_t lda, const __bf16* Bs, int NP, co
     case kBias | kRelu: M2F_X3NT(kBias | kRelu); break;
     case kMask: M2F_X3NT(kMask); break;
     case kBias | kMask: M2F_X3NT(kBias | kMask); break;
+    case kAdd: M2F_X3NT(kAdd); break;
+    case kBias | kAdd: M2F_X3NT(kBias | kAdd); break;
     default: return m2f::fail(M2F_EINVAL, "m2f_gemm_f32x3_nt: epilogue %d", epi);
   }
 #undef M2F_X3NT
@@ -532,6 +546,14 @@ extern "C" int m2f_gemm_f32x3_nt_workspace(int N, int K, int64_t* workspace_byte
 extern "C" int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
                                  int relu, const float* mask, int64_t ldm, float* C, int64_t ldc, int M, int N, int K,
                                  void* workspace, int64_t workspace_bytes, void* stream) {
+  return m2f_gemm_f32x3_nt_add(A, lda, B, ldb, b_kn, bias, relu, mask, ldm, nullptr, nullptr, 0, C, ldc, M, N, K,
+                               workspace, workspace_bytes, stream);
+}
+
+extern "C" int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn,
+                                     const float* bias, int relu, const float* mask, int64_t ldm, const float* D1,
+                                     const float* D2, int64_t ldd, float* C, int64_t ldc, int M, int N, int K,
+                                     void* workspace, int64_t workspace_bytes, void* stream) {
   const char* fn = "m2f_gemm_f32x3_nt";
   if (M < 0 || N <= 0 || K <= 0) return m2f::fail(M2F_EINVAL, "%s: M %d N %d K %d", fn, M, N, K);
   if (!A || !B || !C) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
@@ -539,6 +561,11 @@ extern "C" int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, in
     return m2f::fail(M2F_EINVAL, "%s: K, lda must be multiples of 4 (lda >= K), A 16-byte aligned", fn);
   if (mask && ldm < N) return m2f::fail(M2F_EINVAL, "%s: ldm %lld < N", fn, static_cast<long long>(ldm));
   if (relu && mask) return m2f::fail(M2F_EINVAL, "%s: relu and mask are exclusive", fn);
+  if (D2 && !D1) return m2f::fail(M2F_EINVAL, "%s: D2 without D1", fn);
+  if (D1 && (relu || mask)) return m2f::fail(M2F_EINVAL, "%s: addends exclude relu and mask", fn);
+  if (D1 && (ldd < N || (ldd & 3) || (ldc & 3) || ((N & 3) != 0) || !m2f::aligned(D1, 16) ||
+             (D2 && !m2f::aligned(D2, 16)) || !m2f::aligned(C, 16)))
+    return m2f::fail(M2F_EINVAL, "%s: addends need ldd >= N, N/ldd/ldc multiples of 4, 16-byte alignment", fn);
   if (!workspace || workspace_bytes < nt_workspace(N, K) || !m2f::aligned(workspace, 16))
     return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld (16-byte aligned)", fn,
                      static_cast<long long>(workspace_bytes), static_cast<long long>(nt_workspace(N, K)));
@@ -548,15 +575,15 @@ extern "C" int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, in
   __bf16* Bs = static_cast<__bf16*>(workspace);
   x3_presplit<<<m2f::ceil_div(static_cast<int64_t>(nchunks) * NP, 256), 256, 0, st>>>(B, ldb, b_kn, N, K, NP, nchunks, Bs);
   if (int rc = m2f::check_launch(fn)) return rc;
-  const int epi = (bias ? kBias : 0) | (relu ? kRelu : 0) | (mask ? kMask : 0);
+  const int epi = (bias ? kBias : 0) | (relu ? kRelu : 0) | (mask ? kMask : 0) | (D1 ? kAdd : 0);
   // 128-row blocks of 4 waves; 96-wide columns for N = 3 * 96 k (the 288-wide sampling projection), else 128
   int cfg = (N % 128 != 0 && N % 96 == 0) ? 1 : 0;
   if (const char* e = std::getenv("M2F_GEMM_X3_NT_CFG")) cfg = std::atoi(e);
   switch (cfg) {
-    case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K, st);
-    case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K, st);
-    case 2: return launch_nt<256, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K, st);
-    case 3: return launch_nt<128, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, C, ldc, M, N, K, st);
+    case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
+    case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
+    case 2: return launch_nt<256, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
+    case 3: return launch_nt<128, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
     default: return m2f::fail(M2F_EINVAL, "%s: config %d", fn, cfg);
   }
 }

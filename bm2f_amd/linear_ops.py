@@ -52,22 +52,36 @@ def _c64(v):
     return ctypes.c_int64(int(v))
 
 
-def gemm_nt(a, b, bias=None, relu=False, mask=None, out=None, engine=None, b_kn=False):
-    """C = a @ b.T (+ bias) (ReLU | * (mask > 0)); a (M, K), b (N, K) fp32 row-major (unit column stride).
-    With ``b_kn`` b is (K, N) and C = a @ b (x3 engine: read in place; exact engine: transposed copy)."""
+def gemm_nt(a, b, bias=None, relu=False, mask=None, out=None, engine=None, b_kn=False, add=()):
+    """C = a @ b.T (+ bias) (ReLU | * (mask > 0)) (+ add[0] (+ add[1])); a (M, K), b (N, K) fp32 row-major
+    (unit column stride).  With ``b_kn`` b is (K, N) and C = a @ b (x3 engine: read in place; exact engine:
+    transposed copy).  ``add``: up to two (M, N) addends with one row stride (x3 engine; ``out`` may be one
+    of them)."""
     M, K = a.shape
     N = b.shape[1] if b_kn else b.shape[0]
     if out is None:
         out = torch.empty(M, N, device=a.device, dtype=torch.float32)
     msk = (mask.data_ptr() if mask is not None else None, _c64(mask.stride(0) if mask is not None else 0))
+    add = [d for d in add if d is not None]
     if _engine(engine) == "x3":
         wsb = ctypes.c_int64(0)
         _native.call("m2f_gemm_f32x3_nt_workspace", N, K, ctypes.byref(wsb))
         ws = torch.empty(max(wsb.value, 16), device=a.device, dtype=torch.uint8)
+        if add:
+            if len(add) > 2 or any(d.shape != (M, N) or d.stride() != add[0].stride() or d.stride(1) != 1
+                                   for d in add):
+                raise RuntimeError("gemm_nt: addends must be (M, N) row-major tensors with one row stride")
+            _native.call("m2f_gemm_f32x3_nt_add", a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)),
+                         1 if b_kn else 0, bias.data_ptr() if bias is not None else None, 1 if relu else 0, *msk,
+                         add[0].data_ptr(), add[1].data_ptr() if len(add) > 1 else None, _c64(add[0].stride(0)),
+                         out.data_ptr(), _c64(out.stride(0)), M, N, K, ws.data_ptr(), _c64(ws.numel()), _stream(a))
+            return out
         _native.call("m2f_gemm_f32x3_nt", a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)),
                      1 if b_kn else 0, bias.data_ptr() if bias is not None else None, 1 if relu else 0, *msk,
                      out.data_ptr(), _c64(out.stride(0)), M, N, K, ws.data_ptr(), _c64(ws.numel()), _stream(a))
         return out
+    if add:
+        raise RuntimeError("gemm_nt: addends need the x3 engine")
     if b_kn:
         b = b.t().contiguous()
     _native.call("m2f_gemm_f32_nt", a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)),
@@ -178,6 +192,100 @@ class FFNF32(Function):
         return dx, dw1, db1, dw2, db2
 
 
+def _grad_rows(g, like):
+    """A gradient as contiguous (rows, C) fp32 (zeros when autograd passes None)."""
+    if g is None:
+        return torch.zeros(like.shape, device=like.device, dtype=torch.float32)
+    g = _rows(g)
+    return g if g.is_contiguous() else g.contiguous()
+
+
+class FFNResidualF32(Function):
+    """(linear2(relu(linear1(x))), x): the FFN of :class:`FFNF32` that also hands ``x`` on for the residual
+    add & norm that follows (msdeformattn.py:109-113), so the backward sums the residual gradient into
+    grad_x inside the input-gradient GEMM's epilogue instead of autograd adding two (N*S, 256) tensors."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        x2 = _rows(x)
+        if not x2.is_contiguous():
+            x2 = x2.contiguous()
+        h = gemm_nt(x2, w1, b1, relu=True)
+        y = gemm_nt(h, w2, b2)
+        ctx.save_for_backward(x2, w1, w2, h)
+        ctx.in_shape = x.shape
+        ctx.biases = (b1 is not None, b2 is not None)
+        return y.view(*x.shape[:-1], w2.shape[0]), x2.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, grad, grad_pass):
+        x2, w1, w2, h = ctx.saved_tensors
+        g = _grad_rows(grad, x2)
+        nig = ctx.needs_input_grad
+        dw2, db2 = gemm_tn(g, h, colsum=ctx.biases[1] and nig[4]) if (nig[3] or nig[4]) else (None, None)
+        gh = gemm_nt(g, w2, mask=h, b_kn=True)
+        del h
+        dw1, db1 = gemm_tn(gh, x2, colsum=ctx.biases[0] and nig[2]) if (nig[1] or nig[2]) else (None, None)
+        dx = None
+        if nig[0]:
+            gp = _rows(grad_pass).contiguous() if grad_pass is not None else None
+            dx = gemm_nt(gh, w1, b_kn=True, add=(gp,)).view(ctx.in_shape)
+        return dx, dw1, db1, dw2, db2
+
+
+class EncoderInProjF32(Function):
+    """The two input projections of an encoder layer's MSDeformAttn, and ``src`` handed on for the residual
+    (msdeformattn.py:115-119 with ms_deform_attn.py:97-103):
+
+        value = src @ Wv^T + bv,   proj = (src + pos) @ Wq^T + bq,   src (for the residual add & norm)
+
+    Wq / bq are the sampling-offset and attention-weight projections stacked.  ``src`` has three consumers,
+    so autograd would add three (N*S, 256) gradients; here grad_src = grad_value . Wv + grad_proj . Wq +
+    grad_residual leaves the two input-gradient GEMMs with the sums in their epilogues."""
+
+    @staticmethod
+    def forward(ctx, src, pos, wv, bv, wq, bq):
+        s2 = _rows(src)
+        if not s2.is_contiguous():
+            s2 = s2.contiguous()
+        q2 = s2 + _rows(pos) if pos is not None else s2
+        value = gemm_nt(s2, wv, bv)
+        proj = gemm_nt(q2, wq, bq)
+        ctx.save_for_backward(s2, q2, wv, wq)
+        ctx.in_shape = src.shape
+        ctx.has_pos = pos is not None
+        ctx.biases = (bv is not None, bq is not None)
+        lead = src.shape[:-1]
+        return value.view(*lead, wv.shape[0]), proj.view(*lead, wq.shape[0]), s2.view(src.shape)
+
+    @staticmethod
+    def backward(ctx, gvalue, gproj, gpass):
+        s2, q2, wv, wq = ctx.saved_tensors
+        nig = ctx.needs_input_grad
+        gv = _grad_rows(gvalue, torch.empty(s2.shape[0], wv.shape[0], device=s2.device))
+        gq = _grad_rows(gproj, torch.empty(s2.shape[0], wq.shape[0], device=s2.device))
+        gr = _rows(gpass).contiguous() if gpass is not None else None
+        dsrc = dpos = None
+        if ctx.has_pos and nig[1]:
+            dq = gemm_nt(gq, wq, b_kn=True)
+            dpos = dq.view(ctx.in_shape)
+            if nig[0]:
+                dsrc = gemm_nt(gv, wv, b_kn=True, add=(dq, gr)).view(ctx.in_shape)
+        elif nig[0]:
+            t = gemm_nt(gq, wq, b_kn=True, add=(gr,))
+            dsrc = gemm_nt(gv, wv, b_kn=True, add=(t,), out=t).view(ctx.in_shape)
+        dwv, dbv = gemm_tn(gv, s2, colsum=ctx.biases[0] and nig[3]) if (nig[2] or nig[3]) else (None, None)
+        dwq, dbq = gemm_tn(gq, q2, colsum=ctx.biases[1] and nig[5]) if (nig[4] or nig[5]) else (None, None)
+        return dsrc, dpos, dwv, dbv, dwq, dbq
+
+
+def residual_fusable(x, *mods) -> bool:
+    """Whether the pass-through variants (:class:`FFNResidualF32`, :class:`EncoderInProjF32`) apply: CUDA fp32
+    on the x3 engine (their gradient sums ride in the x3 GEMM epilogues)."""
+    return ENGINE == "x3" and x.shape[-1] % 4 == 0 and _eligible(x, *mods) and all(
+        m.weight.shape[0] % 4 == 0 for m in mods)
+
+
 def _eligible_wb(x, weight, bias):
     return (x.is_cuda and x.dtype == torch.float32 and x.numel() > 0 and x.shape[-1] % 4 == 0
             and weight.dtype == torch.float32 and weight.dim() == 2 and weight.is_contiguous()
@@ -201,6 +309,13 @@ def linear_wb(x: torch.Tensor, weight: torch.Tensor, bias, relu: bool = False) -
         return LinearF32.apply(x, weight, bias, relu)
     y = F.linear(x, weight, bias)
     return F.relu(y) if relu else y
+
+
+def ffn_residual(x: torch.Tensor, lin1: nn.Linear, lin2: nn.Linear):
+    """``(lin2(relu(lin1(x))), x)``; use the second output as the residual (see :class:`FFNResidualF32`)."""
+    if residual_fusable(x, lin1, lin2):
+        return FFNResidualF32.apply(x, lin1.weight, lin1.bias, lin2.weight, lin2.bias)
+    return ffn(x, lin1, lin2), x
 
 
 def ffn(x: torch.Tensor, lin1: nn.Linear, lin2: nn.Linear) -> torch.Tensor:

@@ -297,6 +297,28 @@ class MSDeformAttn(nn.Module):
                 and reference_points.shape[-1] == 2 and not reference_points.requires_grad
                 and not torch.is_autocast_enabled("cuda"))
 
+    def forward_src_pos(self, src, pos, reference_points, input_spatial_shapes, input_level_start_index,
+                        input_padding_mask=None):
+        """``(self.forward(src + pos, reference_points, src, ...), src)`` for an encoder layer whose query is
+        ``src + pos`` and whose residual is ``src`` (msdeformattn.py:115-119).  On the fused path the two
+        input projections are one autograd node (:class:`linear_ops.EncoderInProjF32`) and the returned
+        ``src`` carries the residual's gradient into that node's GEMM epilogues."""
+        if (self._fusable(src, reference_points, src, input_spatial_shapes, input_padding_mask)
+                and (pos is None or (pos.shape == src.shape and pos.dtype == torch.float32))
+                and linear_ops.residual_fusable(src, self.value_proj)):
+            N, Len_in, _ = src.shape
+            w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)
+            b = torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0)
+            value, proj, src_res = linear_ops.EncoderInProjF32.apply(src, pos, self.value_proj.weight,
+                                                                     self.value_proj.bias, w, b)
+            value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
+            out = MSDeformAttnFusedFunction.apply(value, proj, reference_points,
+                                                  _host_shapes(input_spatial_shapes), self.n_points)
+            return linear_ops.linear(out, self.output_proj), src_res
+        query = src if pos is None else src + pos
+        return self.forward(query, reference_points, src, input_spatial_shapes, input_level_start_index,
+                            input_padding_mask), src
+
     def forward(self, query, reference_points, input_flatten, input_spatial_shapes, input_level_start_index,
                 input_padding_mask=None):
         N, Len_q, _ = query.shape

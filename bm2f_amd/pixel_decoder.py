@@ -13,6 +13,7 @@ alter results:
 from __future__ import annotations
 
 import copy
+import os
 from typing import Callable, Dict, List, Optional, Union
 
 import numpy as np
@@ -26,6 +27,11 @@ from . import conv_ops, linear_ops
 from .norm_ops import add_layernorm
 from .position_encoding import PositionEmbeddingSine
 from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill, configurable, get_norm
+
+
+# encoder layers hand their residual inputs through the projection / FFN autograd nodes so gradient sums
+# ride in GEMM epilogues (M2F_RESIDUAL_FUSED=0: plain autograd sums, for A/B measurements)
+RESIDUAL_FUSED = os.environ.get("M2F_RESIDUAL_FUSED", "1") != "0"
 
 
 def _get_clones(module, N):
@@ -75,10 +81,22 @@ class MSDeformAttnTransformerEncoderLayer(nn.Module):
         return self._add_norm(src, src2, self.dropout3, self.norm2)
 
     def forward(self, src, pos, reference_points, spatial_shapes, level_start_index, padding_mask=None):
+        if self._residual_fused():
+            # src's three consumers (value_proj, the query, the residual) and the FFN input's two (linear1,
+            # the residual) have their gradients summed inside the input-gradient GEMMs (linear_ops)
+            src2, src = self.self_attn.forward_src_pos(src, pos, reference_points, spatial_shapes,
+                                                       level_start_index, padding_mask)
+            src = self._add_norm(src, src2, self.dropout1, self.norm1)
+            src2, src = linear_ops.ffn_residual(src, self.linear1, self.linear2)
+            return self._add_norm(src, src2, self.dropout3, self.norm2)
         src2 = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, spatial_shapes,
                               level_start_index, padding_mask)
         src = self._add_norm(src, src2, self.dropout1, self.norm1)
         return self.forward_ffn(src)
+
+    def _residual_fused(self):
+        return (self.activation is F.relu and RESIDUAL_FUSED
+                and all(d.p == 0.0 or not self.training for d in (self.dropout1, self.dropout2, self.dropout3)))
 
 
 class MSDeformAttnTransformerEncoder(nn.Module):

@@ -205,6 +205,16 @@ int m2f_gemm_f32x3_nt_workspace(int N, int K, int64_t* workspace_bytes);
 int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
                       int relu, const float* mask, int64_t ldm, float* C, int64_t ldc, int M, int N, int K,
                       void* workspace, int64_t workspace_bytes, void* stream);
+/* m2f_gemm_f32x3_nt_add: as m2f_gemm_f32x3_nt with C = A.B^T (+ bias) + D1 (+ D2), the addends
+ *   [M][N] with row stride ldd (C may alias D1 or D2).  Replaces the autograd gradient sums
+ *   (AccumulateGrad / AddBackward) over a tensor with several consumers in the encoder layer
+ *   (msdeformattn.py:115-131: src feeds value_proj, the query and the residual; its FFN input feeds
+ *   linear1 and the residual).  Addends exclude relu and mask; N, ldd, ldc multiples of 4; D1, D2, C
+ *   16-byte aligned. */
+int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
+                          int relu, const float* mask, int64_t ldm, const float* D1, const float* D2, int64_t ldd,
+                          float* C, int64_t ldc, int M, int N, int K, void* workspace, int64_t workspace_bytes,
+                          void* stream);
 int m2f_gemm_f32x3_tn_workspace(int M, int N1, int N2, int64_t* workspace_bytes);
 int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                       float* colsum, int M, int N1, int N2, void* workspace, int64_t workspace_bytes,

@@ -139,3 +139,57 @@ def test_x3_nonfinite_inputs_propagate(device):
         c = linear_ops.gemm_nt(a, b, engine=eng)
         ref = a @ b.t()
         assert torch.equal(torch.isfinite(c), torch.isfinite(ref))
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 4, 4), (1000, 256, 288), (129, 256, 1024), (77, 132, 260)])
+@pytest.mark.parametrize("n_add,bias,alias", [(1, False, False), (2, False, False), (1, True, False),
+                                              (2, False, True)])
+def test_gemm_nt_addends_vs_fp64(device, M, N, K, n_add, bias, alias):
+    """m2f_gemm_f32x3_nt_add: C = A.B (+ bias) + D1 (+ D2), C may alias an addend."""
+    g = torch.Generator(device="cpu").manual_seed(M + 7 * N + K + n_add)
+    a = torch.randn(M, K, generator=g).to(device)
+    w = torch.randn(K, N, generator=g).to(device)            # b_kn: the weight of an input gradient
+    bv = torch.randn(N, generator=g).to(device) if bias else None
+    adds = [torch.randn(M, N, generator=g).to(device) for _ in range(n_add)]
+    ref = a.double() @ w.double() + (bv.double() if bias else 0) + sum(d.double() for d in adds)
+    out = linear_ops.gemm_nt(a, w, bv, b_kn=True, add=adds, out=adds[0] if alias else None)
+    assert _rel(out, ref) < 2e-6
+    if alias:
+        assert out.data_ptr() == adds[0].data_ptr()
+
+
+def test_encoder_layer_residual_fused_matches_autograd_sums(device):
+    """The encoder layer with residual gradients summed in GEMM epilogues (EncoderInProjF32 /
+    FFNResidualF32) against the same layer with plain autograd sums: outputs equal, gradients to fp32
+    rounding of the reordered sums."""
+    from bm2f_amd import pixel_decoder
+    from bm2f_amd.msda import attach_host_shapes
+
+    torch.manual_seed(0)
+    layer = pixel_decoder.MSDeformAttnTransformerEncoderLayer(256, 1024, 0.0, "relu", 3, 8, 4).to(device)
+    for p in layer.parameters():                 # reference init zeros the sampling weights; perturb them
+        p.data.add_(torch.randn_like(p) * 0.02)
+    shapes = [(8, 8), (16, 16), (32, 32)]
+    S = sum(h * w for h, w in shapes)
+    st = attach_host_shapes(torch.tensor(shapes, device=device), shapes)
+    lsi = torch.tensor([0, 64, 320], device=device)
+    enc = pixel_decoder.MSDeformAttnTransformerEncoder
+    ref_pts = enc.get_reference_points(shapes, torch.ones(2, 3, 2, device=device), device)
+    src0 = torch.randn(2, S, 256, device=device)
+    pos0 = torch.randn(2, S, 256, device=device)
+    gout = torch.randn(2, S, 256, device=device)
+    res = {}
+    for fused in (True, False):
+        pixel_decoder.RESIDUAL_FUSED = fused
+        try:
+            layer.zero_grad()
+            src = src0.clone().requires_grad_()
+            pos = pos0.clone().requires_grad_()
+            out = layer(src, pos, ref_pts, st, lsi)
+            out.backward(gout)
+            res[fused] = [out.detach(), src.grad, pos.grad] + [p.grad.clone() for p in layer.parameters()]
+        finally:
+            pixel_decoder.RESIDUAL_FUSED = True
+    assert torch.equal(res[True][0], res[False][0])
+    for a, b in zip(res[True][1:], res[False][1:]):
+        assert _rel(a, b) < 1e-6
