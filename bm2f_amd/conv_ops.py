@@ -11,12 +11,18 @@ else uses ``F.conv2d``.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 import torch.nn.functional as F
 from torch.autograd import Function
 
 from . import _native
+
+
+# 3x3 weight-gradient engine: "miopen" (fp32 igemm_wrw on NHWC transposes) or "x3" (csrc/conv_x3.hip; correct
+# but measured 27 vs 14 ms at bs16 256x256 (tools/conv_bench.py): both operands are channel-strided in NCHW)
+WGRAD3 = os.environ.get("M2F_CONV3_WGRAD", "miopen")
 
 
 def _stream(t):
@@ -61,10 +67,8 @@ class Conv2dX3(Function):
             _native.call("m2f_conv_f32x3", g.data_ptr(), weight.data_ptr(), None, dx.data_ptr(), N, Ci, Co, H, W, k, 1,
                          ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(g))
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if k == 3 and (ctx.needs_input_grad[1] or want_b):
-            # 3x3 weight gradient on the library: in NCHW both operands of this pixel reduction are
-            # channel-strided, and the wave-direct loads of the x3 kernel (one channel per lane) measured
-            # 1.7x slower than MIOpen here (tools/conv_bench.py); forward and input gradient stay x3
+        if k == 3 and WGRAD3 == "miopen" and (ctx.needs_input_grad[1] or want_b):
+            # 3x3 weight gradient on the library (default; M2F_CONV3_WGRAD=x3 selects the x3 kernel)
             _, dw, db = torch.ops.aten.convolution_backward(
                 g, x, weight, [Co] if want_b else None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                 [False, bool(ctx.needs_input_grad[1]), want_b])

@@ -227,21 +227,27 @@ __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __re
   const bool csum = bias_slab != nullptr && b1 == 0;
 
   struct Regs {
-    float a[8];
+    f4 a[3];
     f4 b[NJ][2];
   };
-  // chunk c: pixels m = r0 + 16c .. +15 of one image; lane rows 8lh .. 8lh+7 (same image row: W % 8 == 0)
+  // chunk c: pixels m = r0 + 16c .. +15 of one image; lane rows 8lh .. 8lh+7 (same image row: W % 8 == 0).
+  // A lane's 8 shifted pixels x0+dx .. x0+dx+7 come from three aligned float4 loads of its row (x0-4 ..
+  // x0+7 for dx = -1, x0 .. x0+11 for dx = +1; two for dx = 0) instead of eight scalar loads: a quarter
+  // of the address-unit work; the row edges are zeroed when the window is assembled (awin).
   auto gload = [&](Regs& r, int c) {
     const int64_t m = min(r0 + static_cast<int64_t>(c) * kBK, M - kBK);
     const int n = static_cast<int>(m / HW), p = static_cast<int>(m - static_cast<int64_t>(n) * HW);
     const int pa = p + lh * 8, y = pa / W, x0 = pa - y * W;
-    const float* src = I + (static_cast<int64_t>(n) * Ci + ci) * HW;
     const int yy = y + dy;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int xx = x0 + e + dx;
-      const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-      r.a[e] = src[ok ? yy * W + xx : 0];
+    const float* row = I + (static_cast<int64_t>(n) * Ci + ci) * HW + static_cast<int64_t>(yy >= 0 && yy < H ? yy : y) * W;
+    if (T == 1) {
+      r.a[0] = *reinterpret_cast<const f4*>(row + x0);
+      r.a[1] = *reinterpret_cast<const f4*>(row + x0 + 4);
+    } else {  // one code path for every tap: 12 pixels from base (x0 - 4, or x0 when dx = +1)
+      const int base = dx > 0 ? x0 : x0 - 4;
+      r.a[0] = *reinterpret_cast<const f4*>(row + max(base, 0));
+      r.a[1] = *reinterpret_cast<const f4*>(row + base + 4);
+      r.a[2] = *reinterpret_cast<const f4*>(row + min(base + 8, W - 4));
     }
 #pragma unroll
     for (int u = 0; u < NJ; ++u) {
@@ -280,12 +286,27 @@ __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __re
     const int64_t mc = min(m, M - kBK);
     const int n = static_cast<int>(mc / HW), p = static_cast<int>(mc - static_cast<int64_t>(n) * HW);
     const int pa = p + lh * 8, y = pa / W, x0 = pa - y * W, yy = y + dy;
+    const bool rok = live && yy >= 0 && yy < H;
+    float v[8];
+    if (T == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = r.a[e >> 2][e & 3];
+    } else {
+      // window start in the 12 loaded pixels: 3 (dx = -1), 4 (dx = 0), 1 (dx = +1); selects, no branches
+      const int st = dx > 0 ? 1 : 4 + dx;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float c1 = r.a[(e + 1) >> 2][(e + 1) & 3], c3 = r.a[(e + 3) >> 2][(e + 3) & 3];
+        const float c4 = r.a[(e + 4) >> 2][(e + 4) & 3];
+        v[e] = st == 1 ? c1 : (st == 3 ? c3 : c4);
+      }
+      if (dx < 0 && x0 == 0) v[0] = 0.f;      // left of the row
+      if (dx > 0 && x0 + 8 >= W) v[7] = 0.f;  // right of the row
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int xx = x0 + e + dx;
-      const bool ok = live && yy >= 0 && yy < H && xx >= 0 && xx < W;
       __bf16 h, mm, l;
-      split3(ok ? r.a[e] : 0.f, h, mm, l);
+      split3(rok ? v[e] : 0.f, h, mm, l);
       fa[0][e] = h; fa[1][e] = mm; fa[2][e] = l;
     }
   };

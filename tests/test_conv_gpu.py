@@ -17,8 +17,13 @@ def _rel(a, b):
 
 @pytest.mark.parametrize("N,Ci,Co,H,W,k,bias", [(2, 256, 256, 32, 32, 3, False), (1, 256, 256, 16, 24, 3, True),
                                                 (2, 512, 256, 16, 16, 1, True), (1, 2048, 256, 8, 16, 1, True),
-                                                (3, 256, 256, 8, 16, 1, False), (1, 32, 48, 8, 16, 3, True)])
-def test_conv_x3_vs_fp64(device, N, Ci, Co, H, W, k, bias):
+                                                (3, 256, 256, 8, 16, 1, False), (1, 32, 48, 8, 16, 3, True),
+                                                (2, 16, 32, 16, 8, 3, True), (1, 48, 16, 128, 8, 3, False)])
+@pytest.mark.parametrize("wgrad3", ["x3", "miopen"])
+def test_conv_x3_vs_fp64(device, N, Ci, Co, H, W, k, bias, wgrad3, monkeypatch):
+    if k == 1 and wgrad3 == "miopen":
+        pytest.skip("the switch only selects the 3x3 weight-gradient engine")
+    monkeypatch.setattr(conv_ops, "WGRAD3", wgrad3)
     torch.manual_seed(Ci + Co + H)
     conv = nn.Conv2d(Ci, Co, k, padding=k // 2, bias=bias).to(device)
     x = torch.randn(N, Ci, H, W, device=device, requires_grad=True)

@@ -1,0 +1,9 @@
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+timeout -k 10 300 python -u -m pytest tests/test_conv_gpu.py tests/test_modules_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/s5c_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/s5c_tests.log; exit 1; }
+tail -2 gpurun_out/s5c_tests.log
+timeout -k 10 300 python -u tools/conv_bench.py > gpurun_out/s5c_conv.log 2>&1 || { tail -20 gpurun_out/s5c_conv.log; exit 1; }
+cat gpurun_out/s5c_conv.log
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/s5c_bench.log 2>&1 || { tail -30 gpurun_out/s5c_bench.log; exit 1; }
+tail -1 gpurun_out/s5c_bench.log | cut -c1-400
