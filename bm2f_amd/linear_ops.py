@@ -248,12 +248,15 @@ class EncoderInProjF32(Function):
         s2 = _rows(src)
         if not s2.is_contiguous():
             s2 = s2.contiguous()
-        q2 = s2 + _rows(pos) if pos is not None else s2
+        # pos may be one (1, S, C) embedding shared by the batch: broadcast here, summed over the batch in
+        # the backward
+        q2 = (s2.view(src.shape) + pos).view(s2.shape) if pos is not None else s2
         value = gemm_nt(s2, wv, bv)
         proj = gemm_nt(q2, wq, bq)
         ctx.save_for_backward(s2, q2, wv, wq)
         ctx.in_shape = src.shape
         ctx.has_pos = pos is not None
+        ctx.pos_shape = pos.shape if pos is not None else None
         ctx.biases = (bv is not None, bq is not None)
         lead = src.shape[:-1]
         return value.view(*lead, wv.shape[0]), proj.view(*lead, wq.shape[0]), s2.view(src.shape)
@@ -269,6 +272,8 @@ class EncoderInProjF32(Function):
         if ctx.has_pos and nig[1]:
             dq = gemm_nt(gq, wq, b_kn=True)
             dpos = dq.view(ctx.in_shape)
+            if ctx.pos_shape != ctx.in_shape:
+                dpos = dpos.sum(0, keepdim=True)
             if nig[0]:
                 dsrc = gemm_nt(gv, wv, b_kn=True, add=(dq, gr)).view(ctx.in_shape)
         elif nig[0]:

@@ -304,7 +304,8 @@ class MSDeformAttn(nn.Module):
         input projections are one autograd node (:class:`linear_ops.EncoderInProjF32`) and the returned
         ``src`` carries the residual's gradient into that node's GEMM epilogues."""
         if (self._fusable(src, reference_points, src, input_spatial_shapes, input_padding_mask)
-                and (pos is None or (pos.shape == src.shape and pos.dtype == torch.float32))
+                and (pos is None or (pos.dtype == torch.float32 and pos.dim() == 3 and pos.shape[0] in (1, src.shape[0])
+                                     and pos.shape[1:] == src.shape[1:]))
                 and linear_ops.residual_fusable(src, self.value_proj)):
             N, Len_in, _ = src.shape
             w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)

@@ -158,7 +158,8 @@ def test_gemm_nt_addends_vs_fp64(device, M, N, K, n_add, bias, alias):
         assert out.data_ptr() == adds[0].data_ptr()
 
 
-def test_encoder_layer_residual_fused_matches_autograd_sums(device):
+@pytest.mark.parametrize("pos_batch", [2, 1])
+def test_encoder_layer_residual_fused_matches_autograd_sums(device, pos_batch):
     """The encoder layer with residual gradients summed in GEMM epilogues (EncoderInProjF32 /
     FFNResidualF32) against the same layer with plain autograd sums: outputs equal, gradients to fp32
     rounding of the reordered sums."""
@@ -176,7 +177,7 @@ def test_encoder_layer_residual_fused_matches_autograd_sums(device):
     enc = pixel_decoder.MSDeformAttnTransformerEncoder
     ref_pts = enc.get_reference_points(shapes, torch.ones(2, 3, 2, device=device), device)
     src0 = torch.randn(2, S, 256, device=device)
-    pos0 = torch.randn(2, S, 256, device=device)
+    pos0 = torch.randn(pos_batch, S, 256, device=device)      # 1: a batch-shared embedding, broadcast
     gout = torch.randn(2, S, 256, device=device)
     res = {}
     for fused in (True, False):
