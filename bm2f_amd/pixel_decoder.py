@@ -301,7 +301,7 @@ class MSDeformAttnPixelDecoder(nn.Module):
         for idx, f in enumerate(self.in_features[:self.num_fpn_levels][::-1]):
             x = features[f].float()
             cur_fpn = conv_ops.conv_norm_act(x, self.lateral_convs[idx])
-            y = cur_fpn + F.interpolate(out[-1], size=cur_fpn.shape[-2:], mode="bilinear", align_corners=False)
+            y = conv_ops.upsample_add(out[-1], cur_fpn)   # cur_fpn + bilinear resize of out[-1], one pass
             out.append(conv_ops.conv_norm_act(y, self.output_convs[idx]))
 
         multi_scale_features = out[:self.maskformer_num_feature_levels]

@@ -242,6 +242,18 @@ int m2f_conv_f32x3_wgrad(const float* grad_out, const float* I, float* dW_tck, f
 int m2f_bias_act_nchw(void* x, const void* residual, const float* bias, int64_t N, int C, int64_t HW, int dtype,
                       int channels_last, void* stream);
 
+/* FPN merge of the pixel decoder, msdeformattn.py:343-349 (the lateral plus the bilinear upsample of the
+ * coarser map, F.interpolate(..., mode="bilinear", align_corners=False)) for the exact 2x case, fp32:
+ * m2f_upsample2x_add_fwd_f32:  out[N][C][2h][2w] = lateral + up2x(src); src (N, C, h, w) read through
+ *   element strides (sN, sC, sY, sX), so a transposed (N, HW, C) view needs no copy.  2w % 4 == 0;
+ *   lateral and out contiguous, 16-byte aligned.
+ * m2f_upsample2x_bwd_f32:  grad_src[N][C][h][w] (contiguous) = the adjoint of up2x applied to
+ *   grad_out[N][C][2h][2w] (a gather with the forward's weights: deterministic, no atomics).  The
+ *   lateral's gradient is grad_out itself. */
+int m2f_upsample2x_add_fwd_f32(const float* src, int64_t sN, int64_t sC, int64_t sY, int64_t sX, const float* lateral,
+                               float* out, int N, int C, int h, int w, void* stream);
+int m2f_upsample2x_bwd_f32(const float* grad_out, float* grad_src, int N, int C, int h, int w, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Weak-supervision criterion (SUP_TYPE "mask_projection_and_pairwise"), SURVEY 8(f) ranks 1 and 3.
  * ------------------------------------------------------------------------------------------- */

@@ -48,3 +48,33 @@ def test_conv_x3_fallback_shapes(device):
     x = torch.randn(1, 256, 16, 16, device=device)
     assert not conv_ops.eligible(x, conv)
     torch.testing.assert_close(conv_ops.conv2d(x, conv), conv(x))
+
+
+@pytest.mark.parametrize("N,C,h,w,transposed", [(2, 256, 16, 16, True), (1, 8, 5, 6, False), (3, 4, 1, 2, True),
+                                                (2, 16, 7, 10, False)])
+def test_upsample2x_add_vs_fp64(device, N, C, h, w, transposed):
+    """conv_ops.upsample_add (csrc/upsample.hip) = lateral + F.interpolate(bilinear, align_corners=False) at
+    2x, forward and both gradients, against fp64 torch; the coarse map as the encoder's transposed view."""
+    torch.manual_seed(N * 100 + h)
+    if transposed:
+        z = torch.randn(N, h * w, C, device=device, requires_grad=True)
+        src = z.transpose(1, 2).view(N, C, h, w)
+    else:
+        z = torch.randn(N, C, h, w, device=device, requires_grad=True)
+        src = z
+    lat = torch.randn(N, C, 2 * h, 2 * w, device=device, requires_grad=True)
+    y = conv_ops.upsample_add(src, lat)
+    g = torch.randn_like(y)
+    y.backward(g)
+    zd = z.detach().double().requires_grad_()
+    srcd = zd.transpose(1, 2).reshape(N, C, h, w) if transposed else zd
+    latd = lat.detach().double().requires_grad_()
+    yd = latd + F.interpolate(srcd, size=(2 * h, 2 * w), mode="bilinear", align_corners=False)
+    yd.backward(g.double())
+    assert y.is_contiguous()
+    assert _rel(y, yd) < 1e-6
+    assert _rel(z.grad, zd.grad) < 1e-6
+    assert torch.equal(lat.grad, g)
+    # the library's fp32 result for the same inputs (its NHWC path for the transposed view)
+    torch.testing.assert_close(y, lat + F.interpolate(src, size=(2 * h, 2 * w), mode="bilinear",
+                                                      align_corners=False), rtol=1e-6, atol=1e-6)

@@ -1,8 +1,14 @@
 """FPN merge of the pixel decoder (msdeformattn.py:343-349): lateral + bilinear 2x upsample of the encoder's
 finest map, which arrives as a transposed (N, HW, C) view.  Times the layout variants, fwd + bwd.
 python tools/fpn_bench.py"""
+import os
+import sys
+
 import torch
 import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bm2f_amd import conv_ops  # noqa: E402
 
 
 def timeit(fn, iters=10):
@@ -30,9 +36,15 @@ def main():
         "contiguous out": lambda src: F.interpolate(src, size=(2 * h, 2 * w), mode="bilinear",
                                                     align_corners=False).contiguous(),
     }
+    variants["fused (upsample.hip)"] = None
+    variants["fused, contiguous in"] = "c"
     ref = None
     for name, up in variants.items():
         def fwd():
+            if up is None:
+                return conv_ops.upsample_add(z.transpose(1, 2).view(N, C, h, w), lat)
+            if up == "c":
+                return conv_ops.upsample_add(z.transpose(1, 2).contiguous().view(N, C, h, w), lat)
             return lat + up(z.transpose(1, 2).view(N, C, h, w))
         y = fwd()
         if ref is None:
