@@ -92,6 +92,41 @@ def bias_act(x, bias, residual=None):
     return F.relu(y)
 
 
+class _MaxPool3s2(torch.autograd.Function):
+    """``F.max_pool2d(x, 3, 2, 1)`` (NCHW) with a 1-byte winner position per window (csrc/eltwise.hip)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        from . import _native
+        N, C, H, W = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty(N, C, OH, OW, device=x.device, dtype=x.dtype)
+        win = torch.empty(N, C, OH, OW, device=x.device, dtype=torch.uint8)
+        _native.call("m2f_maxpool3s2_fwd", x.data_ptr(), y.data_ptr(), win.data_ptr(), N * C, H, W,
+                     {torch.bfloat16: 2, torch.float32: 0}[x.dtype], torch.cuda.current_stream(x.device).cuda_stream)
+        ctx.save_for_backward(win)
+        ctx.in_shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, grad):
+        from . import _native
+        (win,) = ctx.saved_tensors
+        g = grad.contiguous()
+        N, C, H, W = ctx.in_shape
+        gx = torch.empty(ctx.in_shape, device=g.device, dtype=g.dtype)
+        _native.call("m2f_maxpool3s2_bwd", g.data_ptr(), win.data_ptr(), gx.data_ptr(), N * C, H, W,
+                     {torch.bfloat16: 2, torch.float32: 0}[g.dtype], torch.cuda.current_stream(g.device).cuda_stream)
+        return gx
+
+
+def max_pool_stem(x):
+    """detectron2 BasicStem's ``F.max_pool2d(x, kernel_size=3, stride=2, padding=1)``."""
+    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 4 and x.is_contiguous():
+        return _MaxPool3s2.apply(x)
+    return F.max_pool2d(x, kernel_size=3, stride=2, padding=1)
+
+
 class Bottleneck(nn.Module):
     def __init__(self, cin, cb, cout, stride):
         super().__init__()
@@ -133,7 +168,7 @@ class ResNet50(nn.Module):
 
     def forward(self, x):
         x = bias_act(*self.stem.conv_shift(x))
-        x = F.max_pool2d(x, kernel_size=3, stride=2, padding=1)
+        x = max_pool_stem(x)
         out = {}
         for name in self.stage_names:
             x = getattr(self, name)(x)

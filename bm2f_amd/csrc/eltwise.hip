@@ -61,3 +61,106 @@ extern "C" int m2f_bias_act_nchw(void* x, const void* residual, const float* bia
 #undef M2F_BA
   return m2f::check_launch(fn);
 }
+
+// ---------------------------------------------------------------------------------------------------
+// The benchmark backbone's stem max pool, kernel 3, stride 2, padding 1 (detectron2 BasicStem), NCHW.
+// Forward: torch's max_pool2d_with_indices rule (first maximum in window order, NaN wins), the winner
+// kept as a 1-byte window position (0..8) instead of an int64 flat index.  Backward: each input pixel
+// gathers the gradients of the <= 2 x 2 windows whose winner it is, in torch's (ph, pw) order with an fp32
+// sum -- the same arithmetic as max_pool_backward_nchw, on 1/8 of its index bytes.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool3s2_fwd(const T* __restrict__ x, T* __restrict__ y,
+                                                     uint8_t* __restrict__ win, int H, int W, int OH, int OW,
+                                                     int64_t total) {
+  const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (t >= total) return;
+  const int ow = static_cast<int>(t % OW);
+  const int64_t r = t / OW;
+  const int oh = static_cast<int>(r % OH);
+  const int64_t plane = r / OH;
+  const T* xp = x + plane * H * W;
+  const int h0 = 2 * oh - 1, w0 = 2 * ow - 1;
+  const int hs = max(h0, 0), he = min(h0 + 3, H), ws = max(w0, 0), we = min(w0 + 3, W);
+  float best = -INFINITY;
+  int bi = (hs - h0) * 3 + (ws - w0);
+  for (int h = hs; h < he; ++h)
+    for (int w = ws; w < we; ++w) {
+      const float v = static_cast<float>(xp[h * W + w]);
+      if (v > best || v != v) {
+        best = v;
+        bi = (h - h0) * 3 + (w - w0);
+      }
+    }
+  y[t] = static_cast<T>(best);
+  win[t] = static_cast<uint8_t>(bi);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool3s2_bwd(const T* __restrict__ gy, const uint8_t* __restrict__ win,
+                                                     T* __restrict__ gx, int H, int W, int OH, int OW,
+                                                     int64_t total) {
+  const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (t >= total) return;
+  const int w = static_cast<int>(t % W);
+  const int64_t r = t / W;
+  const int h = static_cast<int>(r % H);
+  const int64_t plane = r / H;
+  // windows ph with 2 ph - 1 <= h <= 2 ph + 1 (torch: phstart = h + 1 < 3 ? 0 : (h + 1 - 3) / 2 + 1)
+  const int phs = h + 1 < 3 ? 0 : (h - 2) / 2 + 1, phe = min((h + 1) / 2 + 1, OH);
+  const int pws = w + 1 < 3 ? 0 : (w - 2) / 2 + 1, pwe = min((w + 1) / 2 + 1, OW);
+  const T* gp = gy + plane * OH * OW;
+  const uint8_t* wp = win + plane * OH * OW;
+  float acc = 0.f;
+  for (int ph = phs; ph < phe; ++ph)
+    for (int pw = pws; pw < pwe; ++pw) {
+      const int o = ph * OW + pw;
+      if (wp[o] == (h - (2 * ph - 1)) * 3 + (w - (2 * pw - 1))) acc += static_cast<float>(gp[o]);
+    }
+  gx[t] = static_cast<T>(acc);
+}
+
+}  // namespace
+
+extern "C" int m2f_maxpool3s2_fwd(const void* x, void* y, uint8_t* window, int64_t planes, int H, int W, int dtype,
+                                  void* stream) {
+  const char* fn = "m2f_maxpool3s2_fwd";
+  if (!x || !y || !window || planes < 0 || H <= 0 || W <= 0) return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int64_t total = planes * OH * OW;
+  if (total == 0) return m2f::ok();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = m2f::ceil_div(total, 256);
+  if (dtype == M2F_BF16)
+    maxpool3s2_fwd<__bf16><<<grid, 256, 0, st>>>(static_cast<const __bf16*>(x), static_cast<__bf16*>(y), window, H,
+                                                 W, OH, OW, total);
+  else if (dtype == M2F_F32)
+    maxpool3s2_fwd<float><<<grid, 256, 0, st>>>(static_cast<const float*>(x), static_cast<float*>(y), window, H, W,
+                                                OH, OW, total);
+  else
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  return m2f::check_launch(fn);
+}
+
+extern "C" int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, int64_t planes, int H,
+                                  int W, int dtype, void* stream) {
+  const char* fn = "m2f_maxpool3s2_bwd";
+  if (!grad_y || !window || !grad_x || planes < 0 || H <= 0 || W <= 0)
+    return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int64_t total = planes * H * W;
+  if (total == 0) return m2f::ok();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = m2f::ceil_div(total, 256);
+  if (dtype == M2F_BF16)
+    maxpool3s2_bwd<__bf16><<<grid, 256, 0, st>>>(static_cast<const __bf16*>(grad_y), window,
+                                                 static_cast<__bf16*>(grad_x), H, W, OH, OW, total);
+  else if (dtype == M2F_F32)
+    maxpool3s2_bwd<float><<<grid, 256, 0, st>>>(static_cast<const float*>(grad_y), window,
+                                                static_cast<float*>(grad_x), H, W, OH, OW, total);
+  else
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  return m2f::check_launch(fn);
+}

@@ -242,6 +242,15 @@ int m2f_conv_f32x3_wgrad(const float* grad_out, const float* I, float* dW_tck, f
 int m2f_bias_act_nchw(void* x, const void* residual, const float* bias, int64_t N, int C, int64_t HW, int dtype,
                       int channels_last, void* stream);
 
+/* The benchmark backbone's stem max pool (kernel 3, stride 2, padding 1; detectron2 BasicStem; not on the
+ * reference's hot path), NCHW, dtype M2F_BF16 or M2F_F32, planes = N*C, output (H-1)/2+1 x (W-1)/2+1.
+ * m2f_maxpool3s2_fwd: torch's max_pool2d_with_indices rule (first maximum in window order, NaN wins); the
+ *   winner's window position (0..8) goes to window[planes][OH][OW] (1 byte instead of an int64 index).
+ * m2f_maxpool3s2_bwd: grad_x = each input pixel's sum over the windows it won (torch's order, fp32). */
+int m2f_maxpool3s2_fwd(const void* x, void* y, uint8_t* window, int64_t planes, int H, int W, int dtype, void* stream);
+int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, int64_t planes, int H, int W, int dtype,
+                       void* stream);
+
 /* FPN merge of the pixel decoder, msdeformattn.py:343-349 (the lateral plus the bilinear upsample of the
  * coarser map, F.interpolate(..., mode="bilinear", align_corners=False)) for the exact 2x case, fp32:
  * m2f_upsample2x_add_fwd_f32:  out[N][C][2h][2w] = lateral + up2x(src); src (N, C, h, w) read through

@@ -27,3 +27,26 @@ def test_bias_act_matches_unfused(device, dtype, residual):
     torch.testing.assert_close(xa.grad, torch.where(mask, g, torch.zeros_like(g)))
     if residual:
         torch.testing.assert_close(ra.grad, torch.where(mask, g, torch.zeros_like(g)))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("H,W", [(16, 24), (7, 9), (1, 1), (2, 3)])
+def test_stem_maxpool_matches_torch(device, dtype, H, W):
+    """The stem max pool (csrc/eltwise.hip, 1-byte winners) against F.max_pool2d(3, 2, 1): forward and
+    gradient bit-exact, with ties (integer-valued inputs), -inf and NaN."""
+    from bm2f_amd.bench_model import max_pool_stem
+    torch.manual_seed(H * 31 + W)
+    x = torch.randint(-3, 4, (2, 5, H, W), device=device).to(dtype)     # many ties
+    x.view(-1)[::7] = float("-inf")
+    if H * W > 4:
+        x.view(-1)[5] = float("nan")
+    xa = x.clone().requires_grad_()
+    xb = x.clone().requires_grad_()
+    ya = max_pool_stem(xa)
+    yb = F.max_pool2d(xb, kernel_size=3, stride=2, padding=1)
+    assert torch.equal(ya.isnan(), yb.isnan())
+    assert torch.equal(ya.nan_to_num(), yb.nan_to_num())
+    g = torch.randn_like(ya)
+    ya.backward(g)
+    yb.backward(g)
+    assert torch.equal(xa.grad, xb.grad)
