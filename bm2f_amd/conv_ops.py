@@ -150,3 +150,48 @@ def upsample_add(src, lateral):
     if ok:
         return Upsample2xAdd.apply(src, lateral)
     return lateral + F.interpolate(src, size=lateral.shape[-2:], mode="bilinear", align_corners=False)
+
+
+def _transpose(src, in_bs, in_ld, dst, out_bs, out_ld, B, R, Q):
+    _native.call("m2f_transpose_f32", src, ctypes.c_int64(in_bs), ctypes.c_int64(in_ld), dst, ctypes.c_int64(out_bs),
+                 ctypes.c_int64(out_ld), B, R, Q, torch.cuda.current_stream().cuda_stream)
+
+
+class FlattenLevels(Function):
+    """``torch.cat([x.flatten(2).transpose(1, 2) for x in xs], 1)`` for NCHW fp32 levels (msdeformattn.py:64-74)
+    with LDS-tiled transposes each way (csrc/eltwise.hip) instead of a strided cat."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        N, C = xs[0].shape[:2]
+        sizes = [x.shape[2] * x.shape[3] for x in xs]
+        S = sum(sizes)
+        out = torch.empty(N, S, C, device=xs[0].device, dtype=torch.float32)
+        start = 0
+        for x, hw in zip(xs, sizes):
+            x = x.contiguous()
+            _transpose(x.data_ptr(), C * hw, hw, out.data_ptr() + start * C * 4, S * C, C, N, C, hw)
+            start += hw
+        ctx.shapes = [x.shape for x in xs]
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        g = grad.contiguous()
+        N, S, C = g.shape
+        grads, start = [], 0
+        for shp in ctx.shapes:
+            hw = shp[2] * shp[3]
+            gx = torch.empty(shp, device=g.device, dtype=torch.float32)
+            _transpose(g.data_ptr() + start * C * 4, S * C, C, gx.data_ptr(), C * hw, hw, N, hw, C)
+            grads.append(gx)
+            start += hw
+        return tuple(grads)
+
+
+def flatten_levels(xs):
+    """``torch.cat([x.flatten(2).transpose(1, 2) for x in xs], 1)``: (N, C, H_l, W_l) levels -> (N, S, C)."""
+    if all(x.is_cuda and x.dtype == torch.float32 and x.dim() == 4 and x.shape[:2] == xs[0].shape[:2] for x in xs) \
+            and xs[0].shape[0] <= 65535:
+        return FlattenLevels.apply(*xs)
+    return torch.cat([x.flatten(2).transpose(1, 2) for x in xs], 1)

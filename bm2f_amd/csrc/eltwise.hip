@@ -164,3 +164,46 @@ extern "C" int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, voi
     return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
   return m2f::check_launch(fn);
 }
+
+// ---------------------------------------------------------------------------------------------------
+// Batched fp32 transpose out[b][q][r] = in[b][r][q] through 64x64 LDS tiles (both sides coalesced): the
+// pixel decoder's level flatten, cat([x_l.flatten(2).transpose(1, 2)], 1) (msdeformattn.py:64-74), and its
+// backward, without the library's strided cat.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+__global__ void __launch_bounds__(256) transpose_f32(const float* __restrict__ in, int64_t in_bs, int64_t in_ld,
+                                                    float* __restrict__ out, int64_t out_bs, int64_t out_ld, int R,
+                                                    int Q) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z;
+  const int r0 = blockIdx.y * 64, q0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const float* ip = in + b * in_bs;
+  float* op = out + b * out_bs;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int r = r0 + ty + 4 * k, q = q0 + tx;
+    if (r < R && q < Q) tile[ty + 4 * k][tx] = ip[static_cast<int64_t>(r) * in_ld + q];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int q = q0 + ty + 4 * k, r = r0 + tx;
+    if (r < R && q < Q) op[static_cast<int64_t>(q) * out_ld + r] = tile[tx][ty + 4 * k];
+  }
+}
+
+}  // namespace
+
+extern "C" int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, float* out, int64_t out_bs,
+                                 int64_t out_ld, int B, int R, int Q, void* stream) {
+  const char* fn = "m2f_transpose_f32";
+  if (!in || !out || B < 0 || R < 0 || Q < 0 || in_ld < Q || out_ld < R)
+    return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  if (B == 0 || R == 0 || Q == 0) return m2f::ok();
+  if (B > 65535) return m2f::fail(M2F_EUNSUPPORTED, "%s: batch %d > 65535", fn, B);
+  const dim3 grid((Q + 63) / 64, (R + 63) / 64, B);
+  transpose_f32<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(in, in_bs, in_ld, out, out_bs, out_ld, R, Q);
+  return m2f::check_launch(fn);
+}

@@ -180,7 +180,7 @@ class MSDeformAttnTransformerEncoderOnly(nn.Module):
     def forward(self, srcs, pos_embeds):
         """srcs / pos_embeds: lists of (N, C, H_l, W_l), coarse -> fine (msdeformattn.py:61-89)."""
         host_shapes = [(int(x.shape[2]), int(x.shape[3])) for x in srcs]
-        src_flatten = torch.cat([s.flatten(2).transpose(1, 2) for s in srcs], 1)
+        src_flatten = conv_ops.flatten_levels(srcs)   # cat of the transposed levels, tiled transposes
         if all(p.dim() == 4 and p.stride(0) == 0 for p in pos_embeds):
             # batch-broadcast embeddings (PositionEmbeddingSine without a padding mask): keep one (1, S, C)
             # copy; the layers broadcast it, and its gradient is (1, S, C) instead of (N, S, C) per layer

@@ -251,6 +251,12 @@ int m2f_maxpool3s2_fwd(const void* x, void* y, uint8_t* window, int64_t planes, 
 int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, int64_t planes, int H, int W, int dtype,
                        void* stream);
 
+/* Batched fp32 transpose out[b][q][r] = in[b][r][q] (row strides in_ld / out_ld, batch strides in_bs /
+ * out_bs, in elements; B <= 65535): the pixel decoder's level flatten, cat([x_l.flatten(2).transpose(1, 2)],
+ * 1) (msdeformattn.py:64-74), and its backward. */
+int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, float* out, int64_t out_bs, int64_t out_ld,
+                      int B, int R, int Q, void* stream);
+
 /* FPN merge of the pixel decoder, msdeformattn.py:343-349 (the lateral plus the bilinear upsample of the
  * coarser map, F.interpolate(..., mode="bilinear", align_corners=False)) for the exact 2x case, fp32:
  * m2f_upsample2x_add_fwd_f32:  out[N][C][2h][2w] = lateral + up2x(src); src (N, C, h, w) read through

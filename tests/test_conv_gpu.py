@@ -78,3 +78,19 @@ def test_upsample2x_add_vs_fp64(device, N, C, h, w, transposed):
     # the library's fp32 result for the same inputs (its NHWC path for the transposed view)
     torch.testing.assert_close(y, lat + F.interpolate(src, size=(2 * h, 2 * w), mode="bilinear",
                                                       align_corners=False), rtol=1e-6, atol=1e-6)
+
+
+def test_flatten_levels_matches_cat(device):
+    """conv_ops.flatten_levels (LDS-tiled transposes) = cat of the transposed levels, values and gradients
+    exact (pure data movement), ragged level sizes included."""
+    torch.manual_seed(0)
+    xs = [torch.randn(3, 40, h, w, device=device, requires_grad=True) for h, w in ((4, 4), (9, 7), (16, 33))]
+    ys = [x.detach().clone().requires_grad_() for x in xs]
+    a = conv_ops.flatten_levels(xs)
+    b = torch.cat([y.flatten(2).transpose(1, 2) for y in ys], 1)
+    assert torch.equal(a, b)
+    g = torch.randn_like(a)
+    a.backward(g)
+    b.backward(g)
+    for x, y in zip(xs, ys):
+        assert torch.equal(x.grad, y.grad)
