@@ -305,10 +305,47 @@ class _TokenLinear(Function):
         return gx, gw, gb
 
 
-def token_linear(x, weight, bias=None):
-    """``F.linear`` for memory-token projections (autocast applied here as F.linear would)."""
+class _TokenLinearCast(Function):
+    """:class:`_TokenLinear` on a low-precision copy of x made once per forward (``x_lp``, shared by the
+    decoder layers that read the same level) whose gradient returns to the fp32 x in fp32: the same
+    values autocast's per-call cast gives (the bf16 input-gradient GEMM result, then its ToCopy back to
+    fp32, summed over the layers in fp32), without casting the memory tokens again in every layer."""
+
+    @staticmethod
+    def forward(ctx, x, x_lp, weight, bias):
+        ctx.save_for_backward(x_lp, weight)
+        ctx.has_bias = bias is not None
+        ctx.x_dtype = x.dtype
+        return F.linear(x_lp, weight, bias)
+
+    @staticmethod
+    def backward(ctx, grad):
+        x_lp, w = ctx.saved_tensors
+        g = _TokenLinear.backward(_SavedLike(ctx, x_lp, w), grad)
+        gx = g[0].to(ctx.x_dtype) if g[0] is not None else None
+        return gx, None, g[1], g[2]
+
+
+class _SavedLike:
+    """The ctx view :meth:`_TokenLinear.backward` expects (saved x, w; needs_input_grad for x, w, b)."""
+
+    def __init__(self, ctx, x, w):
+        self.saved_tensors = (x, w)
+        self.has_bias = ctx.has_bias
+        n = ctx.needs_input_grad
+        self.needs_input_grad = (n[0], n[2], n[3])
+
+
+def token_linear(x, weight, bias=None, x_lp=None):
+    """``F.linear`` for memory-token projections (autocast applied here as F.linear would).  ``x_lp``: an
+    optional detached copy of x in the autocast dtype, made once and shared by several calls."""
     if x.is_cuda and torch.is_autocast_enabled("cuda"):
         dt = torch.get_autocast_dtype("cuda")
+        if x_lp is not None and x_lp.dtype == dt and x.dtype != dt and dt in (torch.bfloat16, torch.float16):
+            weight = weight.to(dt)
+            bias = bias.to(dt) if bias is not None else None
+            with torch.autocast("cuda", enabled=False):
+                return _TokenLinearCast.apply(x, x_lp, weight, bias)
         x, weight = x.to(dt), weight.to(dt)
         bias = bias.to(dt) if bias is not None else None
     if x.dtype not in (torch.bfloat16, torch.float16) or not x.is_cuda:

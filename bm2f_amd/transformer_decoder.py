@@ -97,30 +97,32 @@ class CrossAttentionLayer(nn.Module):
             if p.dim() > 1:
                 nn.init.xavier_uniform_(p)
 
-    def _attend(self, query, key, value, bits):
+    def _attend(self, query, key, value, bits, lowp=None):
         a = self.multihead_attn
         if a.dropout and self.training:
             raise NotImplementedError("attention dropout > 0 is not supported by the masked-attention kernel")
         C = query.shape[-1]
         w, b = a.in_proj_weight, a.in_proj_bias
         q = F.linear(query, w[:C], b[:C])
-        k = decoder_ops.token_linear(key, w[C:2 * C], b[C:2 * C])
-        v = decoder_ops.token_linear(value, w[2 * C:], b[2 * C:])
+        k_lp, v_lp = lowp if lowp is not None else (None, None)
+        k = decoder_ops.token_linear(key, w[C:2 * C], b[C:2 * C], x_lp=k_lp)
+        v = decoder_ops.token_linear(value, w[2 * C:], b[2 * C:], x_lp=v_lp)
         o = decoder_ops.masked_attention(q, k, v, bits, a.num_heads)
         return F.linear(o, a.out_proj.weight, a.out_proj.bias)
 
     def forward(self, tgt, memory, memory_mask=None, memory_key_padding_mask=None, pos=None, query_pos=None,
-                memory_plus_pos=None):
-        """memory_mask: bits (B, Q, words) from decoder_ops.attn_mask_bits."""
+                memory_plus_pos=None, memory_lowp=None):
+        """memory_mask: bits (B, Q, words) from decoder_ops.attn_mask_bits.  memory_lowp: optional detached
+        autocast-dtype copies (key, memory) made once per forward for the layers sharing a level."""
         if memory_key_padding_mask is not None:
             raise NotImplementedError("the decoder passes no key padding mask (reference :405)")
         key = memory_plus_pos if memory_plus_pos is not None else (memory if pos is None else memory + pos)
         if self.normalize_before:
             t2 = self.norm(tgt)
             q = t2 if query_pos is None else t2 + query_pos
-            return tgt + self.dropout(self._attend(q, key, memory, memory_mask))
+            return tgt + self.dropout(self._attend(q, key, memory, memory_mask, memory_lowp))
         q = tgt if query_pos is None else tgt + query_pos
-        return self.norm(tgt + self.dropout(self._attend(q, key, memory, memory_mask)))
+        return self.norm(tgt + self.dropout(self._attend(q, key, memory, memory_mask, memory_lowp)))
 
 
 class FFNLayer(nn.Module):
@@ -254,6 +256,18 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         return src, pos, key, size_list
 
     @staticmethod
+    def _lowp_levels(src, key):
+        """Per level, (key, memory) cast once to the autocast dtype for the K/V projections of the layers
+        that read the level (3 each at 9 layers / 3 levels); gradients still return in fp32 per layer."""
+        dev = src[0].device.type
+        if dev != "cuda" or not torch.is_autocast_enabled(dev):
+            return [None] * len(src)
+        dt = torch.get_autocast_dtype(dev)
+        if src[0].dtype == dt:
+            return [None] * len(src)
+        return [(k.detach().to(dt), s.detach().to(dt)) for s, k in zip(src, key)]
+
+    @staticmethod
     def _lowp_features(mask_features):
         """The einsum operand under autocast: cast once per forward, outside the autograd graph (the
         einsum's backward returns the features' gradient in their own dtype)."""
@@ -267,6 +281,7 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         assert len(x) == self.num_feature_levels
         del mask
         src, pos, key, size_list = self._levels(x)
+        lowp = self._lowp_levels(src, key)
         bs = src[0].shape[0]
         query_embed = self.query_embed.weight.unsqueeze(0).expand(bs, -1, -1)
         output = self.query_feat.weight.unsqueeze(0).repeat(bs, 1, 1)
@@ -283,7 +298,8 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
             level_index = i % self.num_feature_levels
             output = self.transformer_cross_attention_layers[i](
                 output, src[level_index], memory_mask=attn_mask, memory_key_padding_mask=None,
-                pos=pos[level_index], query_pos=query_embed, memory_plus_pos=key[level_index])
+                pos=pos[level_index], query_pos=query_embed, memory_plus_pos=key[level_index],
+                memory_lowp=lowp[level_index])
             output = self.transformer_self_attention_layers[i](output, tgt_mask=None, tgt_key_padding_mask=None,
                                                                query_pos=query_embed)
             output = self.transformer_ffn_layers[i](output)

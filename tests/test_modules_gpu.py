@@ -51,3 +51,30 @@ def test_decoder_teacher_forced_masks_exact(device):
         want = g[f"attn_mask{i}"]
         got = unpack_bits(bits.cpu(), want.shape[-1]).numpy()
         assert (got == want).all(), f"head {i}: {(got != want).sum()} bits differ"
+
+
+def test_decoder_amp_cast_once_matches_per_layer_casts(device, monkeypatch):
+    """Under bf16 autocast the decoder casts each level's memory tokens once per forward
+    (_lowp_levels / token_linear x_lp) instead of in every layer: outputs identical, input gradients equal
+    up to the order of the fp32 gradient sums."""
+    from bm2f_amd.transformer_decoder import MultiScaleMaskedTransformerDecoder as Dec
+    torch.manual_seed(0)
+    d = build_decoder().to(device)
+    x0 = [torch.randn(2, 256, s, s, device=device) for s in (4, 8, 16)]
+    mf0 = torch.randn(2, 256, 32, 32, device=device)
+    res = {}
+    for once in (True, False):
+        if not once:
+            monkeypatch.setattr(Dec, "_lowp_levels", staticmethod(lambda src, key: [None] * len(src)))
+        x = [t.clone().requires_grad_() for t in x0]
+        mf = mf0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = d(x, mf)
+            loss = sum(h["pred_masks"].float().square().mean() + h["pred_logits"].float().square().mean()
+                       for h in [out] + out["aux_outputs"])
+        loss.backward()
+        res[once] = (out["pred_masks"].detach(), [t.grad for t in x], mf.grad)
+    assert torch.equal(res[True][0], res[False][0])
+    for a, b in zip(res[True][1], res[False][1]):
+        assert rel_err(a.cpu(), b.cpu().numpy()) < 1e-5
+    assert rel_err(res[True][2].cpu(), res[False][2].cpu().numpy()) < 1e-5
