@@ -786,17 +786,49 @@ __global__ void __launch_bounds__(256) msda_gv_combine(const float* __restrict__
 // group computes softmax over the L*P logits and loc = ref + offset / (W_l, H_l) exactly as the
 // reference module does (ms_deform_attn.py:102-109), then samples as msda_fwd_f32_vec.
 // ------------------------------------------------------------------------------------------------
-template <int LT>
+//
+// TILED: a workgroup takes one head of an 8 x 4 patch of queries of one level instead of 4 consecutive
+// queries x 8 heads, with the head as the fastest block index: every XCD (blocks are dealt round-robin)
+// then gathers one head's value rows (2.75 MB per 1024^2 image, L2-resident) and a block's 32 queries
+// sample one compact neighbourhood of them (L1 reuse across the patch).  Needs Lq == S (encoder queries
+// are the pixels).
+template <int LT, bool TILED>
 __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ value, FrontEnd fe, TileGeom geo,
                                                       int64_t npairs, int S, int M, int Lq, float* __restrict__ out) {
   constexpr int D = 32, G = 8, P = 4, LP = LT * P;
-  const int64_t pair = static_cast<int64_t>(blockIdx.x) * (256 / G) + threadIdx.x / G;
-  if (pair >= npairs) return;
+  int64_t pair, n;
+  int m, q;
+  if constexpr (TILED) {
+    const int g = threadIdx.x / G;
+    int64_t b = blockIdx.x;
+    m = static_cast<int>(b % M);
+    b /= M;
+    int T = 0;
+#pragma unroll
+    for (int l = 0; l < LT; ++l) T += ((geo.H[l] + 3) / 4) * ((geo.W[l] + 7) / 8);
+    n = b / T;
+    int t = static_cast<int>(b - n * T);
+    int lv = 0;
+#pragma unroll
+    for (int l = 0; l < LT - 1; ++l) {
+      const int nt = ((geo.H[l] + 3) / 4) * ((geo.W[l] + 7) / 8);
+      if (lv == l && t >= nt) { t -= nt; lv = l + 1; }
+    }
+    const int H = geo.H[lv], W = geo.W[lv], tlx = (W + 7) / 8;
+    const int y = (t / tlx) * 4 + (g >> 3), x = (t % tlx) * 8 + (g & 7);
+    if (y >= H || x >= W) return;
+    q = geo.start[lv] + y * W + x;
+    pair = (n * Lq + q) * M + m;
+  } else {
+    pair = static_cast<int64_t>(blockIdx.x) * (256 / G) + threadIdx.x / G;
+    if (pair >= npairs) return;
+    m = static_cast<int>(pair % M);
+    const int64_t nq0 = pair / M;
+    n = nq0 / Lq;
+    q = static_cast<int>(nq0 - n * Lq);
+  }
   const int j = threadIdx.x % G;
-  const int m = static_cast<int>(pair % M);
-  const int64_t nq = pair / M;
-  const int64_t n = nq / Lq;
-  const int q = static_cast<int>(nq - n * Lq);
+  const int64_t nq = n * Lq + q;
   const int64_t rs = static_cast<int64_t>(M) * D;
   const float* prow = fe.proj + nq * fe.ld;
   const float* rrow = fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * LT * 2;
@@ -1133,13 +1165,35 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
   if (!output || !m2f::aligned(output, 16)) return m2f::fail(M2F_EINVAL, "%s: bad output", fn);
   const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const unsigned grid = m2f::ceil_div(d.npairs(), 32);
-  switch (d.L) {
-    case 1: msda_fused_fwd<1><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output); break;
-    case 2: msda_fused_fwd<2><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output); break;
-    case 3: msda_fused_fwd<3><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output); break;
-    default: msda_fused_fwd<4><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output); break;
+  static const bool tiled_env = [] {
+    const char* e = std::getenv("M2F_MSDA_FWD_TILED");
+    return !(e && e[0] == '0');
+  }();
+  if (tiled_env && d.Lq == d.S) {
+    int64_t T = 0;
+    for (int l = 0; l < d.L; ++l) T += static_cast<int64_t>((geo.H[l] + 3) / 4) * ((geo.W[l] + 7) / 8);
+    const int64_t nb = T * d.M * d.N;
+    if (nb > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many workgroups", fn);
+    const unsigned tg = static_cast<unsigned>(nb);
+#define M2F_FFT(LT) msda_fused_fwd<LT, true><<<tg, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output)
+    switch (d.L) {
+      case 1: M2F_FFT(1); break;
+      case 2: M2F_FFT(2); break;
+      case 3: M2F_FFT(3); break;
+      default: M2F_FFT(4); break;
+    }
+#undef M2F_FFT
+    return m2f::check_launch(fn);
   }
+  const unsigned grid = m2f::ceil_div(d.npairs(), 32);
+#define M2F_FF(LT) msda_fused_fwd<LT, false><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output)
+  switch (d.L) {
+    case 1: M2F_FF(1); break;
+    case 2: M2F_FF(2); break;
+    case 3: M2F_FF(3); break;
+    default: M2F_FF(4); break;
+  }
+#undef M2F_FF
   return m2f::check_launch(fn);
 }
 
