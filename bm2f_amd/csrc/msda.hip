@@ -338,7 +338,8 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   __shared__ TileState ts;
 
-  const int tile = blockIdx.x, m = blockIdx.y, n = blockIdx.z;
+  const int tile = geo.head_major ? blockIdx.y : blockIdx.x, m = geo.head_major ? blockIdx.x : blockIdx.y;
+  const int n = blockIdx.z;
   const int ty = tile / geo.ntx, tx = tile - ty * geo.ntx;
   const int L = LT > 0 ? LT : geo.L;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwaves = blockDim.x >> 6;
@@ -973,6 +974,9 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   geo.ablate = env_int("M2F_MSDA_ABLATE", 0);
   geo.bbox = env_int("M2F_MSDA_BBOX", 1);
   geo.exact = env_int("M2F_MSDA_DETERMINISTIC", 1);  // default: bitwise-repeatable gradients (+0.17 ms per launch)
+  // head-major grid measured 4.19 vs 4.13 ms per launch at config 2 (the tile-major order keeps a tile's
+  // heads, which share grad_output rows and sampling geometry, on neighbouring XCD slots): off by default
+  geo.head_major = env_int("M2F_MSDA_BWD_HEAD_MAJOR", 0) != 0 && d.M <= 65535;
   // the index budget must hold every level's share of one tile (halo 0); tiles span at most
   // ceil(n / nt) pixels per axis (tile_lo)
   int own = 0, qt = 0;
@@ -1005,7 +1009,7 @@ void launch_tiled_t(const float* value, const float* loc, const float* attn, con
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     attr = true;
   }
-  const dim3 grid(geo.nty * geo.ntx, d.M, d.N);
+  const dim3 grid = geo.head_major ? dim3(d.M, geo.nty * geo.ntx, d.N) : dim3(geo.nty * geo.ntx, d.M, d.N);
   msda_bwd_f32_tiled<P, LT, FUSED, TPB><<<grid, threads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga,
                                                                     scratch, wtab);
   if (scratch) {

@@ -61,6 +61,8 @@ struct TileGeom {
   int bbox;       // 1: shrink the window to the bounding box of the touched corners (phase 0 pass)
   int wrows;      // scratch rows per workgroup (>= any window) when partial rows go to a scratch buffer
   int exact;      // 1: exact integer-valued f64 row sums (bitwise repeatable); 0: fp32 sums in list order
+  int head_major; // 1: grid (M, tiles, N): the head is the fastest block index, so each XCD (blocks are dealt
+                  // round-robin) owns one head's value / grad_value rows and neighbouring tiles' halos
   int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no list inserts, 2 no phase 3, 4 no spill
                   // atomics, 8 phase 3 without its HBM adds
 };
