@@ -974,8 +974,8 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   geo.ablate = env_int("M2F_MSDA_ABLATE", 0);
   geo.bbox = env_int("M2F_MSDA_BBOX", 1);
   geo.exact = env_int("M2F_MSDA_DETERMINISTIC", 1);  // default: bitwise-repeatable gradients (+0.17 ms per launch)
-  // head-major grid measured 4.19 vs 4.13 ms per launch at config 2 (the tile-major order keeps a tile's
-  // heads, which share grad_output rows and sampling geometry, on neighbouring XCD slots): off by default
+  // head-major grid measured 4.19 vs 4.13 ms per launch at config 2 (the tile-major order puts a tile's 8
+  // heads, which share grad_output and projection rows, on the same XCD): off by default
   geo.head_major = env_int("M2F_MSDA_BWD_HEAD_MAJOR", 0) != 0 && d.M <= 65535;
   // the index budget must hold every level's share of one tile (halo 0); tiles span at most
   // ceil(n / nt) pixels per axis (tile_lo)
