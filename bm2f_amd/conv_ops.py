@@ -20,9 +20,11 @@ from torch.autograd import Function
 from . import _native
 
 
-# 3x3 weight-gradient engine: "miopen" (fp32 igemm_wrw on NHWC transposes) or "x3" (csrc/conv_x3.hip; correct
-# but measured 27 vs 14 ms at bs16 256x256 (tools/conv_bench.py): both operands are channel-strided in NCHW)
-WGRAD3 = os.environ.get("M2F_CONV3_WGRAD", "miopen")
+# 3x3 weight-gradient engine (tools/conv_bench.py, bs16 256x256x256, wgrad share of the backward):
+#   "tn"     nine x3 TN GEMMs over zero-bordered pixel-row copies of dO and I (_wgrad3_tn): ~9.4 ms
+#   "miopen" fp32 igemm_wrw on its own NHWC transposes: ~10.1 ms
+#   "x3"     the implicit-GEMM kernel of csrc/conv_x3.hip on NCHW (channel-strided operands): ~14 ms
+WGRAD3 = os.environ.get("M2F_CONV3_WGRAD", "tn")
 
 
 def _stream(t):
@@ -67,8 +69,11 @@ class Conv2dX3(Function):
             _native.call("m2f_conv_f32x3", g.data_ptr(), weight.data_ptr(), None, dx.data_ptr(), N, Ci, Co, H, W, k, 1,
                          ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(g))
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if k == 3 and WGRAD3 == "miopen" and (ctx.needs_input_grad[1] or want_b):
-            # 3x3 weight gradient on the library (default; M2F_CONV3_WGRAD=x3 selects the x3 kernel)
+        if k == 3 and WGRAD3 == "tn" and ctx.needs_input_grad[1]:
+            dw = _wgrad3_tn(g, x)
+            db = g.sum((0, 2, 3)) if want_b else None
+        elif k == 3 and WGRAD3 == "miopen" and (ctx.needs_input_grad[1] or want_b):
+            # 3x3 weight gradient on the library (M2F_CONV3_WGRAD=miopen)
             _, dw, db = torch.ops.aten.convolution_backward(
                 g, x, weight, [Co] if want_b else None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                 [False, bool(ctx.needs_input_grad[1]), want_b])
@@ -79,6 +84,40 @@ class Conv2dX3(Function):
                          k, ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(g))
             dw = tck.permute(2, 1, 0).reshape(Co, Ci, k, k) if ctx.needs_input_grad[1] else None
         return dx, dw, db
+
+
+def _pad_nhwc(t):
+    """(N, C, H, W) fp32 -> zero-bordered pixel rows (N*(H+2)*(W+2), C) inside a buffer with W+3 zero rows
+    before and after (so a row shift by any 3x3 tap stays in the buffer); returns (buffer, margin)."""
+    N, C, H, W = t.shape
+    P = (H + 2) * (W + 2)
+    margin = W + 3
+    buf = torch.zeros(2 * margin + N * P, C, device=t.device, dtype=torch.float32)
+    t = t.contiguous()
+    for n in range(N):   # per image: H row-batches of the (C x W) -> (W x C) transpose
+        dst = buf.data_ptr() + ((margin + n * P + (W + 2) + 1) * C) * 4
+        _transpose(t.data_ptr() + n * C * H * W * 4, W, H * W, dst, (W + 2) * C, C, H, C, W)
+    return buf, margin
+
+
+def _wgrad3_tn(g, x):
+    """3x3 "same" conv weight gradient as nine x3 TN GEMMs over zero-bordered pixel-row layouts:
+    dW[:, :, ky, kx] = sum_q dO_pad[q]^T I_pad[q + (ky-1)(W+2) + (kx-1)] (border rows of dO_pad are zero,
+    so out-of-image taps contribute nothing)."""
+    from . import linear_ops
+    N, Ci, H, W = x.shape
+    Co = g.shape[1]
+    gb, m = _pad_nhwc(g)
+    xb, _ = _pad_nhwc(x)
+    M = N * (H + 2) * (W + 2)
+    a = gb[m:m + M]
+    dw = torch.empty(Co, Ci, 3, 3, device=x.device, dtype=torch.float32)
+    for ky in range(3):
+        for kx in range(3):
+            off = (ky - 1) * (W + 2) + (kx - 1)
+            out, _ = linear_ops.gemm_tn(a, xb[m + off:m + off + M])
+            dw[:, :, ky, kx] = out
+    return dw
 
 
 def eligible(x, conv) -> bool:

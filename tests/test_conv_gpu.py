@@ -19,7 +19,7 @@ def _rel(a, b):
                                                 (2, 512, 256, 16, 16, 1, True), (1, 2048, 256, 8, 16, 1, True),
                                                 (3, 256, 256, 8, 16, 1, False), (1, 32, 48, 8, 16, 3, True),
                                                 (2, 16, 32, 16, 8, 3, True), (1, 48, 16, 128, 8, 3, False)])
-@pytest.mark.parametrize("wgrad3", ["x3", "miopen"])
+@pytest.mark.parametrize("wgrad3", ["x3", "miopen", "tn"])
 def test_conv_x3_vs_fp64(device, N, Ci, Co, H, W, k, bias, wgrad3, monkeypatch):
     if k == 1 and wgrad3 == "miopen":
         pytest.skip("the switch only selects the 3x3 weight-gradient engine")

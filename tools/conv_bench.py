@@ -36,7 +36,9 @@ def main():
         g = torch.randn(N, Co, H, W, device=dev)
         fl = 2.0 * N * H * W * Ci * Co * k * k
         res = {}
-        for eng, fn in (("miopen", lambda: conv(x)), ("x3", lambda: conv_ops.conv2d(x, conv))):
+        for eng, fn in (("miopen", lambda: conv(x)), ("x3", lambda: conv_ops.conv2d(x, conv)),
+                        ("x3+tn", lambda: conv_ops.conv2d(x, conv))):
+            conv_ops.WGRAD3 = "tn" if eng == "x3+tn" else "miopen"
             tf = timeit(fn)
             y = fn()
             tb = timeit(lambda: torch.autograd.grad(y, (x, conv.weight), g, retain_graph=True))
