@@ -122,6 +122,61 @@ __global__ void __launch_bounds__(256) maxpool3s2_bwd(const T* __restrict__ gy, 
   gx[t] = static_cast<T>(acc);
 }
 
+// 8 consecutive input pixels of one row per thread (W % 8 == 0): the <= 2 x 6 covering windows' gradients
+// and winner bytes are loaded once into registers, the 8 results leave as one 16-byte store
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool3s2_bwd8(const T* __restrict__ gy, const uint8_t* __restrict__ win,
+                                                      T* __restrict__ gx, int H, int W, int OH, int OW,
+                                                      int64_t total8) {
+  const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (t >= total8) return;
+  const int W8 = W / 8;
+  const int w0 = static_cast<int>(t % W8) * 8;
+  const int64_t r = t / W8;
+  const int h = static_cast<int>(r % H);
+  const int64_t plane = r / H;
+  const int phs = h + 1 < 3 ? 0 : (h - 2) / 2 + 1, phe = min((h + 1) / 2 + 1, OH);
+  const int pwb = w0 + 1 < 3 ? 0 : (w0 - 2) / 2 + 1;   // first window column any of the 8 pixels touches
+  const T* gp = gy + plane * OH * OW;
+  const uint8_t* wp = win + plane * OH * OW;
+  float g[2][6];
+  int wi[2][6];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 6; ++b) {
+      const int ph = phs + a, pw = pwb + b;
+      const bool in = ph < phe && pw < OW;
+      const int o = in ? ph * OW + pw : 0;
+      g[a][b] = in ? static_cast<float>(gp[o]) : 0.f;
+      wi[a][b] = in ? static_cast<int>(wp[o]) : -1;
+    }
+  T res[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int w = w0 + e;
+    const int pws = w + 1 < 3 ? 0 : (w - 2) / 2 + 1, pwe = min((w + 1) / 2 + 1, OW);
+    float acc = 0.f;
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 6; ++b) {
+        const int ph = phs + a, pw = pwb + b;
+        // torch's order: ph outer, pw inner, over [phs, phe) x [pws, pwe)
+        if (ph < phe && pw >= pws && pw < pwe && wi[a][b] == (h - (2 * ph - 1)) * 3 + (w - (2 * pw - 1)))
+          acc += g[a][b];
+      }
+    res[e] = static_cast<T>(acc);
+  }
+  T* dst = gx + (plane * H + h) * static_cast<int64_t>(W) + w0;
+  if constexpr (sizeof(T) == 2) {
+    *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(res);
+  } else {
+    reinterpret_cast<uint4*>(dst)[0] = reinterpret_cast<const uint4*>(res)[0];
+    reinterpret_cast<uint4*>(dst)[1] = reinterpret_cast<const uint4*>(res)[1];
+  }
+}
+
 }  // namespace
 
 extern "C" int m2f_maxpool3s2_fwd(const void* x, void* y, uint8_t* window, int64_t planes, int H, int W, int dtype,
@@ -153,6 +208,17 @@ extern "C" int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, voi
   const int64_t total = planes * H * W;
   if (total == 0) return m2f::ok();
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (W % 8 == 0 && m2f::aligned(grad_x, 16) && (dtype == M2F_BF16 || dtype == M2F_F32)) {
+    const int64_t total8 = total / 8;
+    const unsigned g8 = m2f::ceil_div(total8, 256);
+    if (dtype == M2F_BF16)
+      maxpool3s2_bwd8<__bf16><<<g8, 256, 0, st>>>(static_cast<const __bf16*>(grad_y), window,
+                                                   static_cast<__bf16*>(grad_x), H, W, OH, OW, total8);
+    else
+      maxpool3s2_bwd8<float><<<g8, 256, 0, st>>>(static_cast<const float*>(grad_y), window,
+                                                  static_cast<float*>(grad_x), H, W, OH, OW, total8);
+    return m2f::check_launch(fn);
+  }
   const unsigned grid = m2f::ceil_div(total, 256);
   if (dtype == M2F_BF16)
     maxpool3s2_bwd<__bf16><<<grid, 256, 0, st>>>(static_cast<const __bf16*>(grad_y), window,

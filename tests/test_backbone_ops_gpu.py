@@ -30,7 +30,7 @@ def test_bias_act_matches_unfused(device, dtype, residual):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("H,W", [(16, 24), (7, 9), (1, 1), (2, 3)])
+@pytest.mark.parametrize("H,W", [(16, 24), (7, 9), (1, 1), (2, 3), (5, 16), (1, 8)])
 def test_stem_maxpool_matches_torch(device, dtype, H, W):
     """The stem max pool (csrc/eltwise.hip, 1-byte winners) against F.max_pool2d(3, 2, 1): forward and
     gradient bit-exact, with ties (integer-valued inputs), -inf and NaN."""
