@@ -248,8 +248,13 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         src, pos, key, size_list = [], [], [], []
         for i in range(self.num_feature_levels):
             size_list.append(tuple(x[i].shape[-2:]))
-            p = self.pe_layer(x[i], None).flatten(2).transpose(1, 2)
-            s = (self.input_proj[i](x[i]).flatten(2) + self.level_embed.weight[i][None, :, None]).transpose(1, 2)
+            pe = self.pe_layer(x[i], None)
+            if pe.stride(0) == 0:
+                # batch-shared embedding: one contiguous (1, HW, C) copy, so the adds below vectorise
+                p = pe[:1].flatten(2).transpose(1, 2).contiguous().expand(pe.shape[0], -1, -1)
+            else:
+                p = pe.flatten(2).transpose(1, 2)
+            s = self.input_proj[i](x[i]).flatten(2).transpose(1, 2) + self.level_embed.weight[i][None, None, :]
             src.append(s)
             pos.append(p)
             key.append(s + p)
