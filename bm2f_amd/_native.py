@@ -54,6 +54,9 @@ _SIGNATURES = {
     "m2f_maxpool3s2_fwd": [_p, _p, _p, _l, _i, _i, _i, _p],
     "m2f_maxpool3s2_bwd": [_p, _p, _p, _l, _i, _i, _i, _p],
     "m2f_transpose_f32": [_p, _l, _l, _p, _l, _l, _i, _i, _i, _p],
+    "m2f_group_norm_workspace": [_i, _i, _i, _l, _p],
+    "m2f_group_norm_fwd_f32": [_p, _p, _p, _i, _i, _i, _l, _f, _i, _p, _p, _p, _p, _l, _p],
+    "m2f_group_norm_bwd_f32": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _l, _i, _p, _p, _p, _p, _l, _p],
     "m2f_add_layernorm_workspace": [_l, _i, _p],
     "m2f_add_layernorm_fwd_f32": [_p, _p, _p, _p, _l, _i, _f, _p, _p, _p, _p],
     "m2f_add_layernorm_bwd_f32": [_p, _p, _p, _p, _p, _p, _l, _i, _p, _p, _p, _p, _l, _p],

@@ -143,9 +143,12 @@ def conv2d(x, conv):
 
 def conv_norm_act(x, conv):
     """A detectron2-style Conv2d (conv -> norm -> activation) with the conv on the x3 kernels."""
+    from .norm_ops import group_norm_act
     y = conv2d(x, conv)
     norm = getattr(conv, "norm", None)
     act = getattr(conv, "activation", None)
+    if isinstance(norm, torch.nn.GroupNorm) and act in (None, F.relu, torch.relu):
+        return group_norm_act(y, norm, relu=act is not None)   # GN (+ ReLU) fused (csrc/gnorm.hip)
     if norm is not None:
         y = norm(y)
     if act is not None:

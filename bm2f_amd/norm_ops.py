@@ -75,3 +75,62 @@ def add_layernorm(a: torch.Tensor, b: torch.Tensor | None, norm: nn.LayerNorm) -
     if _eligible(a, b, norm):
         return AddLayerNorm.apply(a, b, norm.weight, norm.bias, float(norm.eps))
     return norm(a if b is None else a + b)
+
+
+def _gn_ws(N, C, G, HW, device):
+    b = ctypes.c_int64(0)
+    _native.call("m2f_group_norm_workspace", N, C, G, ctypes.c_int64(HW), ctypes.byref(b))
+    return torch.empty(max(b.value, 16), device=device, dtype=torch.uint8)
+
+
+class GroupNormAct(Function):
+    """``relu?(F.group_norm(x, G, weight, bias, eps))`` for fp32 NCHW (csrc/gnorm.hip): statistics, the
+    affine normalisation and the ReLU in two passes, the backward (ReLU mask recomputed from x) in two."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps, relu):
+        x = x.contiguous()
+        N, C = x.shape[:2]
+        HW = x.numel() // (N * C)
+        y = torch.empty_like(x)
+        mean = torch.empty(N * groups, device=x.device, dtype=torch.float32)
+        rstd = torch.empty_like(mean)
+        ws = _gn_ws(N, C, groups, HW, x.device)
+        _native.call("m2f_group_norm_fwd_f32", x.data_ptr(), weight.data_ptr() if weight is not None else None,
+                     bias.data_ptr() if bias is not None else None, N, C, groups, ctypes.c_int64(HW),
+                     ctypes.c_float(eps), 1 if relu else 0, y.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                     ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(x))
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.meta = (groups, relu)
+        return y
+
+    @staticmethod
+    def backward(ctx, grad):
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        groups, relu = ctx.meta
+        g = grad.contiguous()
+        N, C = x.shape[:2]
+        HW = x.numel() // (N * C)
+        dx = torch.empty_like(x)
+        nig = ctx.needs_input_grad
+        dw = torch.empty(C, device=x.device, dtype=torch.float32) if weight is not None and nig[1] else None
+        db = torch.empty(C, device=x.device, dtype=torch.float32) if bias is not None and nig[2] else None
+        ws = _gn_ws(N, C, groups, HW, x.device)
+        _native.call("m2f_group_norm_bwd_f32", g.data_ptr(), x.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                     weight.data_ptr() if weight is not None else None, bias.data_ptr() if bias is not None else None,
+                     N, C, groups, ctypes.c_int64(HW), 1 if relu else 0, dx.data_ptr(),
+                     dw.data_ptr() if dw is not None else None, db.data_ptr() if db is not None else None,
+                     ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(x))
+        return dx, dw, db, None, None, None
+
+
+def group_norm_act(x: torch.Tensor, norm: nn.GroupNorm, relu: bool = False) -> torch.Tensor:
+    """``norm(x)`` (then ReLU) for an ``nn.GroupNorm``; fp32 CUDA NCHW on the gfx950 kernels."""
+    if (x.is_cuda and x.dtype == torch.float32 and x.dim() >= 3 and isinstance(norm, nn.GroupNorm)
+            and (not norm.affine or (norm.weight.dtype == torch.float32 and norm.bias.dtype == torch.float32))
+            and (x.numel() // (x.shape[0] * x.shape[1])) % 4 == 0 and x.numel() > 0):
+        w = norm.weight if norm.affine else None
+        b = norm.bias if norm.affine else None
+        return GroupNormAct.apply(x, w, b, norm.num_groups, float(norm.eps), relu)
+    y = norm(x)
+    return torch.relu(y) if relu else y

@@ -24,7 +24,7 @@ from torch.nn.init import normal_
 
 from .msda import MSDeformAttn, attach_host_shapes
 from . import conv_ops, linear_ops
-from .norm_ops import add_layernorm
+from .norm_ops import add_layernorm, group_norm_act
 from .position_encoding import PositionEmbeddingSine
 from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill, configurable, get_norm
 
@@ -289,7 +289,7 @@ class MSDeformAttnPixelDecoder(nn.Module):
         for idx, f in enumerate(self.transformer_in_features[::-1]):
             x = features[f].float()
             proj = self.input_proj[idx]
-            srcs.append(proj[1](conv_ops.conv2d(x, proj[0])))   # 1x1 conv (x3 kernels) + GroupNorm
+            srcs.append(group_norm_act(conv_ops.conv2d(x, proj[0]), proj[1]))   # 1x1 conv (x3) + GroupNorm
             pos.append(self.pe_layer(x))
 
         y, spatial_shapes, level_start_index = self.transformer(srcs, pos)

@@ -257,6 +257,20 @@ int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, 
 int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, float* out, int64_t out_bs, int64_t out_ld,
                       int B, int R, int Q, void* stream);
 
+/* GroupNorm (+ ReLU when relu != 0) over fp32 NCHW x (N, C, H*W = HW), G groups, affine gamma/beta (may
+ * be null): the pixel decoder's GN layers (msdeformattn.py:216-219, :269-281; nn.GroupNorm(32, C)
+ * semantics, biased variance, eps).  fwd writes y and the per-(n, g) mean / rstd (N*G floats each) the
+ * backward takes; bwd recomputes the ReLU mask from x and writes dx, and dgamma / dbeta if non-null.
+ * Statistics and reductions in fp64 with fixed-order combines (deterministic).  HW % 4 == 0; x, y, dy,
+ * dx and the workspace (m2f_group_norm_workspace bytes) 16-byte aligned. */
+int m2f_group_norm_workspace(int N, int C, int G, int64_t HW, int64_t* workspace_bytes);
+int m2f_group_norm_fwd_f32(const float* x, const float* gamma, const float* beta, int N, int C, int G, int64_t HW,
+                           float eps, int relu, float* y, float* mean, float* rstd, void* workspace,
+                           int64_t workspace_bytes, void* stream);
+int m2f_group_norm_bwd_f32(const float* dy, const float* x, const float* mean, const float* rstd, const float* gamma,
+                           const float* beta, int N, int C, int G, int64_t HW, int relu, float* dx, float* dgamma,
+                           float* dbeta, void* workspace, int64_t workspace_bytes, void* stream);
+
 /* FPN merge of the pixel decoder, msdeformattn.py:343-349 (the lateral plus the bilinear upsample of the
  * coarser map, F.interpolate(..., mode="bilinear", align_corners=False)) for the exact 2x case, fp32:
  * m2f_upsample2x_add_fwd_f32:  out[N][C][2h][2w] = lateral + up2x(src); src (N, C, h, w) read through
