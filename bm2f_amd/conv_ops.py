@@ -92,7 +92,14 @@ def _pad_nhwc(t):
     N, C, H, W = t.shape
     P = (H + 2) * (W + 2)
     margin = W + 3
-    buf = torch.zeros(2 * margin + N * P, C, device=t.device, dtype=torch.float32)
+    buf = torch.empty(2 * margin + N * P, C, device=t.device, dtype=torch.float32)
+    buf[:margin].zero_()
+    buf[margin + N * P:].zero_()
+    img = buf[margin:margin + N * P].view(N, H + 2, W + 2, C)   # zero only the borders: the transposes
+    img[:, 0].zero_()                                            # below write every interior row
+    img[:, H + 1].zero_()
+    img[:, 1:H + 1, 0].zero_()
+    img[:, 1:H + 1, W + 1].zero_()
     t = t.contiguous()
     for n in range(N):   # per image: H row-batches of the (C x W) -> (W x C) transpose
         dst = buf.data_ptr() + ((margin + n * P + (W + 2) + 1) * C) * 4
