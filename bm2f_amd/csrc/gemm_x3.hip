@@ -34,6 +34,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -526,7 +527,11 @@ TnPlan tn_plan(int M, int N1, int N2) {
   p.nw = 4;  // 3 (96-row tiles, exact for 288) measured slower: fewer threads share the B staging
   if (const char* e = std::getenv("M2F_GEMM_X3_TN_NW")) p.nw = std::atoi(e) == 3 ? 3 : 4;
   p.tiles = ((p.n1 + 32 * p.nw - 1) / (32 * p.nw)) * ((p.n2 + 255) / 256);
-  int splits = (512 + p.tiles - 1) / p.tiles;                // ~512 blocks: 2 per CU
+  // ~512 blocks (2 per CU); 768 when the last row tile is partial (the 288-wide sampling projection:
+  // 0.52 vs 0.65 ms at M = 344064; full tiles measured best at 512, tools/gemm_x3_bench.py)
+  int target = p.n1 % (32 * p.nw) ? 768 : 512;
+  if (const char* e = std::getenv("M2F_GEMM_X3_TN_BLOCKS")) target = std::max(1, std::atoi(e));
+  int splits = (target + p.tiles - 1) / p.tiles;
   const int max_splits = (M + 8 * kBK - 1) / (8 * kBK);       // >= 8 chunks per block
   if (splits > max_splits) splits = max_splits;
   p.splits = splits < 1 ? 1 : splits;
