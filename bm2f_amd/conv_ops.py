@@ -103,7 +103,7 @@ def _pad_nhwc(t):
     t = t.contiguous()
     for n in range(N):   # per image: H row-batches of the (C x W) -> (W x C) transpose
         dst = buf.data_ptr() + ((margin + n * P + (W + 2) + 1) * C) * 4
-        _transpose(t.data_ptr() + n * C * H * W * 4, W, H * W, dst, (W + 2) * C, C, H, C, W)
+        _transpose(t.data_ptr() + n * C * H * W * 4, W, H * W, dst, (W + 2) * C, C, H, C, W, t.device)
     return buf, margin
 
 
@@ -201,9 +201,9 @@ def upsample_add(src, lateral):
     return lateral + F.interpolate(src, size=lateral.shape[-2:], mode="bilinear", align_corners=False)
 
 
-def _transpose(src, in_bs, in_ld, dst, out_bs, out_ld, B, R, Q):
+def _transpose(src, in_bs, in_ld, dst, out_bs, out_ld, B, R, Q, device):
     _native.call("m2f_transpose_f32", src, ctypes.c_int64(in_bs), ctypes.c_int64(in_ld), dst, ctypes.c_int64(out_bs),
-                 ctypes.c_int64(out_ld), B, R, Q, torch.cuda.current_stream().cuda_stream)
+                 ctypes.c_int64(out_ld), B, R, Q, torch.cuda.current_stream(device).cuda_stream)
 
 
 class FlattenLevels(Function):
@@ -219,7 +219,7 @@ class FlattenLevels(Function):
         start = 0
         for x, hw in zip(xs, sizes):
             x = x.contiguous()
-            _transpose(x.data_ptr(), C * hw, hw, out.data_ptr() + start * C * 4, S * C, C, N, C, hw)
+            _transpose(x.data_ptr(), C * hw, hw, out.data_ptr() + start * C * 4, S * C, C, N, C, hw, x.device)
             start += hw
         ctx.shapes = [x.shape for x in xs]
         return out
@@ -232,7 +232,7 @@ class FlattenLevels(Function):
         for shp in ctx.shapes:
             hw = shp[2] * shp[3]
             gx = torch.empty(shp, device=g.device, dtype=torch.float32)
-            _transpose(g.data_ptr() + start * C * 4, S * C, C, gx.data_ptr(), C * hw, hw, N, hw, C)
+            _transpose(g.data_ptr() + start * C * 4, S * C, C, gx.data_ptr(), C * hw, hw, N, hw, C, g.device)
             grads.append(gx)
             start += hw
         return tuple(grads)

@@ -101,6 +101,53 @@ __global__ void __launch_bounds__(256) up2x_bwd(const float* __restrict__ g, flo
   gsrc[t] = acc;
 }
 
+// two horizontally adjacent source pixels per thread (w even): each output row segment 4k-1 .. 4k+4 is one
+// aligned float4 plus two edge values, shared by both pixels; same sums in the same order as up2x_bwd
+__global__ void __launch_bounds__(256) up2x_bwd2(const float* __restrict__ g, float* __restrict__ gsrc, int h, int w,
+                                                 int64_t n_pairs) {
+  const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (t >= n_pairs) return;
+  const int wp = w / 2;
+  const int k = static_cast<int>(t % wp), x0 = 2 * k;
+  const int64_t r = t / wp;
+  const int y = static_cast<int>(r % h);
+  const int64_t plane = r / h;
+  const int H2 = 2 * h, W2 = 2 * w;
+  const float* gp = g + plane * H2 * W2;
+  float wa[6], wb[6];   // column weights of cols 4k-1 .. 4k+4 for source pixels x0, x0+1
+#pragma unroll
+  for (int c = 0; c < 6; ++c) {
+    const int ox = 4 * k - 1 + c;
+    const bool ok = ox >= 0 && ox < W2;
+    wa[c] = ok && c < 4 ? wgt2x(ox, x0, w) : 0.f;
+    wb[c] = ok && c >= 2 ? wgt2x(ox, x0 + 1, w) : 0.f;
+  }
+  float acc_a = 0.f, acc_b = 0.f;
+#pragma unroll
+  for (int dy = -1; dy <= 2; ++dy) {
+    const int oy = 2 * y + dy;
+    if (oy < 0 || oy >= H2) continue;
+    const float wy = wgt2x(oy, y, h);
+    if (wy == 0.f) continue;
+    const float* row = gp + static_cast<int64_t>(oy) * W2;
+    const f4 mid = *reinterpret_cast<const f4*>(row + 4 * k);
+    const float v[6] = {4 * k - 1 >= 0 ? row[4 * k - 1] : 0.f, mid[0], mid[1], mid[2], mid[3],
+                        4 * k + 4 < W2 ? row[4 * k + 4] : 0.f};
+    float ra = 0.f, rb = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {   // up2x_bwd's dx order: cols 2x-1 .. 2x+2, skipping those outside
+      const int oxa = 4 * k - 1 + c, oxb = 4 * k + 1 + c;
+      if (oxa >= 0 && oxa < W2) ra += wa[c] * v[c];
+      if (oxb >= 0 && oxb < W2) rb += wb[c + 2] * v[c + 2];
+    }
+    acc_a += wy * ra;
+    acc_b += wy * rb;
+  }
+  float* dst = gsrc + (plane * h + y) * static_cast<int64_t>(w) + x0;
+  dst[0] = acc_a;
+  dst[1] = acc_b;
+}
+
 }  // namespace
 
 extern "C" int m2f_upsample2x_add_fwd_f32(const float* src, int64_t sN, int64_t sC, int64_t sY, int64_t sX,
@@ -125,6 +172,11 @@ extern "C" int m2f_upsample2x_bwd_f32(const float* grad_out, float* grad_src, in
   if (N < 0 || C <= 0 || h <= 0 || w <= 0) return m2f::fail(M2F_EINVAL, "%s: bad sizes", fn);
   const int64_t n_in = static_cast<int64_t>(N) * C * h * w;
   if (n_in == 0) return m2f::ok();
+  if (w % 2 == 0 && m2f::aligned(grad_out, 16)) {
+    up2x_bwd2<<<m2f::ceil_div(n_in / 2, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(grad_out, grad_src, h, w,
+                                                                                          n_in / 2);
+    return m2f::check_launch(fn);
+  }
   up2x_bwd<<<m2f::ceil_div(n_in, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(grad_out, grad_src, h, w, n_in);
   return m2f::check_launch(fn);
 }
