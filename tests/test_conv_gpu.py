@@ -94,3 +94,25 @@ def test_flatten_levels_matches_cat(device):
     b.backward(g)
     for x, y in zip(xs, ys):
         assert torch.equal(x.grad, y.grad)
+
+
+def test_upsample2x_strided_and_row_kernels_agree(device):
+    """m2f_upsample2x_add_fwd_f32 on a transposed view (generic strided kernel) and on its contiguous copy
+    (row-window kernel): the same taps and products (the compiler may contract them into FMAs differently,
+    so equal to fp32 rounding)."""
+    import ctypes
+    from bm2f_amd import _native
+    torch.manual_seed(1)
+    N, C, h, w = 2, 24, 6, 10
+    z = torch.randn(N, h * w, C, device=device)
+    view = z.transpose(1, 2).view(N, C, h, w)
+    cont = view.contiguous()
+    lat = torch.randn(N, C, 2 * h, 2 * w, device=device)
+    outs = []
+    for src in (view, cont):
+        out = torch.empty_like(lat)
+        _native.call("m2f_upsample2x_add_fwd_f32", src.data_ptr(), *(ctypes.c_int64(s) for s in src.stride()),
+                     lat.data_ptr(), out.data_ptr(), N, C, h, w, torch.cuda.current_stream().cuda_stream)
+        outs.append(out)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-6, atol=1e-6)
