@@ -1,25 +1,33 @@
 #!/usr/bin/env python
 """Benchmark: images/sec of the Mask2Former R50 training step (fwd + bwd + AdamW) on synthetic
-1024x1024 batches, 16 images per GPU (BASELINE.json config 2; configs 3 at --gpus 8 under torchrun).
+1024x1024 batches, 16 images per GPU (BASELINE.json config 2; config 3 at --gpus 8).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 16] [--res 1024] [--amp bf16|fp16|none]
 
-For N > 1 the driver launches one process per GPU with torch.distributed.run; gradients are all-reduced
-by DDP over RCCL (backend "nccl"), the only exchange on this path.  Rank 0 prints ONE
-JSON line.  Besides the contract fields it reports:
-  roofline      the MSDA backward kernel (the hot path's dominant hand-written kernel): algorithmic
-                bytes per launch (115.60 MB per 1024^2 image) / its mean duration,
-                measured with HIP events on the launch stream over the timed region, vs the 8 TB/s
-                HBM peak; traffic = PMC-measured HBM bytes per launch from profiles/, when committed.
-  cpu_baseline  the reference's CPU path (oracle/cpu_path.py: the same model with the reference's
-                ms_deform_attn_core_pytorch and MultiheadAttention math) on a bounded sample, rank 0, N=1.
-  kernels       mean per-launch time of each bm2f kernel family over the timed region.
+One process per GPU.  ``--gpus N`` with N > 1 outside torch.distributed.run starts
+``python -m torch.distributed.run --nproc-per-node N`` itself (before touching the GPU) and exits with its
+status; under torchrun (WORLD_SIZE set) N must equal WORLD_SIZE.  Gradients are all-reduced by DDP over
+RCCL (backend "nccl"), the only exchange on this path.  Rank 0 prints ONE JSON line.
+Besides the contract fields it reports:
+  roofline      the MSDA backward kernel (the hot path's dominant hand-written kernel): algorithmic bytes
+                per launch (115.60 MB per 1024^2 image) / its mean duration, measured with HIP
+                events on the launch stream, vs the 8 TB/s HBM peak; traffic = PMC-measured HBM bytes per
+                launch (profiles/msda_bwd_traffic.json).
+  roofline_all  the same for every hand-written kernel family (HBM- or MFMA-bound as DESIGN.md §3 says),
+                from extra instrumented steps after the timed region (the timed steps carry no events).
+  modes         N=1 only: the same step under AMP fp16 (the reference's training dtype, with a GradScaler
+                as detectron2's AMPTrainer) and with no autocast at all (fp32 parity mode), fewer steps.
+  cpu_baseline  the reference's CPU path (oracle/cpu_path.py) on config 1 (1 x 512^2) and one 1024^2 image,
+                warm-up 1, median of 3, rank 0, N=1; value = the 1024^2 img/s.
+  env           every M2F_* variable in the environment.  The bench refuses to run with any set (they select
+                non-default engines or geometries); --allow-knobs permits them for experiments.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -28,30 +36,119 @@ os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from bm2f_amd.miopen_tuning import use_shipped_find_db  # noqa: E402
-
-use_shipped_find_db()  # FAST find mode + the shipped NORMAL-mode find-db (no search on a fresh box)
-
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 METRIC = "images/sec fwd+bwd, R50 100-query 1024² bs16, at 1/2/4/8 MI355X"
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_PEAK_TF = 2500.0      # dense bf16/f16 MFMA
+F32_PEAK_TF = 157.3        # f32 MFMA (= f32 vector)
 
 
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--queries", type=int, default=100)
+    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16", "none"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-modes", action="store_true", help="skip the fp16 / fp32 mode lines")
+    ap.add_argument("--mode-steps", type=int, default=4)
+    ap.add_argument("--kernel-steps", type=int, default=2, help="instrumented steps for roofline_all")
+    ap.add_argument("--allow-knobs", action="store_true")
+    ap.add_argument("--master-port", type=int, default=29531)
+    return ap.parse_args(argv)
+
+
+def knob_env():
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith("M2F_")}
+
+
+def maybe_launch(args):
+    """--gpus N > 1 without torchrun: run torch.distributed.run as a child (no GPU touched here)."""
+    world = os.environ.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+        return
+    if args.gpus <= 1:
+        return
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={args.master_port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log("launching " + " ".join(cmd[2:]))
+    raise SystemExit(subprocess.call(cmd))
+
+
+# ----------------------------------------------------------------------------------------------------
+# per-kernel timing: HIP events around libbm2f entry points, on torch's current stream (the stream the
+# C ABI launches on), with each call's algorithmic work computed from its arguments
+# ----------------------------------------------------------------------------------------------------
+def _attn_bytes(a, fwd):
+    # m2f_masked_attn_{fwd,bwd}(dtype, q, k, v, bits, [out, gout, lse,] B, Lq, Lk, H, hd, ...)
+    o = 5 if fwd else 8
+    dt, B, Lq, Lk, H, hd = a[0], a[o], a[o + 1], a[o + 2], a[o + 3], a[o + 4]
+    el = 4 if dt == 0 else 2
+    kv = 2 * B * Lk * H * hd * el
+    q = B * Lq * H * hd * el
+    bits = B * Lq * ((Lk + 31) // 32) * 4
+    flops = 4 * B * H * Lq * Lk * hd
+    if fwd:
+        return kv + 2 * q + bits + B * H * Lq * 4, flops
+    return 2 * kv + 4 * q + bits + B * H * Lq * 4, flops * 5 // 2
+
+
+def _msda_bytes(a, fused, bwd):
+    if fused:  # (value, proj, ld, ref, rbs, hs, [gout,] N, S, M, D, L, Lq, P, ...)
+        o = 7 if bwd else 6
+        N, S, M, D, L, Lq, P = a[o:o + 7]
+    else:      # (value, shapes, lsi, loc, attn, [gout,] N, S, M, D, L, Lq, P, ...)
+        o = 6 if bwd else 5
+        N, S, M, D, L, Lq, P = a[o:o + 7]
+    value = N * S * M * D * 4
+    loc = N * Lq * M * L * P * 2 * 4
+    attn = N * Lq * M * L * P * 4
+    out = N * Lq * M * D * 4
+    fwd_b = value + loc + attn + out
+    return (fwd_b + value + loc + attn if bwd else fwd_b), 0
+
+
+def _x3(M, N, K):
+    return 0, 2 * M * N * K
+
+
+ENTRIES = {
+    # name: (family, bound, work(args) -> (bytes, flops))
+    "m2f_msda_fused_bwd_f32": ("msda_bwd", "hbm", lambda a: _msda_bytes(a, True, True)),
+    "m2f_msda_bwd_f32": ("msda_bwd", "hbm", lambda a: _msda_bytes(a, False, True)),
+    "m2f_msda_fused_fwd_f32": ("msda_fwd", "hbm", lambda a: _msda_bytes(a, True, False)),
+    "m2f_msda_fwd_f32": ("msda_fwd", "hbm", lambda a: _msda_bytes(a, False, False)),
+    "m2f_attn_mask_bits": ("attn_mask_bits", "hbm", lambda a: (
+        a[2] * a[3] * a[4] * a[5] * a[6] * (4 if a[1] == 0 else 2) + a[2] * a[3] * a[11] * 4, 0)),
+    "m2f_masked_attn_fwd": ("masked_attn_fwd", "hbm", lambda a: _attn_bytes(a, True)),
+    "m2f_masked_attn_bwd": ("masked_attn_bwd", "hbm", lambda a: _attn_bytes(a, False)),
+    "m2f_mask_heads_fwd": ("mask_einsum_fwd", "mfma", lambda a: (0, 2 * a[4] * a[5] * a[6] * a[7] * a[8])),
+    "m2f_gemm_f32x3_nt": ("x3_gemm_nt", "mfma", lambda a: _x3(a[11], a[12], a[13])),
+    "m2f_gemm_f32x3_nt_add": ("x3_gemm_nt", "mfma", lambda a: _x3(a[14], a[15], a[16])),
+    "m2f_gemm_f32x3_tn": ("x3_gemm_tn", "mfma", lambda a: _x3(a[7], a[8], a[9])),
+    "m2f_conv_f32x3": ("x3_conv", "mfma", lambda a: _x3(a[4] * a[7] * a[8], a[6] if a[10] == 0 else a[5],
+                                                      (a[5] if a[10] == 0 else a[6]) * a[9] * a[9])),
+    "m2f_conv_f32x3_wgrad": ("x3_conv_wgrad", "mfma", lambda a: _x3(a[5] * a[9] * a[9], a[6], a[4] * a[7] * a[8])),
+}
+
+MFMA_NOTE = {
+    "x3_gemm_nt": "fp32 GEMM as 6 bf16 MFMA products (split operands): mfma work = 6 x 2MNK vs the 2.5 PF bf16 peak",
+    "x3_gemm_tn": "as x3_gemm_nt (weight gradients, split over rows, fixed-order slab sums)",
+    "x3_conv": "as x3_gemm_nt (implicit-GEMM conv, 1x1 and 3x3)",
+    "x3_conv_wgrad": "as x3_gemm_nt (1x1 conv weight gradients)",
+    "mask_einsum_fwd": "bqc,bchw->bqhw on bf16/f16 MFMA with the fused bitmask epilogue",
+}
+
+
 class KernelTimer:
-    """HIP events around every libbm2f entry point, recorded on torch's current stream -- the stream the
-    C ABI launches on -- so each pair brackets exactly that call's kernels (and its memset)."""
-
-    KEYS = {"m2f_msda_fused_bwd_f32": "msda_bwd", "m2f_msda_bwd_f32": "msda_bwd",
-            "m2f_msda_fused_fwd_f32": "msda_fwd", "m2f_msda_fwd_f32": "msda_fwd",
-            "m2f_attn_mask_bits": "attn_mask_bits", "m2f_masked_attn_fwd": "masked_attn_fwd",
-            "m2f_masked_attn_bwd": "masked_attn_bwd"}
-
     def __init__(self):
         self.enabled = False
         self.events = {}
@@ -61,26 +158,52 @@ class KernelTimer:
         timer = self
 
         def wrapped(name, *args):
-            key = timer.KEYS.get(name)
-            if not timer.enabled or key is None:
+            ent = ENTRIES.get(name)
+            if not timer.enabled or ent is None:
                 return fn(name, *args)
+            import torch
             s = torch.cuda.Event(enable_timing=True)
             e = torch.cuda.Event(enable_timing=True)
             s.record()
             out = fn(name, *args)
             e.record()
-            timer.events.setdefault(key, []).append((s, e))
+            nbytes, flops = ent[2](args)
+            timer.events.setdefault(ent[0], []).append((s, e, nbytes, flops))
             return out
 
         native.call = wrapped
 
-    def summary(self):
+    def summary(self, steps):
+        import torch
         torch.cuda.synchronize()
         res = {}
-        for key, evs in self.events.items():
-            ms = [s.elapsed_time(e) for s, e in evs]
-            res[key] = {"calls": len(ms), "mean_ms": sum(ms) / len(ms), "total_ms": sum(ms)}
+        for fam, evs in self.events.items():
+            ms = [s.elapsed_time(e) for s, e, _, _ in evs]
+            nb = sum(b for _, _, b, _ in evs)
+            fl = sum(f for _, _, _, f in evs)
+            tot = sum(ms)
+            res[fam] = {"calls_per_step": len(ms) / steps, "mean_ms": tot / len(ms), "ms_per_step": tot / steps,
+                        "bytes": nb, "flops": fl, "total_ms": tot}
         return res
+
+
+def roofline_entry(fam, k, bound):
+    t = k["total_ms"] * 1e-3
+    if bound == "hbm":
+        ach = k["bytes"] / t / 1e9
+        return {"kernel": fam, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "mean_launch_ms": round(k["mean_ms"], 4),
+                "ms_per_step": round(k["ms_per_step"], 3)}
+    if fam.startswith("x3"):
+        ach = 6 * k["flops"] / t / 1e12
+        return {"kernel": fam, "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_PEAK_TF, "unit": "TFLOP/s",
+                "frac": round(ach / BF16_PEAK_TF, 4), "fp32_equiv_tflops": round(k["flops"] / t / 1e12, 1),
+                "mean_launch_ms": round(k["mean_ms"], 4), "ms_per_step": round(k["ms_per_step"], 3),
+                "note": MFMA_NOTE.get(fam)}
+    ach = k["flops"] / t / 1e12
+    return {"kernel": fam, "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_PEAK_TF, "unit": "TFLOP/s",
+            "frac": round(ach / BF16_PEAK_TF, 4), "mean_launch_ms": round(k["mean_ms"], 4),
+            "ms_per_step": round(k["ms_per_step"], 3), "note": MFMA_NOTE.get(fam)}
 
 
 def msda_bwd_bytes(n_images, res, M=8, D=32, L=3, P=4):
@@ -102,17 +225,18 @@ def load_traffic():
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
-    ap.add_argument("--res", type=int, default=1024)
-    ap.add_argument("--queries", type=int, default=100)
-    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16", "none"])
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-steps", type=int, default=2)
-    args = ap.parse_args()
+    args = parse_args()
+    maybe_launch(args)
+    knobs = knob_env()
+    if knobs and not args.allow_knobs:
+        raise SystemExit(f"bench.py: M2F_* variables set ({', '.join(knobs)}); they select non-default engines or "
+                         "geometries. Unset them, or pass --allow-knobs for an experiment (they are recorded).")
+
+    from bm2f_amd.miopen_tuning import use_shipped_find_db
+    use_shipped_find_db()  # FAST find mode + the shipped NORMAL-mode find-db (no search on a fresh box)
+
+    import torch
+    import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -123,7 +247,7 @@ def main():
     device = torch.device("cuda", local)
 
     from bm2f_amd import _native
-    from bm2f_amd.bench_model import MaskFormerR50, default_cfg, make_optimizer, train_step, wrap_ddp
+    from bm2f_amd.bench_model import MaskFormerR50, default_cfg, make_optimizer, make_scaler, train_step, wrap_ddp
 
     timer = KernelTimer()
     timer.install(_native)
@@ -135,44 +259,67 @@ def main():
     opt = make_optimizer(model)
     g = torch.Generator(device=device).manual_seed(1000 + rank)
     images = torch.randn(args.batch, 3, args.res, args.res, device=device, generator=g) * 57.0 + 117.0
-    amp = {"bf16": torch.bfloat16, "fp16": torch.float16, "none": None}[args.amp]
+    dtypes = {"bf16": torch.bfloat16, "fp16": torch.float16, "none": None}
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    t0 = time.perf_counter()
-    for i in range(args.warmup):
-        train_step(model, opt, images, amp)
+    def run(amp_name, steps, warmup, tag):
+        amp = dtypes[amp_name]
+        scaler = make_scaler(amp)
+        t0 = time.perf_counter()
+        for i in range(warmup):
+            train_step(model, opt, images, amp, scaler=scaler)
+            torch.cuda.synchronize()
+            log(f"{tag} warmup {i + 1}/{warmup} done ({time.perf_counter() - t0:.1f}s)")
+        barrier()
         torch.cuda.synchronize()
-        log(f"warmup {i + 1}/{args.warmup} done ({time.perf_counter() - t0:.1f}s)")
+        start = last = time.perf_counter()
+        for i in range(steps):
+            train_step(model, opt, images, amp, scaler=scaler)
+            if time.perf_counter() - last > 30:
+                log(f"{tag} step {i + 1}/{steps}")
+                last = time.perf_counter()
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - start
+        if world > 1:
+            t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = t.item()
+        log(f"{tag}: {steps} steps in {elapsed:.3f}s")
+        return elapsed
 
-    barrier()
-    torch.cuda.synchronize()
-    timer.enabled = True
-    start = time.perf_counter()
-    last = start
-    for i in range(args.steps):
-        train_step(model, opt, images, amp)
-        if time.perf_counter() - last > 30:
-            log(f"step {i + 1}/{args.steps}")
-            last = time.perf_counter()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - start
-    timer.enabled = False
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-    kern = timer.summary()
-    log(f"timed {args.steps} steps in {elapsed:.3f}s")
+    elapsed = run(args.amp, args.steps, args.warmup, "timed")
+
+    # instrumented steps (after the timed region): per-kernel-family durations and algorithmic work
+    kern = {}
+    if args.kernel_steps > 0:
+        timer.enabled = True
+        for _ in range(args.kernel_steps):
+            train_step(model, opt, images, dtypes[args.amp], scaler=make_scaler(dtypes[args.amp]))
+        kern = timer.summary(args.kernel_steps)
+        timer.enabled = False
+
+    modes = None
+    if world == 1 and not args.no_modes:
+        modes = {}
+        for name in ("fp16", "none"):
+            if name == args.amp:
+                continue
+            torch.cuda.empty_cache()
+            el = run(name, args.mode_steps, 2, f"mode {name}")
+            key = "amp_fp16" if name == "fp16" else "fp32_parity"
+            modes[key] = {"value": round(world * args.batch * args.mode_steps / el, 3), "unit": "images/s",
+                          "ms_per_step": round(el / args.mode_steps * 1e3, 3), "steps": args.mode_steps, "warmup": 2,
+                          "autocast": None if name == "none" else name,
+                          "grad_scaler": name == "fp16"}
 
     if rank == 0:
-        images_total = world * args.batch * args.steps
-        value = images_total / elapsed
-        bwd = kern.get("msda_bwd")
+        value = world * args.batch * args.steps / elapsed
         roof = None
+        bwd = kern.get("msda_bwd")
         if bwd:
             nbytes = msda_bwd_bytes(args.batch, args.res)
             achieved = nbytes / (bwd["mean_ms"] * 1e-3) / 1e9
@@ -180,32 +327,36 @@ def main():
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": (tr or {}).get("hbm_bytes_per_launch") if tr else None,
-                    "kernel": "MSDA backward (m2f_msda_fused_bwd_f32: tiled, LDS fixed-point grad_value)",
-                    "algorithmic_bytes_per_launch": nbytes,
-                    "mean_launch_ms": round(bwd["mean_ms"], 4)}
+                    "kernel": "MSDA backward (m2f_msda_fused_bwd_f32)",
+                    "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(bwd["mean_ms"], 4)}
+        bounds = {v[0]: v[1] for v in ENTRIES.values()}
+        roof_all = [roofline_entry(fam, k, bounds[fam]) for fam, k in sorted(kern.items(), key=lambda x: -x[1]["total_ms"])]
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            from oracle.cpu_path import time_cpu_step
+            from oracle.cpu_path import cpu_model, time_cpu_step
             log("cpu baseline ...")
-            sec, threads = time_cpu_step(res=args.res, images=1, steps=args.cpu_steps)
-            cpu = {"value": round(1.0 / sec, 4), "unit": "images/s", "cores": threads, "kind": "port",
-                   "sample": f"1 image {args.res}x{args.res} fwd+bwd (no optimizer), fp32, best of {args.cpu_steps} "
-                             "steps: same model with the reference's CPU MSDA (ms_deform_attn_core_pytorch) and "
-                             "MultiheadAttention math (oracle/cpu_path.py)"}
+            s512, threads, t512 = time_cpu_step(res=512, images=1, steps=3, warmup=1)
+            s1k, _, t1k = time_cpu_step(res=args.res, images=1, steps=3, warmup=1)
+            cpu = {"value": round(1.0 / s1k, 4), "unit": "images/s", "cores": threads, "kind": "port",
+                   "os_cpu_count": os.cpu_count(), "cpu_model": cpu_model(),
+                   "config1_512_images_per_s": round(1.0 / s512, 4),
+                   "sample": f"reference CPU path (oracle/cpu_path.py: the same model with the reference's "
+                             f"ms_deform_attn_core_pytorch and MultiheadAttention math), fp32 fwd+bwd, 1 image, "
+                             f"warm-up 1 + median of 3 at {args.res}^2 (value; s/step {[round(t, 3) for t in t1k]}) "
+                             f"and at 512^2 (config 1; s/step {[round(t, 3) for t in t512]}); {threads} threads = "
+                             f"os.cpu_count() capped by this process's CPU share"}
         line = {
             "metric": METRIC, "value": round(value, 3), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.amp if amp is not None else "fp32",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.amp if args.amp != "none" else "fp32",
             "data": "synthetic (randn images, random-init weights)",
             "config": {"workload": "config 2: Mask2Former R50 COCO-panoptic, 100 queries, 1024x1024, "
                                    f"{args.batch} images/GPU, fwd+bwd+AdamW; pixel decoder + MSDA in fp32 "
                                    f"(as the reference forces), backbone/decoder under AMP {args.amp}",
                        "model": "maskformer2_R50", "global_batch": world * args.batch,
                        "seq_len": sum((args.res // s) ** 2 for s in (32, 16, 8)), "queries": args.queries,
-                       "parallelism": f"dp{world}"},
-            "roofline": roof, "cpu_baseline": cpu,
-            "kernels": {k: {"calls_per_step": v["calls"] / args.steps, "mean_ms": round(v["mean_ms"], 4)}
-                        for k, v in kern.items()},
+                       "parallelism": f"dp{world}", "env": knobs},
+            "roofline": roof, "roofline_all": roof_all, "modes": modes, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

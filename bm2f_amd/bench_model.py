@@ -269,11 +269,25 @@ def make_optimizer(model):
     return torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.05, foreach=True)
 
 
-def train_step(model, opt, images, amp_dtype=torch.bfloat16, clip=0.01):
+def make_scaler(amp_dtype):
+    """detectron2's AMPTrainer scales the loss under fp16 autocast (GradScaler); bf16 and fp32 need none."""
+    if amp_dtype is torch.float16:
+        return torch.amp.GradScaler("cuda")
+    return None
+
+
+def train_step(model, opt, images, amp_dtype=torch.bfloat16, clip=0.01, scaler=None):
     opt.zero_grad(set_to_none=True)
     with torch.autocast(device_type=images.device.type, dtype=amp_dtype, enabled=amp_dtype is not None):
         out = model(images)
         loss = surrogate_loss(out)
+    if scaler is not None:
+        scaler.scale(loss).backward()
+        scaler.unscale_(opt)
+        torch.nn.utils.clip_grad_norm_(model.parameters(), clip, foreach=True)
+        scaler.step(opt)
+        scaler.update()
+        return loss.detach()
     loss.backward()
     torch.nn.utils.clip_grad_norm_(model.parameters(), clip, foreach=True)
     opt.step()

@@ -275,40 +275,42 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // ------------------------------------------------------------------------------------------------
 // fp32 backward, spatially tiled: encoder self-attention (Lq == S, query i = pyramid position i).
 //
-// Workgroup = (spatial tile, head m, image n).  A tile is the same normalised rectangle on every level
-// (level l's tile ty spans rows [ty*H_l/nty, (ty+1)*H_l/nty)), so its queries at every level sample the
-// same neighbourhood.  Phase 0 takes the bounding box of the corners the tile's samples touch per level,
-// the contribution bound, and stages the tile's grad_output rows (this head) in LDS; the window = that box
-// clipped to the tile +- halo (halo shrunk until the window fits the index budget).
+// Workgroup = (spatial tile, head m, image n), 1024 threads.  A tile is the same normalised rectangle on
+// every level (level l's tile ty spans rows [ty*H_l/nty, (ty+1)*H_l/nty)), so its queries at every level
+// sample the same neighbourhood of every level.
 //
-// grad_value is a scatter: every (query, point, corner) adds w_c * a * g[query] (32 channels) to one
-// pixel row.  Scattering those rows into LDS costs 16 LDS atomics per corner per 8-lane group, and
-// gfx950's LDS atomics are slow (ds_add_f32 ~190 cycles per wave-instruction, ds_add_u64 ~30:
-// tools/ubench).  Instead the scatter is turned into a gather inside the workgroup:
-//   phase 2  for each in-window corner ONE lane stores the record's coefficient w_c * a and pushes the
-//            record onto its window row's list (one ds_wrxchg per corner: head[row] <-> record id;
-//            the record id encodes (query, level, point, corner), so only coef + next are stored);
-//   phase 3  an 8-lane group per window row walks the row's list, accumulating coef * g[query] (g from
-//            LDS) in registers as exact int64 fixed point (scale 2^e from the phase-0 bound so no sum can
-//            overflow: order-independent, hence deterministic), and adds the row to HBM once with
-//            row-contiguous atomics (32 lanes = 128 B).
-// Corners outside the window, and workgroups whose bound is 0 or non-finite, use direct fp32 atomics, so
-// NaN/inf propagate exactly as in the reference.  grad_loc / grad_attn are owned per (q, m) and written
-// once; channel reductions use DPP within the 8-lane group.
+// grad_value is a scatter: every (query, sample, corner) adds w_c * a * g[query] (32 channels) to one
+// pixel row.  Here it becomes a gather inside the workgroup:
+//   phase 0  one lane per query derives its L*P samples ONCE (softmax and ref + offset / (W, H) on the
+//            fused path, or the given loc / attn) into a 12-byte descriptor {h, w, a} per sample in LDS
+//            (h = loc_y * H - 0.5 ...; h = w = -2 when the sample lies outside (-1, H) x (-1, W)), stages
+//            the tile's grad_output rows (this head) in LDS and takes the bounding box of the touched
+//            corners per level.  The window = that box clipped to the tile +- halo.
+//   phase 2  an 8-lane group per query (float4 of channels per lane) gathers each sample's 4 corner rows,
+//            writes grad_loc / grad_attn (channel sums by DPP), and pushes the sample id onto the list of
+//            its top-left corner's cell in the window (one LDS exchange per sample: the 2x2 corner block of
+//            a sample is one cell of the window grid extended by one row / column up and left).  Samples
+//            whose corners leave the window add their 4 corner rows with direct fp32 atomics.
+//   phase 3  a 4-lane group per window pixel walks the 4 lists whose cells cover it ((y,x) -> corner 1 of
+//            cell (y,x), corner 2 of (y,x-1), corner 3 of (y-1,x), corner 4 of (y-1,x-1)), accumulating
+//            w_c * a * g[query] in fp32 from the LDS descriptors and g rows (8 channels per lane), then adds
+//            the row to HBM once with row-contiguous fp32 atomics (two 128-B rows per instruction).
+// Summation order (list order, atomics across workgroups) is not fixed, as in the reference's atomics.
+// grad_loc / grad_attn (or d offset / d logit) are owned per (q, m) and written once.
 //
-// FUSED = true is the same kernel for the fused front end (see msda_fused_fwd): the samples come from the
-// raw projection (offsets | logits) and the reference points, and the outputs are the gradients w.r.t.
-// that projection: d offset = sum_c dval/dloc * g * a / (W, H) * (W, H) (the level scale cancels) and
-// d logit = a * (d attn - sum_k a_k d attn_k) (softmax backward over the L*P logits of the pair).
+// FUSED = true: the samples come from the raw projection (offsets | logits) and the reference points, and
+// the outputs are the gradients w.r.t. that projection: d offset = d loc / (W, H) = sum_c dval/dloc * g * a
+// in pixel units (the level scale cancels) and d logit = a * (d attn - sum_k a_k d attn_k) (softmax
+// backward over the pair's L*P logits).
 // ------------------------------------------------------------------------------------------------
-constexpr int kWalkLanes = 4;  // phase-3 lanes per window row (4: 3.96 ms; 8: 4.10; 2: 4.15 at config 2)
+constexpr int kWalkLanes = 4;   // phase-3 lanes per window pixel (8 channels each)
+constexpr int kBwdThreads = 1024;
 
 struct TileState {
   int bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
-  unsigned int gmax, amax;
-  float scale;
-  double unscale, rscale;  // rscale = 2^e: fp32 partial sums re-expressed in fixed-point units
-  int wy0[kTileMaxL], wx0[kTileMaxL], wh[kTileMaxL], ww[kTileMaxL], woff[kTileMaxL + 1];
+  int wy0[kTileMaxL], wx0[kTileMaxL], wh[kTileMaxL], ww[kTileMaxL];
+  int roff[kTileMaxL + 1];   // window pixel offsets per level
+  int coff[kTileMaxL + 1];   // extended-cell offsets per level ((wh+1) x (ww+1) cells)
   int qc[kTileMaxL + 1], qy0[kTileMaxL], qx0[kTileMaxL], qw[kTileMaxL];
 };
 
@@ -327,34 +329,27 @@ __device__ __forceinline__ int tile_query(const TileState& ts, const TileGeom& g
   return geo.start[lq] + (ts.qy0[lq] + r / ts.qw[lq]) * geo.W[lq] + ts.qx0[lq] + r % ts.qw[lq];
 }
 
-template <int P, int LT, bool FUSED, int TPB>
-__global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
+template <int LT, bool FUSED>
+__global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
-    float* __restrict__ gloc, float* __restrict__ gattn, float* __restrict__ scratch, int* __restrict__ wtab) {
-  constexpr int D = 32;
-  constexpr int PB = TPB <= 768 ? 4 : 1;  // points per gather batch (1024 threads: 128 VGPRs, no room)
-  static_assert(P % PB == 0, "batches cover the points");
+    float* __restrict__ gloc, float* __restrict__ gattn) {
+  constexpr int D = 32, P = 4, LP = LT * P;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   __shared__ TileState ts;
 
-  const int tile = geo.head_major ? blockIdx.y : blockIdx.x, m = geo.head_major ? blockIdx.x : blockIdx.y;
-  const int n = blockIdx.z;
+  const int tile = blockIdx.x, m = blockIdx.y, n = blockIdx.z;
   const int ty = tile / geo.ntx, tx = tile - ty * geo.ntx;
-  const int L = LT > 0 ? LT : geo.L;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwaves = blockDim.x >> 6;
-  const int j = lane & 7, gq = lane >> 3;
-  const int64_t rs = static_cast<int64_t>(M) * D;
-  const int MLP2 = M * L * P * 2;  // fused: column of the first logit in a projection row
-  const int LP4 = L * P * 4;       // records per query
-  // LDS carve-up: g rows [max_qt][32] f32 | coef [max_qt * LP4] f32 | next [max_qt * LP4] u16 | head [max_rows] i32
+  const int rs = M * D;  // value row stride (elements); N*S*M*D < 2^31 is checked on the host
+  // LDS carve-up: g rows [max_qt][32] f32 | desc [max_qt * LP][3] f32 | nxt [max_qt * LP] u16 | head [max_cells] i32
   float* gsh = reinterpret_cast<float*>(lds_raw);
-  float* coef = gsh + geo.max_qt * D;
-  unsigned short* nxt = reinterpret_cast<unsigned short*>(coef + geo.max_qt * LP4);
-  int* head = reinterpret_cast<int*>(lds_raw + ((geo.max_qt * D + geo.max_qt * LP4) * 4 +
-                                                ((geo.max_qt * LP4 * 2 + 15) & ~15)));
+  float* desc = gsh + geo.max_qt * D;
+  unsigned short* nxt = reinterpret_cast<unsigned short*>(desc + geo.max_qt * LP * 3);
+  int* head = reinterpret_cast<int*>(lds_raw + ((geo.max_qt * D + geo.max_qt * LP * 3) * 4 +
+                                                ((geo.max_qt * LP * 2 + 15) & ~15)));
 
-  if (tid < L) {
+  if (tid < LT) {
     const int l = tid;
     const int y0 = tile_lo(ty, geo.H[l], geo.nty), y1 = tile_lo(ty + 1, geo.H[l], geo.nty);
     const int x0 = tile_lo(tx, geo.W[l], geo.ntx), x1 = tile_lo(tx + 1, geo.W[l], geo.ntx);
@@ -364,372 +359,301 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
     ts.qc[l + 1] = (y1 - y0) * (x1 - x0);
     ts.bb[l][0] = 0x7fffffff; ts.bb[l][1] = -1; ts.bb[l][2] = 0x7fffffff; ts.bb[l][3] = -1;
   }
-  if (tid == 0) { ts.gmax = 0u; ts.amax = 0u; }
   __syncthreads();
   if (tid == 0) {
     ts.qc[0] = 0;
-    for (int l = 0; l < L; ++l) ts.qc[l + 1] += ts.qc[l];
+    for (int l = 0; l < LT; ++l) ts.qc[l + 1] += ts.qc[l];
   }
   __syncthreads();
-  const int Qt = ts.qc[L];
+  const int Qt = ts.qc[LT];
 
-  // ---- phase 0: bounding boxes of the touched corners, and the contribution bound ------------------
+  // ---- phase 0a: this head's grad_output rows of the tile's queries -> LDS (float4 per lane) --------
+  for (int idx = tid; idx < Qt * 8; idx += blockDim.x) {
+    const int qi = idx >> 3, j = idx & 7;
+    const int q = tile_query(ts, geo, qi);
+    const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
+    *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = ld4(gout + pair * D + 4 * j);
+  }
+
+  // ---- phase 0b: sample descriptors (one lane per query) and the touched-corner bounding boxes -------
   {
-    int bmin_y[kTileMaxL], bmax_y[kTileMaxL], bmin_x[kTileMaxL], bmax_x[kTileMaxL];
+    int bmin_y[LT], bmax_y[LT], bmin_x[LT], bmax_x[LT];
 #pragma unroll
-    for (int l = 0; l < kTileMaxL; ++l) { bmin_y[l] = 0x7fffffff; bmax_y[l] = -1; bmin_x[l] = 0x7fffffff; bmax_x[l] = -1; }
-    float gmax = 0.f, amax = 0.f;
-    for (int base = wid * 8; base < Qt; base += nwaves * 8) {
-      const int qi = base + gq;
+    for (int l = 0; l < LT; ++l) { bmin_y[l] = 0x7fffffff; bmax_y[l] = -1; bmin_x[l] = 0x7fffffff; bmax_x[l] = -1; }
+    for (int qi = tid; qi < ((Qt + 63) & ~63); qi += blockDim.x) {
       if (qi < Qt) {
         const int q = tile_query(ts, geo, qi);
-        const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
-        const f4 gv4 = ld4(gout + pair * D + 4 * j);
-        *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = gv4;
-        const float gm = fmaxf(fmaxf(fabsf(gv4.x), fabsf(gv4.y)), fmaxf(fabsf(gv4.z), fabsf(gv4.w)));
-        // fmaxf drops NaN: fold non-finite values in as +inf so the workgroup takes the atomic path
-        const bool gbad = !(isfinite(gv4.x) && isfinite(gv4.y) && isfinite(gv4.z) && isfinite(gv4.w));
-        gmax = gbad ? INFINITY : fmaxf(gmax, gm);
-        const float* prow = FUSED ? fe.proj + (static_cast<int64_t>(n) * S + q) * fe.ld : nullptr;
-        const float* rrow = FUSED ? fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * L * 2 : nullptr;
-        for (int k = j; k < L * P; k += 8) {
-          const int l = k / P;
-          float lx, ly;
-          if constexpr (FUSED) {
-            // softmax weights are in [0, 1]: the bound only needs the logits to be finite
-            const float lg = prow[MLP2 + m * L * P + k];
-            amax = isfinite(lg) ? fmaxf(amax, 1.f) : INFINITY;
-            const float2 off = *reinterpret_cast<const float2*>(prow + (m * L * P + k) * 2);
-            const float2 rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
-            lx = rf.x + off.x / static_cast<float>(geo.W[l]);
-            ly = rf.y + off.y / static_cast<float>(geo.H[l]);
-          } else {
-            const float av = attn[pair * L * P + k];
-            amax = isfinite(av) ? fmaxf(amax, fabsf(av)) : INFINITY;
-            const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (pair * L * P + k));
-            lx = xy.x;
-            ly = xy.y;
-          }
-          const int H = geo.H[l], W = geo.W[l];
-          const float h = ly * H - 0.5f, w = lx * W - 0.5f;
-          if (geo.bbox && h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W)) {
-            const int h0 = static_cast<int>(floorf(h)), w0 = static_cast<int>(floorf(w));
-            const int ylo = max(h0, 0), yhi = min(h0 + 1, H - 1), xlo = max(w0, 0), xhi = min(w0 + 1, W - 1);
+        const int64_t nq = static_cast<int64_t>(n) * S + q;
+        float av[LP], lx[LP], ly[LP];
+        if constexpr (FUSED) {
+          const float* prow = fe.proj + nq * fe.ld;
+          const float* lg = prow + M * LP * 2 + m * LP;
+          const float* of = prow + m * LP * 2;
+          const float* rrow = fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * LT * 2;
+          float mx = -INFINITY;
 #pragma unroll
-            for (int ll = 0; ll < kTileMaxL; ++ll)
-              if (ll == l) {
-                bmin_y[ll] = min(bmin_y[ll], ylo); bmax_y[ll] = max(bmax_y[ll], yhi);
-                bmin_x[ll] = min(bmin_x[ll], xlo); bmax_x[ll] = max(bmax_x[ll], xhi);
-              }
+          for (int k = 0; k < LP; ++k) { av[k] = lg[k]; mx = fmaxf(mx, av[k]); }
+          float sum = 0.f;
+#pragma unroll
+          for (int k = 0; k < LP; ++k) { av[k] = expf(av[k] - mx); sum += av[k]; }
+          const float inv = 1.f / sum;
+#pragma unroll
+          for (int l = 0; l < LT; ++l) {
+            const float2 rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
+#pragma unroll
+            for (int p = 0; p < P; ++p) {
+              const float2 off = *reinterpret_cast<const float2*>(of + (l * P + p) * 2);
+              lx[l * P + p] = rf.x + off.x / static_cast<float>(geo.W[l]);
+              ly[l * P + p] = rf.y + off.y / static_cast<float>(geo.H[l]);
+              av[l * P + p] *= inv;
+            }
+          }
+        } else {
+          const int64_t pair = nq * M + m;
+#pragma unroll
+          for (int k = 0; k < LP; ++k) {
+            const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (pair * LP + k));
+            lx[k] = xy.x;
+            ly[k] = xy.y;
+            av[k] = attn[pair * LP + k];
+          }
+        }
+        float* dq = desc + qi * LP * 3;
+#pragma unroll
+        for (int l = 0; l < LT; ++l) {
+          const int H = geo.H[l], W = geo.W[l];
+#pragma unroll
+          for (int p = 0; p < P; ++p) {
+            const int k = l * P + p;
+            float h = ly[k] * H - 0.5f, w = lx[k] * W - 0.5f;
+            const bool ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
+            h = ok ? h : -2.f;
+            w = ok ? w : -2.f;
+            dq[3 * k] = h;
+            dq[3 * k + 1] = w;
+            dq[3 * k + 2] = av[k];
+            if (ok) {
+              const int h0 = static_cast<int>(floorf(h)), w0 = static_cast<int>(floorf(w));
+              bmin_y[l] = min(bmin_y[l], max(h0, 0)); bmax_y[l] = max(bmax_y[l], min(h0 + 1, H - 1));
+              bmin_x[l] = min(bmin_x[l], max(w0, 0)); bmax_x[l] = max(bmax_x[l], min(w0 + 1, W - 1));
+            }
           }
         }
       }
-    }
-    if (!geo.bbox) {  // window = tile +- halo: no reduction
 #pragma unroll
-      for (int l = 0; l < kTileMaxL; ++l) { bmin_y[l] = 0; bmax_y[l] = 0x3fffffff; bmin_x[l] = 0; bmax_x[l] = 0x3fffffff; }
-    }
+      for (int l = 0; l < LT; ++l) {
 #pragma unroll
-    for (int l = 0; l < kTileMaxL; ++l) {
-#pragma unroll
-      for (int o = 32; o > 0 && geo.bbox; o >>= 1) {
-        bmin_y[l] = min(bmin_y[l], __shfl_xor(bmin_y[l], o)); bmax_y[l] = max(bmax_y[l], __shfl_xor(bmax_y[l], o));
-        bmin_x[l] = min(bmin_x[l], __shfl_xor(bmin_x[l], o)); bmax_x[l] = max(bmax_x[l], __shfl_xor(bmax_x[l], o));
+        for (int o = 32; o > 0; o >>= 1) {
+          bmin_y[l] = min(bmin_y[l], __shfl_xor(bmin_y[l], o)); bmax_y[l] = max(bmax_y[l], __shfl_xor(bmax_y[l], o));
+          bmin_x[l] = min(bmin_x[l], __shfl_xor(bmin_x[l], o)); bmax_x[l] = max(bmax_x[l], __shfl_xor(bmax_x[l], o));
+        }
       }
-      if (lane == 0 && l < L) {
+    }
+    if (lane == 0 && tid < ((Qt + 63) & ~63)) {
+#pragma unroll
+      for (int l = 0; l < LT; ++l) {
         atomicMin(&ts.bb[l][0], bmin_y[l]); atomicMax(&ts.bb[l][1], bmax_y[l]);
         atomicMin(&ts.bb[l][2], bmin_x[l]); atomicMax(&ts.bb[l][3], bmax_x[l]);
       }
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      gmax = fmaxf(gmax, __shfl_xor(gmax, o));
-      amax = fmaxf(amax, __shfl_xor(amax, o));
-    }
-    if (lane == 0) {
-      atomicMax(&ts.gmax, __float_as_uint(gmax));
-      atomicMax(&ts.amax, __float_as_uint(amax));
-    }
   }
   __syncthreads();
 
-  // ---- window choice ----------------------------------------------------------------------------
+  // ---- window: touched box clipped to the tile +- halo; the halo shrinks until the cells fit ----------
   if (tid == 0) {
-    const float bound = __uint_as_float(ts.gmax) * __uint_as_float(ts.amax);
-    const bool use_lds = bound > 1e-30f && bound < 1e30f;  // else: direct atomics (zeros, inf or NaN)
-    // at most Qt*L*P contributions reach one element: keep their sum below 2^52 so the f64
-    // accumulation of integer-valued terms in phase 3 is exact
-    const int cnt_bits = 32 - __clz(max(Qt * L * P, 1)) + 1;
-    const int e = use_lds ? 52 - cnt_bits - static_cast<int>(ceilf(log2f(bound))) : 0;
-    ts.scale = use_lds ? ldexpf(1.f, e) : 0.f;
-    ts.unscale = use_lds ? ldexp(1.0, -e) : 0.0;
-    ts.rscale = use_lds ? ldexp(1.0, e) : 0.0;
-    for (int halo = use_lds ? geo.max_halo : -1; halo >= 0; --halo) {
-      int total = 0;
-      for (int l = 0; l < L; ++l) {
+    for (int halo = geo.max_halo; halo >= 0; --halo) {
+      int rows = 0, cells = 0;
+      for (int l = 0; l < LT; ++l) {
         const int H = geo.H[l], W = geo.W[l];
         const int ry0 = max(tile_lo(ty, H, geo.nty) - halo, 0), ry1 = min(tile_lo(ty + 1, H, geo.nty) - 1 + halo, H - 1);
         const int rx0 = max(tile_lo(tx, W, geo.ntx) - halo, 0), rx1 = min(tile_lo(tx + 1, W, geo.ntx) - 1 + halo, W - 1);
         const int wy0 = max(ry0, ts.bb[l][0]), wy1 = min(ry1, ts.bb[l][1]);
         const int wx0 = max(rx0, ts.bb[l][2]), wx1 = min(rx1, ts.bb[l][3]);
-        const int wh = wy1 >= wy0 ? wy1 - wy0 + 1 : 0, ww = wx1 >= wx0 ? wx1 - wx0 + 1 : 0;
+        const bool any = wy1 >= wy0 && wx1 >= wx0;
         ts.wy0[l] = wy0; ts.wx0[l] = wx0;
-        ts.wh[l] = (wh && ww) ? wh : 0; ts.ww[l] = (wh && ww) ? ww : 0;
-        ts.woff[l] = total;
-        total += ts.wh[l] * ts.ww[l];
+        ts.wh[l] = any ? wy1 - wy0 + 1 : 0; ts.ww[l] = any ? wx1 - wx0 + 1 : 0;
+        ts.roff[l] = rows;
+        ts.coff[l] = cells;
+        rows += ts.wh[l] * ts.ww[l];
+        cells += any ? (ts.wh[l] + 1) * (ts.ww[l] + 1) : 0;
       }
-      ts.woff[L] = total;
-      if (total <= geo.max_rows) break;
+      ts.roff[LT] = rows;
+      ts.coff[LT] = cells;
+      if (cells <= geo.max_rows) break;
       if (halo == 0) {  // cannot happen when the budget covers a tile's own footprint; stay correct anyway
-        for (int l = 0; l <= L; ++l) ts.woff[l] = 0;
-        for (int l = 0; l < L; ++l) { ts.wh[l] = 0; ts.ww[l] = 0; }
+        for (int l = 0; l <= LT; ++l) { ts.roff[l] = 0; ts.coff[l] = 0; }
+        for (int l = 0; l < LT; ++l) { ts.wh[l] = 0; ts.ww[l] = 0; }
       }
-    }
-    if (!use_lds) {
-      for (int l = 0; l <= L; ++l) ts.woff[l] = 0;
-      for (int l = 0; l < L; ++l) { ts.wh[l] = 0; ts.ww[l] = 0; ts.wy0[l] = 0; ts.wx0[l] = 0; }
     }
   }
   __syncthreads();
-  const int rows_total = ts.woff[L];
-  const float fscale = ts.scale;
-  for (int i = tid; i < rows_total; i += blockDim.x) head[i] = -1;
-  const int64_t wg = (static_cast<int64_t>(n) * M + m) * (geo.nty * geo.ntx) + tile;
-  if (scratch && tid == 0) {  // the window of this workgroup, for the combine pass
-    int* wt = wtab + wg * kWtab;
-    for (int l = 0; l < kTileMaxL; ++l) {
-      const bool on = l < L;
-      wt[5 * l + 0] = on ? ts.wy0[l] : 0;
-      wt[5 * l + 1] = on ? ts.wx0[l] : 0;
-      wt[5 * l + 2] = on ? ts.wh[l] : 0;
-      wt[5 * l + 3] = on ? ts.ww[l] : 0;
-      wt[5 * l + 4] = on ? ts.woff[l] : 0;
-    }
-    wt[20] = rows_total;
-  }
+  const int cells_total = ts.coff[LT];
+  for (int i = tid; i < cells_total; i += blockDim.x) head[i] = 0xffff;
   __syncthreads();
 
-  // ---- phase 2: gradients; grad_value into the windows --------------------------------------------
-  constexpr int LPS = (LT > 0 ? LT : 1) * P;  // fused path: per-pair arrays, statically indexed
-  for (int base = wid * 8; base < Qt; base += nwaves * 8) {
-    const int qi = base + gq;
-    if (qi >= Qt) continue;  // whole lane group (same qi) idles together
-    const int q = tile_query(ts, geo, qi);
-    const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
-    const f4 g = ld4(gout + pair * D + 4 * j);
+  // ---- phase 2: gather, grad_loc / grad_attn, list pushes -----------------------------------------------
+  {
+    const int j = lane & 7, gq = lane >> 3;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    // fused: softmax statistics of the pair (every lane), this lane's two grad_attn values, and
-    // sum_k a_k dA_k; a_k itself is recomputed per point (fewer live registers than keeping all L*P)
-    float smx = 0.f, sinv = 0.f, myga0 = 0.f, myga1 = 0.f, dot = 0.f;
-    const float* prow = FUSED ? fe.proj + (static_cast<int64_t>(n) * S + q) * fe.ld : nullptr;
-    const float* rrow = FUSED ? fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * (LT > 0 ? LT : 1) * 2 : nullptr;
-    const float* lgt = FUSED ? prow + MLP2 + m * LPS : nullptr;
-    if constexpr (FUSED) {
-      float mx = -INFINITY;
-#pragma unroll
-      for (int k = 0; k < LPS; ++k) mx = fmaxf(mx, lgt[k]);
-      float sum = 0.f;
-#pragma unroll
-      for (int k = 0; k < LPS; ++k) sum += expf(lgt[k] - mx);
-      smx = mx;
-      sinv = 1.f / sum;
-    }
+    for (int base = wid * 8; base < Qt; base += nwaves * 8) {
+      const int qi = base + gq;
+      if (qi >= Qt) continue;  // whole lane group (same qi) idles together
+      const int q = tile_query(ts, geo, qi);
+      const int64_t nq = static_cast<int64_t>(n) * S + q;
+      const f4 g = *reinterpret_cast<const f4*>(gsh + qi * D + 4 * j);
+      const float* dq = desc + qi * LP * 3;
+      float dot = 0.f, myga0 = 0.f, myga1 = 0.f;
 #pragma unroll 1
-    for (int l = 0; l < L; ++l) {
-      const int H = geo.H[l], W = geo.W[l];
-      const int64_t lbase = ((static_cast<int64_t>(n) * S + geo.start[l]) * M + m) * D + 4 * j;
-      const int wy0 = ts.wy0[l], wx0 = ts.wx0[l], wh = ts.wh[l], ww = ts.ww[l], woff = ts.woff[l];
-      float st_a = 0.f, st_l = 0.f;
-      static_assert(P <= 4, "one lane per grad_loc component: 2P <= 8");
-      float2 rf = make_float2(0.f, 0.f);
-      if constexpr (FUSED) rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
-      // points in batches of PB: every corner load of a batch is issued before any of its math, so a
-      // wave keeps 4*PB row gathers in flight (the kernel is gather-latency bound).  With PB = 1 (the
-      // 128-VGPR budget of 1024-thread blocks) the point loop stays rolled: unrolled it spilled
-      constexpr int PUNROLL = PB == 1 ? 1 : P / PB;
-#pragma unroll PUNROLL
-      for (int p0 = 0; p0 < P; p0 += PB) {
-        Corners kb[PB];
-        float ab[PB];
-        f4 vb[PB][4];
+      for (int l = 0; l < LT; ++l) {
+        const int H = geo.H[l], W = geo.W[l];
+        const int lbase = ((n * S + geo.start[l]) * M + m) * D + 4 * j;
+        const int wy0 = ts.wy0[l], wx0 = ts.wx0[l], wh = ts.wh[l], ww = ts.ww[l], coff = ts.coff[l];
+        float st_l = 0.f, st_a = 0.f;
+        // points in batches of PB: every corner load of a batch is issued before any of its math
+        constexpr int PB = 2;
 #pragma unroll
-        for (int pp = 0; pp < PB; ++pp) {
-          const int p = p0 + pp;
-          const int64_t kk = (pair * L + l) * P + p;
-          float sx, sy, a;
-          if constexpr (FUSED) {
-            const float2 off = *reinterpret_cast<const float2*>(prow + (m * LT * P + l * P + p) * 2);
-            sx = rf.x + off.x / static_cast<float>(W);
-            sy = rf.y + off.y / static_cast<float>(H);
-            a = expf(lgt[l * P + p] - smx) * sinv;
-          } else {
-            const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * kk);
-            sx = xy.x; sy = xy.y; a = attn[kk];
+        for (int p0 = 0; p0 < P; p0 += PB) {
+          f4 vb[PB][4];
+          float hh[PB], wwf[PB], aa[PB];
+          int h0s[PB], w0s[PB];
+#pragma unroll
+          for (int pp = 0; pp < PB; ++pp) {
+            const int k = l * P + p0 + pp;
+            hh[pp] = dq[3 * k]; wwf[pp] = dq[3 * k + 1]; aa[pp] = dq[3 * k + 2];
+            const int h0 = static_cast<int>(floorf(hh[pp])), w0 = static_cast<int>(floorf(wwf[pp]));
+            h0s[pp] = h0; w0s[pp] = w0;
+            const int y0 = min(max(h0, 0), H - 1), y1 = min(max(h0 + 1, 0), H - 1);
+            const int x0 = min(max(w0, 0), W - 1), x1 = min(max(w0 + 1, 0), W - 1);
+            vb[pp][0] = ld4(value + lbase + (y0 * W + x0) * rs);
+            vb[pp][1] = ld4(value + lbase + (y0 * W + x1) * rs);
+            vb[pp][2] = ld4(value + lbase + (y1 * W + x0) * rs);
+            vb[pp][3] = ld4(value + lbase + (y1 * W + x1) * rs);
           }
-          kb[pp] = make_corners(sx, sy, H, W, lbase, rs);
-          ab[pp] = a;
-          vb[pp][0] = ld4(value + kb[pp].o1); vb[pp][1] = ld4(value + kb[pp].o2);
-          vb[pp][2] = ld4(value + kb[pp].o3); vb[pp][3] = ld4(value + kb[pp].o4);
-        }
 #pragma unroll
-        for (int pp = 0; pp < PB; ++pp) {
-        const int p = p0 + pp;
-        const Corners& k = kb[pp];
-        const float a = ab[pp];
-        const f4 v1 = k.c1 ? vb[pp][0] : z, v2 = k.c2 ? vb[pp][1] : z;
-        const f4 v3 = k.c3 ? vb[pp][2] : z, v4 = k.c4 ? vb[pp][3] : z;
-        const f4 tg = g * a;
-        const f4 val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
-        const f4 gw = -k.hy * v1 + k.hy * v2 - k.ly * v3 + k.ly * v4;
-        const f4 gh = -k.hx * v1 - k.lx * v2 + k.hx * v3 + k.lx * v4;
-        const f4 ta = g * val, tx2 = gw * tg, ty2 = gh * tg;
-        const float pa = sum8_dpp(ta.x + ta.y + ta.z + ta.w);
-        const float px = sum8_dpp(tx2.x + tx2.y + tx2.z + tx2.w);
-        const float py = sum8_dpp(ty2.x + ty2.y + ty2.z + ty2.w);
-        // every lane of the group holds the sums: lane p stores grad_attn of point p, lanes 2p, 2p+1
-        // store its grad_loc pair -- one store instruction per level instead of 3 per point.
-        // Fused: d offset = d loc / (W, H) = (px, py) exactly (loc = ref + off / (W, H)).
-        if constexpr (FUSED) {
-          const int kp = l * P + p;
-          const float gak = k.ok ? pa : 0.f;
-          dot += a * gak;
-          if (kp == j) myga0 = gak;
-          if (kp == j + 8) myga1 = gak;
-          if ((j >> 1) == p) st_l = k.ok ? ((j & 1) ? py : px) : 0.f;
-        } else {
-          if (j == p) st_a = k.ok ? pa : 0.f;
-          if ((j >> 1) == p) st_l = k.ok ? ((j & 1) ? H * py : W * px) : 0.f;
-        }
-        if (k.ok) {
-          const int dy = k.h0 - wy0, dx = k.w0 - wx0;
-          const bool iny0 = dy >= 0 && dy < wh, iny1 = dy + 1 >= 0 && dy + 1 < wh;
-          const bool inx0 = dx >= 0 && dx < ww, inx1 = dx + 1 >= 0 && dx + 1 < ww;
-          const int rbase = woff + dy * ww + dx;
-          // lane j < 4 pushes corner j's record onto its row list (one LDS exchange per corner)
-          if (j < 4) {
-            const bool valid = j == 0 ? k.c1 : (j == 1 ? k.c2 : (j == 2 ? k.c3 : k.c4));
-            const bool inside = (j < 2 ? iny0 : iny1) && ((j & 1) ? inx1 : inx0);
-            if (valid && inside && !(geo.ablate & 1)) {
-              const float wc = j == 0 ? k.w1 : (j == 1 ? k.w2 : (j == 2 ? k.w3 : k.w4));
-              const int id = ((qi * L + l) * P + p) * 4 + j;
-              coef[id] = wc * a;
-              const int old = atomicExch(head + rbase + (j >> 1) * ww + (j & 1), id);
-              nxt[id] = static_cast<unsigned short>(old);
+          for (int pp = 0; pp < PB; ++pp) {
+            const int p = p0 + pp;
+            const int k = l * P + p;
+            const int h0 = h0s[pp], w0 = w0s[pp];
+            const float a = aa[pp];
+            const bool ok = hh[pp] > -1.f;  // not-ok samples carry h = w = -2
+            const float ly = hh[pp] - static_cast<float>(h0), lx = wwf[pp] - static_cast<float>(w0);
+            const float hy = 1.f - ly, hx = 1.f - lx;
+            const bool c1 = h0 >= 0 && w0 >= 0, c2 = h0 >= 0 && w0 + 1 <= W - 1;
+            const bool c3 = h0 + 1 <= H - 1 && w0 >= 0, c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
+            const f4 v1 = c1 ? vb[pp][0] : z, v2 = c2 ? vb[pp][1] : z, v3 = c3 ? vb[pp][2] : z, v4 = c4 ? vb[pp][3] : z;
+            const f4 val = (hy * hx) * v1 + (hy * lx) * v2 + (ly * hx) * v3 + (ly * lx) * v4;
+            const f4 gw = hy * (v2 - v1) + ly * (v4 - v3);
+            const f4 gh = hx * (v3 - v1) + lx * (v4 - v2);
+            const f4 ta = g * val, tx2 = g * gw, ty2 = g * gh;
+            const float pa = sum8_dpp(ta.x + ta.y + ta.z + ta.w);
+            const float px = sum8_dpp(tx2.x + tx2.y + tx2.z + tx2.w) * a;
+            const float py = sum8_dpp(ty2.x + ty2.y + ty2.z + ty2.w) * a;
+            // lane p stores grad_attn of point p; lanes 2p, 2p+1 its grad_loc pair (one store per level)
+            if constexpr (FUSED) {
+              const float gak = ok ? pa : 0.f;
+              dot += a * gak;
+              if (k == j) myga0 = gak;
+              if (k == j + 8) myga1 = gak;
+              if ((j >> 1) == p) st_l = ok ? ((j & 1) ? py : px) : 0.f;
+            } else {
+              if (j == p) st_a = ok ? pa : 0.f;
+              if ((j >> 1) == p) st_l = ok ? ((j & 1) ? H * py : W * px) : 0.f;
+            }
+            if (!ok) continue;
+            // the sample's 2x2 corner block as one cell of the window grid (extended one row / column up
+            // and left): in the window when every corner inside the level lies inside the window
+            const bool ry = (h0 < 0 || (h0 >= wy0 && h0 < wy0 + wh)) &&
+                            (h0 + 1 > H - 1 || (h0 + 1 >= wy0 && h0 + 1 < wy0 + wh));
+            const bool rx = (w0 < 0 || (w0 >= wx0 && w0 < wx0 + ww)) &&
+                            (w0 + 1 > W - 1 || (w0 + 1 >= wx0 && w0 + 1 < wx0 + ww));
+            if (wh > 0 && ry && rx) {
+              if (j == 0) {
+                const int cell = coff + (h0 - wy0 + 1) * (ww + 1) + (w0 - wx0 + 1);
+                const int sid = qi * LP + k;
+                nxt[sid] = static_cast<unsigned short>(atomicExch(head + cell, sid));
+              }
+            } else {
+              // outside the window: the 4 corner rows go straight to HBM (fp32 atomics, as the reference)
+              const f4 tg = g * a;
+              const int o1 = lbase + (min(max(h0, 0), H - 1) * W + min(max(w0, 0), W - 1)) * rs;
+              const int dx = rs, dy = W * rs;
+              if (c1) { const f4 t = (hy * hx) * tg; float* o = gvalue + o1; atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w); }
+              if (c2) { const f4 t = (hy * lx) * tg; float* o = gvalue + o1 + (c1 ? dx : 0); atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w); }
+              if (c3) { const f4 t = (ly * hx) * tg; float* o = gvalue + o1 + (c1 ? dy : 0); atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w); }
+              if (c4) { const f4 t = (ly * lx) * tg; float* o = gvalue + lbase + ((h0 + 1) * W + w0 + 1) * rs; atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w); }
             }
           }
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const bool valid = c == 0 ? k.c1 : (c == 1 ? k.c2 : (c == 2 ? k.c3 : k.c4));
-            const bool inside = (c < 2 ? iny0 : iny1) && ((c & 1) ? inx1 : inx0);
-            if (!valid || inside || (geo.ablate & 4)) continue;
-            const float wc = c == 0 ? k.w1 : (c == 1 ? k.w2 : (c == 2 ? k.w3 : k.w4));
-            const f4 contrib = wc * tg;
-            const int64_t o = c == 0 ? k.o1 : (c == 1 ? k.o2 : (c == 2 ? k.o3 : k.o4));
-            atomicAdd(gvalue + o, contrib.x); atomicAdd(gvalue + o + 1, contrib.y);
-            atomicAdd(gvalue + o + 2, contrib.z); atomicAdd(gvalue + o + 3, contrib.w);
-          }
         }
+        if constexpr (FUSED) {
+          // gproj row: offsets (M, L, P, 2) -> this level's 2P values are contiguous
+          if (j < 2 * P) gloc[nq * (3 * M * LP) + (m * LT + l) * P * 2 + j] = st_l;
+        } else {
+          const int64_t kl = ((nq * M + m) * LT + l) * P;
+          if (j < P) gattn[kl + j] = st_a;
+          if (j < 2 * P) gloc[2 * kl + j] = st_l;
         }
       }
       if constexpr (FUSED) {
-        // gproj row: offsets (M, L, P, 2) -> this level's 2P values are contiguous
-        if (j < 2 * P) gloc[(static_cast<int64_t>(n) * S + q) * (MLP2 + MLP2 / 2) + (m * LT + l) * P * 2 + j] = st_l;
-      } else {
-        const int64_t kl = (pair * L + l) * P;
-        if (j < P) gattn[kl + j] = st_a;
-        if (j < 2 * P) gloc[2 * kl + j] = st_l;
+        // softmax backward over the pair's L*P logits: d logit_k = a_k (d a_k - sum_i a_i d a_i)
+        float* gl = gloc + nq * (3 * M * LP) + 2 * M * LP + m * LP;
+        static_assert(LP <= 16, "two logits per lane of the 8-lane group");
+        if (j < LP) gl[j] = dq[3 * j + 2] * (myga0 - dot);
+        if (j + 8 < LP) gl[j + 8] = dq[3 * (j + 8) + 2] * (myga1 - dot);
       }
-    }
-    if constexpr (FUSED) {
-      // softmax backward over the pair's L*P logits: d logit_k = a_k (d a_k - sum_i a_i d a_i)
-      float* gl = gloc + (static_cast<int64_t>(n) * S + q) * (MLP2 + MLP2 / 2) + MLP2 + m * LPS;
-      static_assert(LPS <= 16, "two logits per lane of the 8-lane group");
-      if (j < LPS) gl[j] = expf(lgt[j] - smx) * sinv * (myga0 - dot);
-      if (j + 8 < LPS) gl[j + 8] = expf(lgt[j + 8] - smx) * sinv * (myga1 - dot);
     }
   }
   __syncthreads();
 
-  // ---- phase 3: per window row, an LPR-lane group (32/LPR channels per lane) walks its list; the row
-  // goes to HBM once: as a partial row in this workgroup's scratch slot (plain stores, summed by
-  // msda_gv_combine) or, without scratch, added to grad_value with atomics.  Few lanes per row means many
-  // independent list walks per wave: the walk is one dependent LDS round trip per record, so more chains
-  // in flight hide more of that latency.
-  if (!(geo.ablate & 2)) {
+  // ---- phase 3: per window pixel, walk the 4 covering lists; one row-contiguous atomic add per row -------
+  {
     constexpr int LPR = kWalkLanes, CPL = D / LPR, RPW = 64 / LPR;  // lanes per row, channels per lane, rows per wave
-    const double unscale = ts.unscale;
-    const float inv_lp4 = 1.f / static_cast<float>(LP4);
-    const int jl = tid % LPR;
-    // rows in wave-lockstep batches of RPW (one per group), so the flush can transpose them
+    const int rows_total = ts.roff[LT];
+    const int jl = lane % LPR;
     for (int base = wid * RPW; base < rows_total; base += nwaves * RPW) {
       const int row = base + lane / LPR;
-      int id = row < rows_total ? head[row] : -1;
-      float v[CPL];
-      if (id >= 0 && geo.exact) {
-        // every term is an integer (fixed point, |sum| < 2^52): the f64 adds are exact, so the result
-        // does not depend on the list order
-        double a[CPL];
+      float acc[CPL];
 #pragma unroll
-        for (int k = 0; k < CPL; ++k) a[k] = 0.0;
-        while (id != 0xffff) {
-          const float c = coef[id] * fscale;
-          const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
-          f4 g[CPL / 4];
-#pragma unroll
-          for (int k = 0; k < CPL / 4; ++k) g[k] = *reinterpret_cast<const f4*>(gsh + q * D + CPL * jl + 4 * k);
-          id = nxt[id];
-#pragma unroll
-          for (int k = 0; k < CPL / 4; ++k) {
-            a[4 * k + 0] += static_cast<double>(rintf(c * g[k].x));
-            a[4 * k + 1] += static_cast<double>(rintf(c * g[k].y));
-            a[4 * k + 2] += static_cast<double>(rintf(c * g[k].z));
-            a[4 * k + 3] += static_cast<double>(rintf(c * g[k].w));
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) v[k] = static_cast<float>(a[k] * unscale);
-      } else {
-        // fp32 accumulation in list order: as accurate as the reference's fp32 atomics and, like them,
-        // not bitwise repeatable (M2F_MSDA_DETERMINISTIC=0; the default is the exact branch above)
-        f4 sacc[CPL / 4];
-#pragma unroll
-        for (int k = 0; k < CPL / 4; ++k) sacc[k] = f4{0.f, 0.f, 0.f, 0.f};
-        while (id >= 0 && id != 0xffff) {
-          const float c = coef[id];
-          const int q = static_cast<int>((static_cast<float>(id) + 0.5f) * inv_lp4);
-#pragma unroll
-          for (int k = 0; k < CPL / 4; ++k) sacc[k] += c * *reinterpret_cast<const f4*>(gsh + q * D + CPL * jl + 4 * k);
-          id = nxt[id];
-        }
-#pragma unroll
-        for (int k = 0; k < CPL / 4; ++k) {
-          v[4 * k] = sacc[k].x; v[4 * k + 1] = sacc[k].y; v[4 * k + 2] = sacc[k].z; v[4 * k + 3] = sacc[k].w;
-        }
-      }
-      if (scratch) {
-        if (row < rows_total) {
-          float* dst = scratch + (wg * geo.wrows + row) * D + CPL * jl;
-#pragma unroll
-          for (int k = 0; k < CPL / 4; ++k)
-            *reinterpret_cast<f4*>(dst + 4 * k) = f4{v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]};
-        }
-        continue;
-      }
-      if (geo.ablate & 8) {  // timing experiment: walk the lists, skip the HBM adds
-        if (v[0] == 12345.f) gvalue[0] = 0.f;
-        continue;
-      }
+      for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
       int64_t off = -1;  // element offset of channel 0 of this group's grad_value row (-1: none)
-      if (row < rows_total && head[row] >= 0) {
+      if (row < rows_total) {
         int l = 0;
-        while (row >= ts.woff[l + 1]) ++l;
-        const int rr = row - ts.woff[l];
-        const int y = ts.wy0[l] + rr / ts.ww[l], x = ts.wx0[l] + rr % ts.ww[l];
-        off = ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D;
+        while (row >= ts.roff[l + 1]) ++l;
+        const int ww = ts.ww[l], rr = row - ts.roff[l];
+        const int ey = rr / ww, ex = rr - ey * ww;  // window coordinates; cells are offset by (1, 1)
+        const int cw = ww + 1, cbase = ts.coff[l] + (ey + 1) * cw + ex + 1;
+        // corner 1 of cell (y, x), corner 2 of (y, x-1), corner 3 of (y-1, x), corner 4 of (y-1, x-1)
+        int id[4] = {head[cbase], head[cbase - 1], head[cbase - cw], head[cbase - cw - 1]};
+        bool any = false;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) any |= id[c] != 0xffff;
+        if (any) {
+          // every list holds distinct samples of this workgroup: bounded by their count
+          for (int it = 0; it < geo.max_qt * LP && (id[0] & id[1] & id[2] & id[3]) != 0xffff; ++it) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              if (id[c] == 0xffff) continue;
+              const int sid = id[c];
+              id[c] = nxt[sid];
+              const float h = desc[3 * sid], w = desc[3 * sid + 1], a = desc[3 * sid + 2];
+              const float ly = h - floorf(h), lx = w - floorf(w);
+              const float wy = (c & 2) ? ly : 1.f - ly, wx = (c & 1) ? lx : 1.f - lx;
+              const float coef = wy * wx * a;
+              const int qi = sid / LP;
+              const float* gr = gsh + qi * D + CPL * jl;
+#pragma unroll
+              for (int k = 0; k < CPL / 4; ++k) {
+                const f4 gv = *reinterpret_cast<const f4*>(gr + 4 * k);
+                acc[4 * k] += coef * gv.x; acc[4 * k + 1] += coef * gv.y;
+                acc[4 * k + 2] += coef * gv.z; acc[4 * k + 3] += coef * gv.w;
+              }
+            }
+          }
+          const int y = ts.wy0[l] + ey, x = ts.wx0[l] + ex;
+          off = ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D;
+        }
       }
-      // transpose the wave's rows (ds_bpermute) so that each atomic instruction covers two whole
-      // 128-byte rows, one dword per lane: gfx950's L2 takes atomics per request, and this issues 2
-      // requests per row instead of 8 (tools/ubench/global_atomic.hip: 1.6 vs 6.5 ms per 2.1 GB)
+      // transpose the wave's rows (ds_bpermute) so that each atomic instruction covers two whole 128-byte
+      // rows, one dword per lane: the L2 takes atomics per request, two requests per row this way
       const int c = lane & 31;
 #pragma unroll
       for (int i = 0; i < RPW / 2; ++i) {
@@ -737,48 +661,14 @@ __global__ void __launch_bounds__(TPB) msda_bwd_f32_tiled(
         float val = 0.f;
 #pragma unroll
         for (int k = 0; k < CPL; ++k) {
-          const float xk = __shfl(v[k], src);
+          const float xk = __shfl(acc[k], src);
           val = (c % CPL) == k ? xk : val;
         }
         const int64_t o = __shfl(off, src);
-        if (o >= 0 && val != 0.f) atomicAdd(gvalue + o + c, val);
+        if (o >= 0) atomicAdd(gvalue + o + c, val);
       }
     }
   }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Combine pass of the tiled backward with scratch: every grad_value row (n, pixel s, head m) adds the
-// partial rows that the workgroups whose windows cover it left in scratch, in a fixed neighbour order
-// (deterministic), to what the out-of-window atomics put there.  One 8-lane group per row, float4 per
-// lane; only tiles within the halo of the pixel can cover it.
-// ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) msda_gv_combine(const float* __restrict__ scratch, const int* __restrict__ wtab,
-                                                       TileGeom geo, int S, int M, float* __restrict__ gvalue) {
-  constexpr int D = 32;
-  const int s = blockIdx.x * 32 + (threadIdx.x >> 3), j = threadIdx.x & 7;
-  const int m = blockIdx.y, n = blockIdx.z;
-  if (s >= S) return;
-  int l = 0;
-  while (l + 1 < geo.L && s >= geo.start[l + 1]) ++l;
-  const int H = geo.H[l], W = geo.W[l];
-  const int y = (s - geo.start[l]) / W, x = (s - geo.start[l]) % W;
-  const int h = geo.max_halo;
-  const int ty0 = tile_of(max(y - h, 0), H, geo.nty), ty1 = tile_of(min(y + h, H - 1), H, geo.nty);
-  const int tx0 = tile_of(max(x - h, 0), W, geo.ntx), tx1 = tile_of(min(x + h, W - 1), W, geo.ntx);
-  const int64_t wg0 = (static_cast<int64_t>(n) * M + m) * (geo.nty * geo.ntx);
-  f4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int ty = ty0; ty <= ty1; ++ty)
-    for (int tx = tx0; tx <= tx1; ++tx) {
-      const int64_t wg = wg0 + ty * geo.ntx + tx;
-      const int* wt = wtab + wg * kWtab + 5 * l;
-      const int wy0 = wt[0], wx0 = wt[1], wh = wt[2], ww = wt[3], woff = wt[4];
-      if (y < wy0 || y >= wy0 + wh || x < wx0 || x >= wx0 + ww) continue;
-      const int row = woff + (y - wy0) * ww + (x - wx0);
-      acc += *reinterpret_cast<const f4*>(scratch + (wg * geo.wrows + row) * D + 4 * j);
-    }
-  f4* dst = reinterpret_cast<f4*>(gvalue + ((static_cast<int64_t>(n) * S + s) * M + m) * D + 4 * j);
-  *dst = *dst + acc;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -950,8 +840,12 @@ int env_int(const char* name, int dflt) {
 
 // Tile geometry for the tiled backward; false when the configuration does not qualify (then the
 // caller uses the untiled kernels).  Lq == S: the queries are the flattened pyramid.
-bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds, int& threads) {
+//   M2F_MSDA_TILE (16): tile edge on the finest level;  M2F_MSDA_HALO (8): window halo;
+//   M2F_MSDA_WIN_ROWS (2304): list-head cells per workgroup (the halo shrinks until the window fits).
+// Geometry only: every setting computes the same gradients (tests sweep them).
+bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds) {
   if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
+  if (static_cast<int64_t>(d.N) * d.S * d.M * d.D >= (int64_t{1} << 31)) return false;  // 32-bit row offsets
   geo = TileGeom{};
   geo.L = d.L;
   int64_t total = 0;
@@ -965,70 +859,49 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   if (total != d.S) return false;
-  const int tile = env_int("M2F_MSDA_TILE", 16);
-  threads = env_int("M2F_MSDA_THREADS", 1024);
+  const int tile = std::max(1, env_int("M2F_MSDA_TILE", 16));
   geo.nty = (geo.H[fi] + tile - 1) / tile;
   geo.ntx = (geo.W[fi] + tile - 1) / tile;
-  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 2048);
-  geo.max_halo = env_int("M2F_MSDA_HALO", 8);
-  geo.ablate = env_int("M2F_MSDA_ABLATE", 0);
-  geo.bbox = env_int("M2F_MSDA_BBOX", 1);
-  geo.exact = env_int("M2F_MSDA_DETERMINISTIC", 1);  // default: bitwise-repeatable gradients (+0.17 ms per launch)
-  // head-major grid measured 4.19 vs 4.13 ms per launch at config 2 (the tile-major order puts a tile's 8
-  // heads, which share grad_output and projection rows, on the same XCD): off by default
-  geo.head_major = env_int("M2F_MSDA_BWD_HEAD_MAJOR", 0) != 0 && d.M <= 65535;
-  // the index budget must hold every level's share of one tile (halo 0); tiles span at most
-  // ceil(n / nt) pixels per axis (tile_lo)
+  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 2304);
+  geo.max_halo = std::max(0, env_int("M2F_MSDA_HALO", 8));
+  // the cell budget must hold every level's share of one tile at halo 0 (tiles span at most
+  // ceil(n / nt) pixels per axis, tile_lo), plus the extra cell row / column
   int own = 0, qt = 0;
   for (int l = 0; l < d.L; ++l) {
     const int th = (geo.H[l] + geo.nty - 1) / geo.nty, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx;
-    own += (th + 1) * (tw + 1);
+    own += (th + 2) * (tw + 2);
     qt += th * tw;
   }
   geo.max_qt = qt;
-  int wrows = 0;  // the largest window any workgroup can choose: tile +- max_halo, clipped to the level
-  for (int l = 0; l < d.L; ++l) {
-    const int th = (geo.H[l] + geo.nty - 1) / geo.nty, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx;
-    wrows += std::min(geo.H[l], th + 2 * geo.max_halo) * std::min(geo.W[l], tw + 2 * geo.max_halo);
-  }
-  geo.wrows = std::min(wrows, geo.max_rows);
-  const int lp4 = d.L * d.P * 4;
-  if (own > geo.max_rows || static_cast<int64_t>(qt) * lp4 >= 0xffff) return false;
-  lds = static_cast<size_t>(qt) * 32 * 4 + static_cast<size_t>(qt) * lp4 * 4 +
-        ((static_cast<size_t>(qt) * lp4 * 2 + 15) & ~static_cast<size_t>(15)) + static_cast<size_t>(geo.max_rows) * 4;
-  return lds <= 150 * 1024 && threads >= 64 && threads <= 1024 && threads % 64 == 0;
+  const int lp = d.L * d.P;
+  if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff) return false;
+  lds = static_cast<size_t>(qt) * 32 * 4 + static_cast<size_t>(qt) * lp * 3 * 4 +
+        ((static_cast<size_t>(qt) * lp * 2 + 15) & ~static_cast<size_t>(15)) + static_cast<size_t>(geo.max_rows) * 4;
+  return lds <= 150 * 1024;
 }
 
-template <int P, int LT, bool FUSED, int TPB>
-void launch_tiled_t(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                    const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                    hipStream_t st, float* scratch, int* wtab) {
+template <int LT, bool FUSED>
+void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                  const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, hipStream_t st) {
   static bool attr = false;  // one flag per instantiation
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<P, LT, FUSED, TPB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     attr = true;
   }
-  const dim3 grid = geo.head_major ? dim3(d.M, geo.nty * geo.ntx, d.N) : dim3(geo.nty * geo.ntx, d.M, d.N);
-  msda_bwd_f32_tiled<P, LT, FUSED, TPB><<<grid, threads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga,
-                                                                    scratch, wtab);
-  if (scratch) {
-    const dim3 cgrid((d.S + 31) / 32, d.M, d.N);
-    msda_gv_combine<<<cgrid, 256, 0, st>>>(scratch, wtab, geo, d.S, d.M, gv);
-  }
+  const dim3 grid(geo.nty * geo.ntx, d.M, d.N);
+  msda_bwd_f32_tiled<LT, FUSED><<<grid, kBwdThreads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
 }
 
-// the register budget follows the block size: <= 512 threads get 2 waves/SIMD worth, 768 three, 1024 four
-template <int P, int LT, bool FUSED>
-void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                  const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                  hipStream_t st, float* scratch = nullptr, int* wtab = nullptr) {
-  if (threads <= 512)
-    launch_tiled_t<P, LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st, scratch, wtab);
-  else if (threads <= 768)
-    launch_tiled_t<P, LT, FUSED, 768>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st, scratch, wtab);
-  else
-    launch_tiled_t<P, LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st, scratch, wtab);
+template <bool FUSED>
+void launch_tiled_levels(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                         const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, hipStream_t st) {
+  switch (d.L) {
+    case 1: launch_tiled<1, FUSED>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st); break;
+    case 2: launch_tiled<2, FUSED>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st); break;
+    case 3: launch_tiled<3, FUSED>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st); break;
+    default: launch_tiled<4, FUSED>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st); break;
+  }
 }
 
 bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,
@@ -1036,9 +909,8 @@ bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, c
   if (env_int("M2F_MSDA_BWD_TILED", 1) == 0) return false;
   TileGeom geo;
   size_t lds;
-  int threads;
-  if (!make_tile_geom(d, host_shapes, geo, lds, threads)) return false;
-  launch_tiled<4, 0, false>(value, loc, attn, FrontEnd{}, gout, geo, lds, threads, d, gv, gl, ga, st);
+  if (!make_tile_geom(d, host_shapes, geo, lds)) return false;
+  launch_tiled_levels<false>(value, loc, attn, FrontEnd{}, gout, geo, lds, d, gv, gl, ga, st);
   return true;
 }
 
@@ -1201,15 +1073,6 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
   return m2f::check_launch(fn);
 }
 
-namespace {
-// scratch partial rows (wrows x 32 fp32 per workgroup) + window tables, 256-byte aligned pieces
-void fused_ws_layout(const Dims& d, const TileGeom& geo, int64_t& scratch_bytes, int64_t& total) {
-  const int64_t nwg = static_cast<int64_t>(geo.nty) * geo.ntx * d.M * d.N;
-  scratch_bytes = (nwg * geo.wrows * 32 * 4 + 255) / 256 * 256;
-  total = scratch_bytes + (nwg * kWtab * 4 + 255) / 256 * 256;
-}
-}  // namespace
-
 extern "C" int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, int batch, int spatial_size,
                                             int num_heads, int channels, int num_levels, int num_point,
                                             int64_t* workspace_bytes) {
@@ -1218,12 +1081,9 @@ extern "C" int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, 
   if (!host_spatial_shapes || !workspace_bytes) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
   TileGeom geo;
   size_t lds;
-  int threads;
-  if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
+  if (!make_tile_geom(d, host_spatial_shapes, geo, lds))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout", fn);
-  int64_t sb, total;
-  fused_ws_layout(d, geo, sb, total);
-  *workspace_bytes = total;
+  *workspace_bytes = 0;  // the backward needs no workspace (kept for ABI stability)
   return m2f::ok();
 }
 
@@ -1242,30 +1102,15 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
     return m2f::fail(M2F_EINVAL, "%s: bad gradient pointer", fn);
   TileGeom geo;
   size_t lds;
-  int threads;
-  if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
+  if (!make_tile_geom(d, host_spatial_shapes, geo, lds))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout (num_query == spatial_size)", fn);
-  float* scratch = nullptr;
-  int* wtab = nullptr;
-  if (workspace) {  // partial rows + combine pass (no flush atomics); without a workspace: atomic flush
-    int64_t sb, total;
-    fused_ws_layout(d, geo, sb, total);
-    if (workspace_bytes < total || !m2f::aligned(workspace, 16))
-      return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld bytes", fn, static_cast<long long>(workspace_bytes),
-                       static_cast<long long>(total));
-    scratch = static_cast<float*>(workspace);
-    wtab = reinterpret_cast<int*>(static_cast<char*>(workspace) + sb);
-  }
+  (void)workspace;
+  (void)workspace_bytes;
   hipStream_t st = static_cast<hipStream_t>(stream);
   const size_t gv_bytes = static_cast<size_t>(d.N) * d.S * d.M * d.D * sizeof(float);
   hipError_t e = hipMemsetAsync(grad_value, 0, gv_bytes, st);
   if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
   const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
-  switch (d.L) {
-    case 1: launch_tiled<4, 1, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st, scratch, wtab); break;
-    case 2: launch_tiled<4, 2, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st, scratch, wtab); break;
-    case 3: launch_tiled<4, 3, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st, scratch, wtab); break;
-    default: launch_tiled<4, 4, true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj, nullptr, st, scratch, wtab); break;
-  }
+  launch_tiled_levels<true>(value, nullptr, nullptr, fe, grad_output, geo, lds, d, grad_value, grad_proj, nullptr, st);
   return m2f::check_launch(fn);
 }

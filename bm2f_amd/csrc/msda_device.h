@@ -55,16 +55,9 @@ struct TileGeom {
   int L;
   int H[kTileMaxL], W[kTileMaxL], start[kTileMaxL];
   int nty, ntx;   // tile grid shared by all levels
-  int max_rows;   // window index space (rows = pixels of one head): list heads in LDS
+  int max_rows;   // list-head cells per workgroup (the window grid extended by one row / column)
   int max_halo;   // windows never extend more than this many pixels past the tile
   int max_qt;     // queries of the largest tile (sizes the LDS carve-up)
-  int bbox;       // 1: shrink the window to the bounding box of the touched corners (phase 0 pass)
-  int wrows;      // scratch rows per workgroup (>= any window) when partial rows go to a scratch buffer
-  int exact;      // 1: exact integer-valued f64 row sums (bitwise repeatable); 0: fp32 sums in list order
-  int head_major; // 1: grid (M, tiles, N): the head is the fastest block index, so each XCD (blocks are dealt
-                  // round-robin) owns one head's value / grad_value rows and neighbouring tiles' halos
-  int ablate;     // timing experiments only (M2F_MSDA_ABLATE): 1 no list inserts, 2 no phase 3, 4 no spill
-                  // atomics, 8 phase 3 without its HBM adds
 };
 
 __device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
@@ -76,8 +69,6 @@ __device__ __forceinline__ int tile_of(int y, int n, int nt) {
   while (t + 1 < nt && tile_lo(t + 1, n, nt) <= y) ++t;
   return t;
 }
-
-constexpr int kWtab = 24;  // window table ints per workgroup: (wy0, wx0, wh, ww, woff) x 4 levels, rows
 
 // Sum over each aligned group of 8 lanes with DPP moves (VALU, no LDS crossbar): xor 1, xor 2 within
 // quads, then row_half_mirror (lane i <-> 7-i) pairs the two quads.

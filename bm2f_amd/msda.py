@@ -202,18 +202,9 @@ class MSDeformAttnFusedFunction(Function):
         hs = _host_shape_buffer(host_shapes)
         grad_value = torch.empty_like(value)
         grad_proj = torch.empty((N, S, M * L * n_points * 3), dtype=proj.dtype, device=proj.device)
-        ws = None
-        # partial rows + ordered combine pass instead of the atomic flush: deterministic, but measured slower
-        # at config 2 (4.57 vs 4.19 ms: 3.2 GB of plain scratch traffic against the L2-resident atomics)
-        if os.environ.get("M2F_MSDA_SCRATCH", "0") != "0":
-            wsb = ctypes.c_int64(0)
-            _native.call("m2f_msda_fused_bwd_workspace", ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, n_points,
-                         ctypes.byref(wsb))
-            ws = torch.empty(max(wsb.value, 16), dtype=torch.uint8, device=value.device)
         _native.call("m2f_msda_fused_bwd_f32", _ptr(value), _ptr(proj), proj.stride(1), _ptr(ref), ref.stride(0),
                      ctypes.cast(hs, ctypes.c_void_p), _ptr(grad_out), N, S, M, D, L, S, n_points, _ptr(grad_value),
-                     _ptr(grad_proj), _ptr(ws) if ws is not None else None,
-                     ctypes.c_int64(ws.numel() if ws is not None else 0), _stream(value.device))
+                     _ptr(grad_proj), None, ctypes.c_int64(0), _stream(value.device))
         return grad_value, grad_proj, None, None, None
 
 

@@ -6,11 +6,14 @@ replaced by the oracle's CPU restatement of the reference algorithm: MSDA throug
 ops/modules/ms_deform_attn.py:116-121), and the decoder's mask/attention ops through
 oracle.decoder_ref (F.interpolate + sigmoid threshold, MultiheadAttention math with a bool mask).
 This is the reference's CPU forward/backward, fp32, as SURVEY §6 timed it in the survey container.
+
+Sampling follows BASELINE.md §3: config 1 (1 x 512^2) and one 1024^2 image, warm-up 1, median of 3.
 """
 from __future__ import annotations
 
 import contextlib
 import os
+import statistics
 import time
 
 import torch
@@ -42,11 +45,38 @@ def reference_cpu_ops():
         msda.MSDeformAttnFunction.apply, decoder_ops.attn_mask_bits, decoder_ops.masked_attention = saved
 
 
-def time_cpu_step(res=1024, images=1, steps=2, threads=None, seed=0):
-    """Seconds per fwd+bwd step of `images` images at res x res on the host (fp32, reference CPU path)."""
+def cpu_threads():
+    """Threads for the CPU leg: os.cpu_count(), capped by the CPU share this process may use (its affinity
+    mask and OMP_NUM_THREADS: a GPU box exposes the whole machine's CPUs but grants one GPU's share)."""
+    n = os.cpu_count() or 1
+    try:
+        n = min(n, len(os.sched_getaffinity(0)))
+    except (AttributeError, OSError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def time_cpu_step(res=1024, images=1, steps=3, warmup=1, threads=None, seed=0):
+    """Median seconds per fwd+bwd step of `images` images at res x res on the host (fp32, reference CPU
+    path), after `warmup` untimed steps.  Returns (median_s, threads, all_times)."""
     from bm2f_amd.bench_model import MaskFormerR50, surrogate_loss
 
-    threads = threads or min(16, os.cpu_count() or 1)
+    threads = threads or cpu_threads()
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
     try:
@@ -55,12 +85,13 @@ def time_cpu_step(res=1024, images=1, steps=2, threads=None, seed=0):
         x = torch.randn(images, 3, res, res) * 57.0 + 117.0
         times = []
         with reference_cpu_ops():
-            for _ in range(steps):
+            for i in range(warmup + steps):
                 t0 = time.perf_counter()
                 model.zero_grad(set_to_none=True)
                 loss = surrogate_loss(model(x))
                 loss.backward()
-                times.append(time.perf_counter() - t0)
-        return min(times), threads
+                if i >= warmup:
+                    times.append(time.perf_counter() - t0)
+        return statistics.median(times), threads, times
     finally:
         torch.set_num_threads(prev)

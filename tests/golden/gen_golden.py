@@ -254,11 +254,13 @@ DEC_PARAM_GRADS = [
 ]
 
 
-def gen_decoder(ref, out):
+def gen_decoder(ref, out, num_queries=100, num_classes=133, name="decoder.npz", amp=None):
+    """amp: None (fp32) or torch.float16 -- the reference's training precision (SOLVER.AMP.ENABLED), run
+    under CPU autocast here."""
     torch.manual_seed(0)
     dec = ref.dec.MultiScaleMaskedTransformerDecoder(
-        256, True, num_classes=133, hidden_dim=256, num_queries=100, nheads=8, dim_feedforward=2048, dec_layers=9,
-        pre_norm=False, mask_dim=256, enforce_input_project=False)
+        256, True, num_classes=num_classes, hidden_dim=256, num_queries=num_queries, nheads=8, dim_feedforward=2048,
+        dec_layers=9, pre_norm=False, mask_dim=256, enforce_input_project=False)
     fill_module(dec)
     dec.train()
     gen = torch.Generator().manual_seed(5)
@@ -266,7 +268,8 @@ def gen_decoder(ref, out):
     x = [torch.randn(B, 256, s, s, generator=gen).requires_grad_() for s in (2, 4, 8)]
     mf = torch.randn(B, 256, 16, 16, generator=gen).requires_grad_()
     captured, handles = _capture_masks(dec)
-    o = dec(x, mf)
+    with torch.autocast("cpu", dtype=amp or torch.float32, enabled=amp is not None):
+        o = dec(x, mf)
     for h in handles:
         h.remove()
     logits = [a["pred_logits"] for a in o["aux_outputs"]] + [o["pred_logits"]]
@@ -278,8 +281,8 @@ def gen_decoder(ref, out):
     res["in_mask_features"] = npf(mf)
     res.update({f"ingrad_x{i}": npf(t.grad) for i, t in enumerate(x)})
     res["ingrad_mask_features"] = npf(mf.grad)
-    res["pred_logits"] = np.stack([npf(t) for t in logits])
-    res["pred_masks"] = np.stack([npf(t) for t in masks])
+    res["pred_logits"] = np.stack([npf(t.float()) for t in logits])
+    res["pred_masks"] = np.stack([npf(t.float()) for t in masks])
     # attn_mask handed to cross-attn layer i, (B*h, Q, HW) bool; heads are identical copies -> keep head 0
     for i, mk in enumerate(captured):
         bq = mk.view(B, 8, mk.shape[1], mk.shape[2])
@@ -287,21 +290,30 @@ def gen_decoder(ref, out):
         res[f"attn_mask{i}"] = npf(bq[:, 0])
     res.update({f"pgrad_{k}": npf(pnames[k].grad) for k in DEC_PARAM_GRADS})
     res["state_dict_keys"] = np.array(sorted(dec.state_dict().keys()))
-    np.savez_compressed(os.path.join(out, "decoder.npz"), **res)
+    np.savez_compressed(os.path.join(out, name), **res)
 
 
-def gen_video_decoder(ref, out):
+def gen_decoder_q200(ref, out):
+    """Config 4's decoder shape (COCO instance, Swin-L: Q=200, K=80), reduced spatial size."""
+    gen_decoder(ref, out, num_queries=200, num_classes=80, name="decoder_q200.npz")
+
+
+def gen_decoder_amp16(ref, out):
+    """The decoder under fp16 autocast, the reference's training precision."""
+    gen_decoder(ref, out, name="decoder_amp16.npz", amp=torch.float16)
+
+
+def gen_video_decoder(ref, out, T=3, B=1, num_queries=20, levels=((2, 3), (4, 5), (8, 9)), mf_hw=(16, 18),
+                      name="video_decoder.npz"):
     torch.manual_seed(0)
-    T = 3
     dec = ref.vdec.VideoMultiScaleMaskedTransformerDecoder(
-        256, True, num_classes=40, hidden_dim=256, num_queries=20, nheads=8, dim_feedforward=2048, dec_layers=9,
-        pre_norm=False, mask_dim=256, enforce_input_project=False, num_frames=T)
+        256, True, num_classes=40, hidden_dim=256, num_queries=num_queries, nheads=8, dim_feedforward=2048,
+        dec_layers=9, pre_norm=False, mask_dim=256, enforce_input_project=False, num_frames=T)
     fill_module(dec)
     dec.train()
     gen = torch.Generator().manual_seed(9)
-    B = 1
-    x = [torch.randn(B * T, 256, s, s + 1, generator=gen).requires_grad_() for s in (2, 4, 8)]
-    mf = torch.randn(B * T, 256, 16, 18, generator=gen).requires_grad_()
+    x = [torch.randn(B * T, 256, h, w, generator=gen).requires_grad_() for h, w in levels]
+    mf = torch.randn(B * T, 256, *mf_hw, generator=gen).requires_grad_()
     captured, handles = _capture_masks(dec)
     o = dec(x, mf)
     for h in handles:
@@ -320,7 +332,14 @@ def gen_video_decoder(ref, out):
         bq = mk.view(B, 8, mk.shape[1], mk.shape[2])
         res[f"attn_mask{i}"] = npf(bq[:, 0])
     res["state_dict_keys"] = np.array(sorted(dec.state_dict().keys()))
-    np.savez_compressed(os.path.join(out, "video_decoder.npz"), **res)
+    np.savez_compressed(os.path.join(out, name), **res)
+
+
+def gen_video_decoder_t5(ref, out):
+    """Config 5's clip layout (youtubevis_2019: T=5 frames, 384x640 -> a non-square 3:5 pyramid) at 1/4 of its
+    spatial size: levels 3x5 / 6x10 / 12x20, mask features 12x20; one clip, Q=20 (fixture size)."""
+    gen_video_decoder(ref, out, T=5, B=1, num_queries=20, levels=((3, 5), (6, 10), (12, 20)), mf_hw=(12, 20),
+                      name="video_decoder_t5.npz")
 
 
 def main():
@@ -331,7 +350,8 @@ def main():
     args = ap.parse_args()
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = import_reference(args.ref)
-    for fn in (gen_msda_testpy, gen_msda_slice, gen_pixdec, gen_decoder, gen_video_decoder):
+    for fn in (gen_msda_testpy, gen_msda_slice, gen_pixdec, gen_decoder, gen_decoder_q200, gen_decoder_amp16,
+               gen_video_decoder, gen_video_decoder_t5):
         if args.only and args.only not in fn.__name__:
             continue
         fn(ref, args.out)

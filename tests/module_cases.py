@@ -28,12 +28,21 @@ def build_decoder(num_queries=100, num_classes=133):
     return fill_module(d).train()
 
 
-def build_video_decoder(T=3):
+def build_video_decoder(T=3, num_queries=20):
     from bm2f_amd.video_decoder import VideoMultiScaleMaskedTransformerDecoder
-    d = VideoMultiScaleMaskedTransformerDecoder(256, True, num_classes=40, hidden_dim=256, num_queries=20, nheads=8,
-                                                dim_feedforward=2048, dec_layers=9, pre_norm=False, mask_dim=256,
-                                                enforce_input_project=False, num_frames=T)
+    d = VideoMultiScaleMaskedTransformerDecoder(256, True, num_classes=40, hidden_dim=256, num_queries=num_queries,
+                                                nheads=8, dim_feedforward=2048, dec_layers=9, pre_norm=False,
+                                                mask_dim=256, enforce_input_project=False, num_frames=T)
     return fill_module(d).train()
+
+
+# decoder fixtures (tests/golden/gen_golden.py): name -> (builder, video)
+DECODER_CASES = {
+    "decoder.npz": (lambda: build_decoder(), False),
+    "decoder_q200.npz": (lambda: build_decoder(num_queries=200, num_classes=80), False),     # config 4 shape
+    "video_decoder.npz": (lambda: build_video_decoder(T=3), True),
+    "video_decoder_t5.npz": (lambda: build_video_decoder(T=5), True),                        # config 5 layout
+}
 
 
 @contextlib.contextmanager

@@ -40,11 +40,12 @@ def test_pixdec_forward_backward_cpu():
             assert rel_err(params[key[6:]].grad, g[key]) < 1e-4, key
 
 
-@pytest.mark.parametrize("fixture,video", [("decoder.npz", False), ("video_decoder.npz", True)])
-def test_decoder_forward_backward_cpu(fixture, video):
-    from module_cases import run_decoder
+@pytest.mark.parametrize("fixture", ["decoder.npz", "decoder_q200.npz", "video_decoder.npz", "video_decoder_t5.npz"])
+def test_decoder_forward_backward_cpu(fixture):
+    from module_cases import DECODER_CASES, run_decoder
     from oracle.decoder_ref import torch_decoder_ops, unpack_bits
-    d = build_video_decoder() if video else build_decoder()
+    build, video = DECODER_CASES[fixture]
+    d = build()
     with torch_decoder_ops():
         g, x, mf, logits, masks, captured = run_decoder(d, torch.device("cpu"), fixture, video)
     assert rel_err(torch.stack([t.detach() for t in logits]), g["pred_logits"]) < 1e-4

@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden
+from conftest import golden, loc_crossing_mask
 from oracle import msda_ref
 
 pytestmark = pytest.mark.gpu
@@ -183,14 +183,16 @@ def _pyramid_case(shapes, N, M, far_frac, seed):
     return value, st, lsi, loc.contiguous(), attn, gout
 
 
-@pytest.mark.parametrize("tile,rows,halo,threads", [(16, 2048, 8, 1024), (12, 2048, 8, 768), (8, 480, 8, 512),
-                                                     (4, 64, 2, 256), (8, 200, 0, 1024), (6, 2048, 12, 320)])
-def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, threads):
+@pytest.mark.parametrize("tile,rows,halo", [(16, 2304, 8), (12, 2304, 8), (8, 480, 8), (4, 64, 2), (8, 200, 0),
+                                           (6, 2304, 12), (16, 700, 8)])
+def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo):
+    """The tiled backward over tile / cell-budget / halo geometries (M2F_MSDA_*: geometry only), on a
+    non-square pyramid whose tiles do not divide every level evenly, 5 % of the samples thrown far (the
+    direct-atomic path), against the C oracle and the untiled kernel."""
     from bm2f_amd import msda
     monkeypatch.setenv("M2F_MSDA_TILE", str(tile))
     monkeypatch.setenv("M2F_MSDA_WIN_ROWS", str(rows))
     monkeypatch.setenv("M2F_MSDA_HALO", str(halo))
-    monkeypatch.setenv("M2F_MSDA_THREADS", str(threads))
     shapes = [(6, 10), (12, 20), (24, 40)]   # non-square, tiles not dividing every level evenly
     value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 2, 8, 0.05, tile + rows)
     dst = msda.attach_host_shapes(st.to(device), shapes)
@@ -199,7 +201,9 @@ def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, threads
     wv, wl, wa = msda_ref.msda_backward(value.double(), st, lsi, loc.double(), attn.double(), gout.double())
     _close(gv.cpu(), wv)
     _close(ga.cpu(), wa)
-    _close(gl.cpu(), wl, atol_frac=1e-4)
+    amb = loc_crossing_mask(loc, shapes)
+    assert amb.mean() < 2e-3
+    _close(np.where(amb, 0.0, gl.cpu().numpy()), np.where(amb, 0.0, wl), atol_frac=1e-4)
     # identical to the untiled kernel up to summation order
     monkeypatch.setenv("M2F_MSDA_BWD_TILED", "0")
     gv2, gl2, ga2 = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
@@ -263,42 +267,3 @@ def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5)
     for a, b in zip(grads[0], grads[1]):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * max(b.abs().max().item(), 1e-6))
-
-
-@pytest.mark.parametrize("shapes,halo", [([(4, 4), (8, 8), (16, 16)], 8), ([(6, 10), (12, 20), (24, 40)], 3),
-                                         ([(16, 16), (32, 32), (64, 64)], 8)])
-def test_fused_backward_scratch_combine(device, monkeypatch, shapes, halo):
-    """Partial rows in scratch + the ordered combine pass == the atomic flush, and bitwise repeatable when
-    every sample lands in a window (halo 8 here; with halo 3 some go through fp32 atomics)."""
-    from bm2f_amd.msda import MSDeformAttn, attach_host_shapes
-    monkeypatch.setenv("M2F_MSDA_HALO", str(halo))
-    monkeypatch.setenv("M2F_MSDA_DETERMINISTIC", "1")   # exact row sums: bitwise repeatable
-    torch.manual_seed(1)
-    L = len(shapes)
-    m = MSDeformAttn(256, L, 8, 4).to(device)
-    with torch.no_grad():
-        m.sampling_offsets.weight.normal_(0, 0.05)
-        m.attention_weights.weight.normal_(0, 0.05)
-    st = torch.tensor(shapes, dtype=torch.int64, device=device)
-    attach_host_shapes(st, shapes)
-    lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
-    S = int(st.prod(1).sum())
-    refs = []
-    for h, w in shapes:
-        ys, xs = torch.meshgrid(torch.linspace(0.5, h - 0.5, h), torch.linspace(0.5, w - 0.5, w), indexing="ij")
-        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
-    ref = torch.cat(refs, 0).to(device)[None, :, None, :].expand(2, S, L, 2)
-    src = torch.randn(2, S, 256, device=device)
-    grads = []
-    for scratch in ("1", "1", "0"):
-        monkeypatch.setenv("M2F_MSDA_SCRATCH", scratch)
-        m.zero_grad()
-        x = src.clone().requires_grad_()
-        out = m(x, ref, x, st, lsi)
-        out.backward(torch.ones_like(out) * 0.01 + out.detach() * 0.1)
-        grads.append([x.grad.clone()] + [p.grad.clone() for p in m.parameters()])
-    if halo == 8:
-        for a, b in zip(grads[0], grads[1]):
-            assert torch.equal(a, b)
-    for a, b in zip(grads[0], grads[2]):
-        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * max(b.abs().max().item(), 1e-6))
