@@ -281,21 +281,24 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 //
 // grad_value is a scatter: every (query, sample, corner) adds w_c * a * g[query] (32 channels) to one
 // pixel row.  Here it becomes a gather inside the workgroup:
-//   phase 0  one lane per query derives its L*P samples ONCE (softmax and ref + offset / (W, H) on the
-//            fused path, or the given loc / attn) into a 12-byte descriptor {h, w, a} per sample in LDS
-//            (h = loc_y * H - 0.5 ...; h = w = -2 when the sample lies outside (-1, H) x (-1, W)), stages
-//            the tile's grad_output rows (this head) in LDS and takes the bounding box of the touched
-//            corners per level.  The window = that box clipped to the tile +- halo.
+//   phase 0  one lane per (query, level) derives that level's P samples ONCE (softmax and ref + offset /
+//            (W, H) on the fused path, or the given loc / attn) into a 12-byte descriptor {h, w, a} per
+//            sample in LDS (h = loc_y * H - 0.5 ...; h = w = -2 when the sample lies outside (-1, H) x
+//            (-1, W)), stages the tile's grad_output rows (this head) in LDS and takes the bounding box of
+//            the touched corners per level.  The window = that box clipped to the tile +- halo.
+//   phase 1  counting sort of the samples by the window cell of their 2x2 corner block (the window grid
+//            extended by one row / column up and left): an LDS counter per cell (returning adds give each
+//            sample its rank), a block-wide exclusive scan, and one u16 sample id per slot.  Samples whose
+//            corners leave the window are flagged instead.
 //   phase 2  an 8-lane group per query (float4 of channels per lane) gathers each sample's 4 corner rows,
-//            writes grad_loc / grad_attn (channel sums by DPP), and pushes the sample id onto the list of
-//            its top-left corner's cell in the window (one LDS exchange per sample: the 2x2 corner block of
-//            a sample is one cell of the window grid extended by one row / column up and left).  Samples
-//            whose corners leave the window add their 4 corner rows with direct fp32 atomics.
-//   phase 3  a 4-lane group per window pixel walks the 4 lists whose cells cover it ((y,x) -> corner 1 of
-//            cell (y,x), corner 2 of (y,x-1), corner 3 of (y-1,x), corner 4 of (y-1,x-1)), accumulating
-//            w_c * a * g[query] in fp32 from the LDS descriptors and g rows (8 channels per lane), then adds
-//            the row to HBM once with row-contiguous fp32 atomics (two 128-B rows per instruction).
-// Summation order (list order, atomics across workgroups) is not fixed, as in the reference's atomics.
+//            forms the 4 per-corner channel dots with g, reduces them by DPP and writes grad_loc /
+//            grad_attn from those four sums.  Flagged samples add their 4 corner rows with fp32 atomics.
+//   phase 3  a 4-lane group per window pixel reads the 4 slot ranges whose cells cover it ((y,x) ->
+//            corner 1 of cell (y,x), corner 2 of (y,x-1), corner 3 of (y-1,x), corner 4 of (y-1,x-1)),
+//            accumulating w_c * a * g[query] in fp32 from the LDS descriptors and g rows (8 channels per
+//            lane); the wave's 16 rows are transposed through LDS so that each fp32 atomic instruction adds
+//            two whole 128-B rows to HBM.
+// Summation order (slot order, atomics across workgroups) is not fixed, as in the reference's atomics.
 // grad_loc / grad_attn (or d offset / d logit) are owned per (q, m) and written once.
 //
 // FUSED = true: the samples come from the raw projection (offsets | logits) and the reference points, and
@@ -305,6 +308,9 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // ------------------------------------------------------------------------------------------------
 constexpr int kWalkLanes = 4;   // phase-3 lanes per window pixel (8 channels each)
 constexpr int kBwdThreads = 1024;
+constexpr int kBwdWaves = kBwdThreads / 64;
+constexpr int kSortPerThread = 6;  // samples per thread in the counting sort: max_qt * L * P <= 6 * 1024
+constexpr int kStageFloats = 16 * 32 + 16;  // per wave: 16 rows x 32 channels + 16 row offsets
 
 struct TileState {
   int bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
@@ -312,6 +318,8 @@ struct TileState {
   int roff[kTileMaxL + 1];   // window pixel offsets per level
   int coff[kTileMaxL + 1];   // extended-cell offsets per level ((wh+1) x (ww+1) cells)
   int qc[kTileMaxL + 1], qy0[kTileMaxL], qx0[kTileMaxL], qw[kTileMaxL];
+  int wsum[kBwdWaves];       // block scan
+  int next_batch;            // phase-3 row batches handed out dynamically
 };
 
 // Fused-front-end inputs (raw projection + reference points).
@@ -329,26 +337,61 @@ __device__ __forceinline__ int tile_query(const TileState& ts, const TileGeom& g
   return geo.start[lq] + (ts.qy0[lq] + r / ts.qw[lq]) * geo.W[lq] + ts.qx0[lq] + r % ts.qw[lq];
 }
 
-template <int LT, bool FUSED>
+__device__ __forceinline__ int wave_incl_scan(int v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(v, o);
+    v += lane >= o ? t : 0;
+  }
+  return v;
+}
+
+// window cell of a sample whose top-left corner is (h0, w0), or -1 when a corner inside the level lies
+// outside the window
+__device__ __forceinline__ int window_cell(const TileState& ts, int l, int h0, int w0, int H, int W) {
+  const int wy0 = ts.wy0[l], wx0 = ts.wx0[l], wh = ts.wh[l], ww = ts.ww[l];
+  const bool ry = (h0 < 0 || (h0 >= wy0 && h0 < wy0 + wh)) && (h0 + 1 > H - 1 || (h0 + 1 >= wy0 && h0 + 1 < wy0 + wh));
+  const bool rx = (w0 < 0 || (w0 >= wx0 && w0 < wx0 + ww)) && (w0 + 1 > W - 1 || (w0 + 1 >= wx0 && w0 + 1 < wx0 + ww));
+  return (wh > 0 && ry && rx) ? ts.coff[l] + (h0 - wy0 + 1) * (ww + 1) + (w0 - wx0 + 1) : -1;
+}
+
+// STAMP (diagnostic builds only, M2F_DIAG): s_memtime at the phase barriers of each workgroup into `stamps`;
+// NOFLUSH (diagnostic builds only): phase 3 without its HBM adds, to price them.
+template <int LT, bool FUSED, bool STAMP = false, bool NOFLUSH = false>
 __global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
-    float* __restrict__ gloc, float* __restrict__ gattn) {
+    float* __restrict__ gloc, float* __restrict__ gattn, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int D = 32, P = 4, LP = LT * P;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   __shared__ TileState ts;
+#define M2F_STAMP(k)                                                                                        \
+  if constexpr (STAMP) {                                                                                    \
+    if (threadIdx.x == 0)                                                                                   \
+      stamps[static_cast<int64_t>(blockIdx.x) * 8 + (k)] = __builtin_amdgcn_s_memtime();                     \
+  }
 
-  const int tile = blockIdx.x, m = blockIdx.y, n = blockIdx.z;
+  // XCD-aware order: blocks are dealt round-robin over the 8 XCDs (b, b+8, ... share one); remap so each
+  // XCD takes a contiguous run of (image, head) pairs, tile fastest, and its L2 holds one head's value
+  // rows (2.75 MB per 1024^2 image) instead of several (speed only: any placement computes the same)
+  const int ntiles = geo.nty * geo.ntx;
+  const int nwg = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tile = wg % ntiles, pm = wg / ntiles, m = pm % M, n = pm / M;
   const int ty = tile / geo.ntx, tx = tile - ty * geo.ntx;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nwaves = blockDim.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int rs = M * D;  // value row stride (elements); N*S*M*D < 2^31 is checked on the host
-  // LDS carve-up: g rows [max_qt][32] f32 | desc [max_qt * LP][3] f32 | nxt [max_qt * LP] u16 | head [max_cells] i32
+  const int nsamp_max = geo.max_qt * LP;
+  // LDS carve-up (16-byte aligned pieces): g rows [max_qt][32] | desc [max_qt * LP][3] | stage [waves][528]
+  //   | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32 | slots [max_qt * LP] u16
   float* gsh = reinterpret_cast<float*>(lds_raw);
   float* desc = gsh + geo.max_qt * D;
-  unsigned short* nxt = reinterpret_cast<unsigned short*>(desc + geo.max_qt * LP * 3);
-  int* head = reinterpret_cast<int*>(lds_raw + ((geo.max_qt * D + geo.max_qt * LP * 3) * 4 +
-                                                ((geo.max_qt * LP * 2 + 15) & ~15)));
+  float* stage = desc + ((nsamp_max * 3 + 3) & ~3);
+  int* cstart = reinterpret_cast<int*>(stage + kBwdWaves * kStageFloats);
+  unsigned* oow = reinterpret_cast<unsigned*>(cstart + ((geo.max_rows + 1 + 3) & ~3));
+  unsigned short* slots = reinterpret_cast<unsigned short*>(oow + (((nsamp_max + 31) / 32 + 3) & ~3));
 
+  M2F_STAMP(5)
   if (tid < LT) {
     const int l = tid;
     const int y0 = tile_lo(ty, geo.H[l], geo.nty), y1 = tile_lo(ty + 1, geo.H[l], geo.nty);
@@ -359,13 +402,17 @@ __global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
     ts.qc[l + 1] = (y1 - y0) * (x1 - x0);
     ts.bb[l][0] = 0x7fffffff; ts.bb[l][1] = -1; ts.bb[l][2] = 0x7fffffff; ts.bb[l][3] = -1;
   }
+  for (int i = tid; i < (nsamp_max + 31) / 32; i += blockDim.x) oow[i] = 0u;
+  if (tid == 0) ts.next_batch = kBwdWaves;
   __syncthreads();
   if (tid == 0) {
     ts.qc[0] = 0;
     for (int l = 0; l < LT; ++l) ts.qc[l + 1] += ts.qc[l];
   }
   __syncthreads();
+  M2F_STAMP(0)
   const int Qt = ts.qc[LT];
+  const int nsamp = Qt * LP;
 
   // ---- phase 0a: this head's grad_output rows of the tile's queries -> LDS (float4 per lane) --------
   for (int idx = tid; idx < Qt * 8; idx += blockDim.x) {
@@ -375,89 +422,85 @@ __global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
     *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = ld4(gout + pair * D + 4 * j);
   }
 
-  // ---- phase 0b: sample descriptors (one lane per query) and the touched-corner bounding boxes -------
+  // ---- phase 0b: sample descriptors (one lane per (query, level)) and the touched-corner boxes --------
   {
     int bmin_y[LT], bmax_y[LT], bmin_x[LT], bmax_x[LT];
 #pragma unroll
     for (int l = 0; l < LT; ++l) { bmin_y[l] = 0x7fffffff; bmax_y[l] = -1; bmin_x[l] = 0x7fffffff; bmax_x[l] = -1; }
-    for (int qi = tid; qi < ((Qt + 63) & ~63); qi += blockDim.x) {
-      if (qi < Qt) {
-        const int q = tile_query(ts, geo, qi);
-        const int64_t nq = static_cast<int64_t>(n) * S + q;
-        float av[LP], lx[LP], ly[LP];
-        if constexpr (FUSED) {
-          const float* prow = fe.proj + nq * fe.ld;
-          const float* lg = prow + M * LP * 2 + m * LP;
-          const float* of = prow + m * LP * 2;
-          const float* rrow = fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * LT * 2;
-          float mx = -INFINITY;
+    for (int t = tid; t < Qt * LT; t += blockDim.x) {
+      const int qi = t / LT, l = t - qi * LT;
+      const int q = tile_query(ts, geo, qi);
+      const int64_t nq = static_cast<int64_t>(n) * S + q;
+      const int H = geo.H[l], W = geo.W[l];
+      float av[P], lx[P], ly[P];
+      if constexpr (FUSED) {
+        const float* prow = fe.proj + nq * fe.ld;
+        const float* lg = prow + M * LP * 2 + m * LP;
+        float e[LP];
+        float mx = -INFINITY;
 #pragma unroll
-          for (int k = 0; k < LP; ++k) { av[k] = lg[k]; mx = fmaxf(mx, av[k]); }
-          float sum = 0.f;
+        for (int k = 0; k < LP; ++k) { e[k] = lg[k]; mx = fmaxf(mx, e[k]); }
+        float sum = 0.f;
 #pragma unroll
-          for (int k = 0; k < LP; ++k) { av[k] = expf(av[k] - mx); sum += av[k]; }
-          const float inv = 1.f / sum;
+        for (int k = 0; k < LP; ++k) sum += expf(e[k] - mx);
+        const float inv = 1.f / sum;
+        const float2 rf = *reinterpret_cast<const float2*>(fe.ref + n * fe.ref_bs + (static_cast<int64_t>(q) * LT + l) * 2);
+        const float* of = prow + (m * LP + l * P) * 2;
 #pragma unroll
-          for (int l = 0; l < LT; ++l) {
-            const float2 rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
-#pragma unroll
-            for (int p = 0; p < P; ++p) {
-              const float2 off = *reinterpret_cast<const float2*>(of + (l * P + p) * 2);
-              lx[l * P + p] = rf.x + off.x / static_cast<float>(geo.W[l]);
-              ly[l * P + p] = rf.y + off.y / static_cast<float>(geo.H[l]);
-              av[l * P + p] *= inv;
-            }
-          }
-        } else {
-          const int64_t pair = nq * M + m;
-#pragma unroll
-          for (int k = 0; k < LP; ++k) {
-            const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (pair * LP + k));
-            lx[k] = xy.x;
-            ly[k] = xy.y;
-            av[k] = attn[pair * LP + k];
-          }
+        for (int p = 0; p < P; ++p) {
+          const float2 off = *reinterpret_cast<const float2*>(of + 2 * p);
+          lx[p] = rf.x + off.x / static_cast<float>(W);
+          ly[p] = rf.y + off.y / static_cast<float>(H);
+          av[p] = expf(lg[l * P + p] - mx) * inv;
         }
-        float* dq = desc + qi * LP * 3;
+      } else {
+        const int64_t kb = (nq * M + m) * LP + l * P;
 #pragma unroll
-        for (int l = 0; l < LT; ++l) {
-          const int H = geo.H[l], W = geo.W[l];
-#pragma unroll
-          for (int p = 0; p < P; ++p) {
-            const int k = l * P + p;
-            float h = ly[k] * H - 0.5f, w = lx[k] * W - 0.5f;
-            const bool ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
-            h = ok ? h : -2.f;
-            w = ok ? w : -2.f;
-            dq[3 * k] = h;
-            dq[3 * k + 1] = w;
-            dq[3 * k + 2] = av[k];
-            if (ok) {
-              const int h0 = static_cast<int>(floorf(h)), w0 = static_cast<int>(floorf(w));
-              bmin_y[l] = min(bmin_y[l], max(h0, 0)); bmax_y[l] = max(bmax_y[l], min(h0 + 1, H - 1));
-              bmin_x[l] = min(bmin_x[l], max(w0, 0)); bmax_x[l] = max(bmax_x[l], min(w0 + 1, W - 1));
-            }
-          }
+        for (int p = 0; p < P; ++p) {
+          const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (kb + p));
+          lx[p] = xy.x;
+          ly[p] = xy.y;
+          av[p] = attn[kb + p];
         }
       }
+      float* dq = desc + (qi * LP + l * P) * 3;
 #pragma unroll
-      for (int l = 0; l < LT; ++l) {
+      for (int p = 0; p < P; ++p) {
+        float h = ly[p] * H - 0.5f, w = lx[p] * W - 0.5f;
+        const bool ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
+        h = ok ? h : -2.f;
+        w = ok ? w : -2.f;
+        dq[3 * p] = h;
+        dq[3 * p + 1] = w;
+        dq[3 * p + 2] = av[p];
+        if (ok) {
+          const int h0 = static_cast<int>(floorf(h)), w0 = static_cast<int>(floorf(w));
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          bmin_y[l] = min(bmin_y[l], __shfl_xor(bmin_y[l], o)); bmax_y[l] = max(bmax_y[l], __shfl_xor(bmax_y[l], o));
-          bmin_x[l] = min(bmin_x[l], __shfl_xor(bmin_x[l], o)); bmax_x[l] = max(bmax_x[l], __shfl_xor(bmax_x[l], o));
+          for (int ll = 0; ll < LT; ++ll)
+            if (ll == l) {
+              bmin_y[ll] = min(bmin_y[ll], max(h0, 0)); bmax_y[ll] = max(bmax_y[ll], min(h0 + 1, H - 1));
+              bmin_x[ll] = min(bmin_x[ll], max(w0, 0)); bmax_x[ll] = max(bmax_x[ll], min(w0 + 1, W - 1));
+            }
         }
       }
     }
-    if (lane == 0 && tid < ((Qt + 63) & ~63)) {
+    // per-level boxes over the wave, then over the workgroup
 #pragma unroll
-      for (int l = 0; l < LT; ++l) {
-        atomicMin(&ts.bb[l][0], bmin_y[l]); atomicMax(&ts.bb[l][1], bmax_y[l]);
-        atomicMin(&ts.bb[l][2], bmin_x[l]); atomicMax(&ts.bb[l][3], bmax_x[l]);
+    for (int l = 0; l < LT; ++l) {
+      int a0 = bmin_y[l], a1 = bmax_y[l], a2 = bmin_x[l], a3 = bmax_x[l];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        a0 = min(a0, __shfl_xor(a0, o)); a1 = max(a1, __shfl_xor(a1, o));
+        a2 = min(a2, __shfl_xor(a2, o)); a3 = max(a3, __shfl_xor(a3, o));
+      }
+      if (lane == 0 && a1 >= 0) {
+        atomicMin(&ts.bb[l][0], a0); atomicMax(&ts.bb[l][1], a1);
+        atomicMin(&ts.bb[l][2], a2); atomicMax(&ts.bb[l][3], a3);
       }
     }
   }
   __syncthreads();
+  M2F_STAMP(1)
 
   // ---- window: touched box clipped to the tile +- halo; the halo shrinks until the cells fit ----------
   if (tid == 0) {
@@ -488,14 +531,62 @@ __global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
   }
   __syncthreads();
   const int cells_total = ts.coff[LT];
-  for (int i = tid; i < cells_total; i += blockDim.x) head[i] = 0xffff;
+  for (int i = tid; i <= cells_total; i += blockDim.x) cstart[i] = 0;
   __syncthreads();
 
-  // ---- phase 2: gather, grad_loc / grad_attn, list pushes -----------------------------------------------
+  // ---- phase 1: counting sort of the in-window samples by cell ------------------------------------------
+  {
+    int cell[kSortPerThread], rank[kSortPerThread];
+#pragma unroll
+    for (int r = 0; r < kSortPerThread; ++r) {
+      const int sid = tid + r * kBwdThreads;
+      cell[r] = -1;
+      if (sid < nsamp) {
+        const float h = desc[3 * sid], w = desc[3 * sid + 1];
+        if (h > -1.f) {  // ok sample
+          const int l = (sid % LP) / P;
+          const int c = window_cell(ts, l, static_cast<int>(floorf(h)), static_cast<int>(floorf(w)), geo.H[l], geo.W[l]);
+          if (c >= 0) {
+            cell[r] = c;
+            rank[r] = atomicAdd(cstart + c, 1);
+          } else {
+            atomicOr(oow + (sid >> 5), 1u << (sid & 31));
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // exclusive scan of cstart[0 .. cells_total] (cstart[cells_total] = 0 -> total)
+    const int per = (cells_total + 1 + kBwdThreads - 1) / kBwdThreads;
+    const int c0 = tid * per;
+    int run = 0;
+    for (int i = 0; i < per; ++i) run += (c0 + i <= cells_total) ? cstart[c0 + i] : 0;
+    const int incl = wave_incl_scan(run, lane);
+    if (lane == 63) ts.wsum[wid] = incl;
+    __syncthreads();
+    int wbase = 0;
+    for (int w = 0; w < wid; ++w) wbase += ts.wsum[w];
+    int acc = wbase + incl - run;
+    for (int i = 0; i < per; ++i) {
+      if (c0 + i <= cells_total) {
+        const int v = cstart[c0 + i];
+        cstart[c0 + i] = acc;
+        acc += v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kSortPerThread; ++r)
+      if (cell[r] >= 0) slots[cstart[cell[r]] + rank[r]] = static_cast<unsigned short>(tid + r * kBwdThreads);
+  }
+  __syncthreads();
+  M2F_STAMP(2)
+
+  // ---- phase 2: gather, grad_loc / grad_attn; out-of-window samples scatter with atomics ---------------
   {
     const int j = lane & 7, gq = lane >> 3;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
-    for (int base = wid * 8; base < Qt; base += nwaves * 8) {
+    for (int base = wid * 8; base < Qt; base += kBwdWaves * 8) {
       const int qi = base + gq;
       if (qi >= Qt) continue;  // whole lane group (same qi) idles together
       const int q = tile_query(ts, geo, qi);
@@ -507,7 +598,6 @@ __global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
       for (int l = 0; l < LT; ++l) {
         const int H = geo.H[l], W = geo.W[l];
         const int lbase = ((n * S + geo.start[l]) * M + m) * D + 4 * j;
-        const int wy0 = ts.wy0[l], wx0 = ts.wx0[l], wh = ts.wh[l], ww = ts.ww[l], coff = ts.coff[l];
         float st_l = 0.f, st_a = 0.f;
         // points in batches of PB: every corner load of a batch is issued before any of its math
         constexpr int PB = 2;
@@ -540,14 +630,18 @@ __global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
             const float hy = 1.f - ly, hx = 1.f - lx;
             const bool c1 = h0 >= 0 && w0 >= 0, c2 = h0 >= 0 && w0 + 1 <= W - 1;
             const bool c3 = h0 + 1 <= H - 1 && w0 >= 0, c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
-            const f4 v1 = c1 ? vb[pp][0] : z, v2 = c2 ? vb[pp][1] : z, v3 = c3 ? vb[pp][2] : z, v4 = c4 ? vb[pp][3] : z;
-            const f4 val = (hy * hx) * v1 + (hy * lx) * v2 + (ly * hx) * v3 + (ly * lx) * v4;
-            const f4 gw = hy * (v2 - v1) + ly * (v4 - v3);
-            const f4 gh = hx * (v3 - v1) + lx * (v4 - v2);
-            const f4 ta = g * val, tx2 = g * gw, ty2 = g * gh;
-            const float pa = sum8_dpp(ta.x + ta.y + ta.z + ta.w);
-            const float px = sum8_dpp(tx2.x + tx2.y + tx2.z + tx2.w) * a;
-            const float py = sum8_dpp(ty2.x + ty2.y + ty2.z + ty2.w) * a;
+            // per-corner channel dots with g, summed over the group; everything else is scalar.  Corners
+            // outside the level are zeroed by a select on the loaded rows (branch-free: a branch here makes
+            // the compiler sink the load into it and wait for it alone)
+            const f4 t1 = g * (c1 ? vb[pp][0] : z), t2 = g * (c2 ? vb[pp][1] : z);
+            const f4 t3 = g * (c3 ? vb[pp][2] : z), t4 = g * (c4 ? vb[pp][3] : z);
+            const float d1 = sum8_dpp(t1.x + t1.y + t1.z + t1.w);
+            const float d2 = sum8_dpp(t2.x + t2.y + t2.z + t2.w);
+            const float d3 = sum8_dpp(t3.x + t3.y + t3.z + t3.w);
+            const float d4 = sum8_dpp(t4.x + t4.y + t4.z + t4.w);
+            const float pa = (hy * hx) * d1 + (hy * lx) * d2 + (ly * hx) * d3 + (ly * lx) * d4;
+            const float px = a * (hy * (d2 - d1) + ly * (d4 - d3));
+            const float py = a * (hx * (d3 - d1) + lx * (d4 - d2));
             // lane p stores grad_attn of point p; lanes 2p, 2p+1 its grad_loc pair (one store per level)
             if constexpr (FUSED) {
               const float gak = ok ? pa : 0.f;
@@ -559,20 +653,8 @@ __global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
               if (j == p) st_a = ok ? pa : 0.f;
               if ((j >> 1) == p) st_l = ok ? ((j & 1) ? H * py : W * px) : 0.f;
             }
-            if (!ok) continue;
-            // the sample's 2x2 corner block as one cell of the window grid (extended one row / column up
-            // and left): in the window when every corner inside the level lies inside the window
-            const bool ry = (h0 < 0 || (h0 >= wy0 && h0 < wy0 + wh)) &&
-                            (h0 + 1 > H - 1 || (h0 + 1 >= wy0 && h0 + 1 < wy0 + wh));
-            const bool rx = (w0 < 0 || (w0 >= wx0 && w0 < wx0 + ww)) &&
-                            (w0 + 1 > W - 1 || (w0 + 1 >= wx0 && w0 + 1 < wx0 + ww));
-            if (wh > 0 && ry && rx) {
-              if (j == 0) {
-                const int cell = coff + (h0 - wy0 + 1) * (ww + 1) + (w0 - wx0 + 1);
-                const int sid = qi * LP + k;
-                nxt[sid] = static_cast<unsigned short>(atomicExch(head + cell, sid));
-              }
-            } else {
+            const int sid = qi * LP + k;
+            if (ok && ((oow[sid >> 5] >> (sid & 31)) & 1u)) {
               // outside the window: the 4 corner rows go straight to HBM (fp32 atomics, as the reference)
               const f4 tg = g * a;
               const int o1 = lbase + (min(max(h0, 0), H - 1) * W + min(max(w0, 0), W - 1)) * rs;
@@ -603,72 +685,104 @@ __global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
     }
   }
   __syncthreads();
+  M2F_STAMP(3)
 
-  // ---- phase 3: per window pixel, walk the 4 covering lists; one row-contiguous atomic add per row -------
+  // ---- phase 3: per window pixel, the 4 covering slot ranges; one row-contiguous atomic add per row -----
   {
     constexpr int LPR = kWalkLanes, CPL = D / LPR, RPW = 64 / LPR;  // lanes per row, channels per lane, rows per wave
     const int rows_total = ts.roff[LT];
-    const int jl = lane % LPR;
-    for (int base = wid * RPW; base < rows_total; base += nwaves * RPW) {
-      const int row = base + lane / LPR;
+    const int jl = lane % LPR, rw = lane / LPR;
+    float* wst = stage + wid * kStageFloats;               // this wave's 16 rows x 32 channels
+    int* woff = reinterpret_cast<int*>(wst + 16 * 32);     // and their grad_value element offsets
+    // row batches of 16 per wave, handed out in order by an LDS counter: the coarse levels' rows (first,
+    // ~37 records each at config 2 against ~9 on the finest level) do not pile up on the first waves
+    for (int b = wid; b * RPW < rows_total;) {
+      const int base = b * RPW;
+      const int row = base + rw;
       float acc[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
-      int64_t off = -1;  // element offset of channel 0 of this group's grad_value row (-1: none)
+      int off = -1;  // element offset of channel 0 of this group's grad_value row (-1: none)
+      int l = 0, ey = 0, ex = 0;
+      bool any = false;
       if (row < rows_total) {
-        int l = 0;
         while (row >= ts.roff[l + 1]) ++l;
         const int ww = ts.ww[l], rr = row - ts.roff[l];
-        const int ey = rr / ww, ex = rr - ey * ww;  // window coordinates; cells are offset by (1, 1)
+        ey = rr / ww;
+        ex = rr - ey * ww;  // window coordinates; cells are offset by (1, 1)
         const int cw = ww + 1, cbase = ts.coff[l] + (ey + 1) * cw + ex + 1;
         // corner 1 of cell (y, x), corner 2 of (y, x-1), corner 3 of (y-1, x), corner 4 of (y-1, x-1)
-        int id[4] = {head[cbase], head[cbase - 1], head[cbase - cw], head[cbase - cw - 1]};
-        bool any = false;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) any |= id[c] != 0xffff;
-        if (any) {
-          // every list holds distinct samples of this workgroup: bounded by their count
-          for (int it = 0; it < geo.max_qt * LP && (id[0] & id[1] & id[2] & id[3]) != 0xffff; ++it) {
+        for (int c = 0; c < 4; ++c) {
+          const int cell = cbase - ((c & 2) ? cw : 0) - (c & 1);
+          const int s0 = cstart[cell], s1 = cstart[cell + 1];
+          any |= s1 > s0;
+          // two records per step: their LDS reads overlap
+          int i = s0;
+          for (; i + 1 < s1; i += 2) {
+            const int sa = slots[i], sb = slots[i + 1];
+            const float ha = desc[3 * sa], wa = desc[3 * sa + 1], aa = desc[3 * sa + 2];
+            const float hb = desc[3 * sb], wb = desc[3 * sb + 1], ab = desc[3 * sb + 2];
+            const f4* ga = reinterpret_cast<const f4*>(gsh + (sa / LP) * D + CPL * jl);
+            const f4* gb = reinterpret_cast<const f4*>(gsh + (sb / LP) * D + CPL * jl);
+            const float lya = ha - floorf(ha), lxa = wa - floorf(wa), lyb = hb - floorf(hb), lxb = wb - floorf(wb);
+            const float ca = ((c & 2) ? lya : 1.f - lya) * ((c & 1) ? lxa : 1.f - lxa) * aa;
+            const float cb = ((c & 2) ? lyb : 1.f - lyb) * ((c & 1) ? lxb : 1.f - lxb) * ab;
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              if (id[c] == 0xffff) continue;
-              const int sid = id[c];
-              id[c] = nxt[sid];
-              const float h = desc[3 * sid], w = desc[3 * sid + 1], a = desc[3 * sid + 2];
-              const float ly = h - floorf(h), lx = w - floorf(w);
-              const float wy = (c & 2) ? ly : 1.f - ly, wx = (c & 1) ? lx : 1.f - lx;
-              const float coef = wy * wx * a;
-              const int qi = sid / LP;
-              const float* gr = gsh + qi * D + CPL * jl;
-#pragma unroll
-              for (int k = 0; k < CPL / 4; ++k) {
-                const f4 gv = *reinterpret_cast<const f4*>(gr + 4 * k);
-                acc[4 * k] += coef * gv.x; acc[4 * k + 1] += coef * gv.y;
-                acc[4 * k + 2] += coef * gv.z; acc[4 * k + 3] += coef * gv.w;
-              }
+            for (int k = 0; k < CPL / 4; ++k) {
+              const f4 va = ga[k], vb2 = gb[k];
+              acc[4 * k] += ca * va.x + cb * vb2.x; acc[4 * k + 1] += ca * va.y + cb * vb2.y;
+              acc[4 * k + 2] += ca * va.z + cb * vb2.z; acc[4 * k + 3] += ca * va.w + cb * vb2.w;
             }
           }
-          const int y = ts.wy0[l] + ey, x = ts.wx0[l] + ex;
-          off = ((static_cast<int64_t>(n) * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D;
+          if (i < s1) {
+            const int sa = slots[i];
+            const float ha = desc[3 * sa], wa = desc[3 * sa + 1], aa = desc[3 * sa + 2];
+            const f4* ga = reinterpret_cast<const f4*>(gsh + (sa / LP) * D + CPL * jl);
+            const float lya = ha - floorf(ha), lxa = wa - floorf(wa);
+            const float ca = ((c & 2) ? lya : 1.f - lya) * ((c & 1) ? lxa : 1.f - lxa) * aa;
+#pragma unroll
+            for (int k = 0; k < CPL / 4; ++k) {
+              const f4 va = ga[k];
+              acc[4 * k] += ca * va.x; acc[4 * k + 1] += ca * va.y;
+              acc[4 * k + 2] += ca * va.z; acc[4 * k + 3] += ca * va.w;
+            }
+          }
         }
       }
-      // transpose the wave's rows (ds_bpermute) so that each atomic instruction covers two whole 128-byte
-      // rows, one dword per lane: the L2 takes atomics per request, two requests per row this way
-      const int c = lane & 31;
+      if (any) {
+        const int y = ts.wy0[l] + ey, x = ts.wx0[l] + ex;
+        off = ((n * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D;
+      }
+      // transpose the wave's 16 rows through LDS so that each atomic instruction adds two whole 128-B rows,
+      // one dword per lane (the L2 takes atomics per 64-B request)
+#pragma unroll
+      for (int k = 0; k < CPL / 4; ++k)
+        *reinterpret_cast<f4*>(wst + rw * 32 + CPL * jl + 4 * k) = f4{acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
+      if (jl == 0) woff[rw] = off;
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage writes are in LDS
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int i = 0; i < RPW / 2; ++i) {
-        const int src = (2 * i + (lane >> 5)) * LPR + c / CPL;  // lane holding channel c of row 2i + half
-        float val = 0.f;
-#pragma unroll
-        for (int k = 0; k < CPL; ++k) {
-          const float xk = __shfl(acc[k], src);
-          val = (c % CPL) == k ? xk : val;
+        const int r2 = 2 * i + (lane >> 5);
+        const int o = woff[r2];
+        const float v = wst[r2 * 32 + (lane & 31)];
+        if constexpr (NOFLUSH) {
+          asm volatile("" ::"v"(v), "v"(o));
+        } else {
+          if (o >= 0) atomicAdd(gvalue + o + (lane & 31), v);
         }
-        const int64_t o = __shfl(off, src);
-        if (o >= 0) atomicAdd(gvalue + o + c, val);
       }
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the next batch overwrites the stage
+      __builtin_amdgcn_wave_barrier();
+      int nb = 0;
+      if (lane == 0) nb = atomicAdd(&ts.next_batch, 1);
+      b = __shfl(nb, 0);
     }
   }
+  if constexpr (STAMP) __syncthreads();
+  M2F_STAMP(4)
+#undef M2F_STAMP
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -875,9 +989,12 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   geo.max_qt = qt;
   const int lp = d.L * d.P;
   if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff) return false;
-  lds = static_cast<size_t>(qt) * 32 * 4 + static_cast<size_t>(qt) * lp * 3 * 4 +
-        ((static_cast<size_t>(qt) * lp * 2 + 15) & ~static_cast<size_t>(15)) + static_cast<size_t>(geo.max_rows) * 4;
-  return lds <= 150 * 1024;
+  if (static_cast<int64_t>(qt) * lp > static_cast<int64_t>(kSortPerThread) * kBwdThreads) return false;
+  const size_t ns = static_cast<size_t>(qt) * lp;
+  lds = (static_cast<size_t>(qt) * 32 + ((ns * 3 + 3) & ~static_cast<size_t>(3)) + kBwdWaves * kStageFloats) * 4 +
+        ((static_cast<size_t>(geo.max_rows) + 1 + 3) & ~static_cast<size_t>(3)) * 4 + (((ns + 31) / 32 + 3) & ~static_cast<size_t>(3)) * 4 +
+        ns * 2;
+  return lds <= 156 * 1024;
 }
 
 template <int LT, bool FUSED>
@@ -889,7 +1006,7 @@ void launch_tiled(const float* value, const float* loc, const float* attn, const
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     attr = true;
   }
-  const dim3 grid(geo.nty * geo.ntx, d.M, d.N);
+  const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
   msda_bwd_f32_tiled<LT, FUSED><<<grid, kBwdThreads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
 }
 
@@ -1114,3 +1231,33 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
   launch_tiled_levels<true>(value, nullptr, nullptr, fe, grad_output, geo, lds, d, grad_value, grad_proj, nullptr, st);
   return m2f::check_launch(fn);
 }
+
+#ifdef M2F_DIAG
+// Diagnostic build only (tools/msda_stamps.py builds it as a separate library): the unfused tiled backward with
+// s_memtime stamps at its phase barriers, stamps[wg * 8 + k], k = 0..4.
+extern "C" int m2f_diag_msda_bwd_stamps_f32(const float* value, const float* loc, const float* attn,
+                                            const float* grad_output, int batch, int spatial_size, int num_heads,
+                                            int num_levels, const int64_t* host_spatial_shapes, float* grad_value,
+                                            float* grad_loc, float* grad_attn, unsigned long long* stamps,
+                                            int noflush, void* stream) {
+  const Dims d{batch, spatial_size, num_heads, 32, num_levels, spatial_size, 4};
+  TileGeom geo;
+  size_t lds;
+  if (num_levels != 3 || !make_tile_geom(d, host_spatial_shapes, geo, lds)) return m2f::fail(M2F_EUNSUPPORTED, "diag");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  (void)hipMemsetAsync(grad_value, 0, static_cast<size_t>(d.N) * d.S * d.M * 32 * 4, st);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, true, false>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
+  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, true, true>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
+  const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
+  if (noflush)
+    msda_bwd_f32_tiled<3, false, true, true><<<grid, kBwdThreads, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, geo,
+                                                                          d.S, d.M, grad_value, grad_loc, grad_attn, stamps);
+  else
+    msda_bwd_f32_tiled<3, false, true, false><<<grid, kBwdThreads, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output,
+                                                                           geo, d.S, d.M, grad_value, grad_loc, grad_attn,
+                                                                           stamps);
+  return m2f::check_launch("m2f_diag_msda_bwd_stamps_f32");
+}
+#endif

@@ -1,0 +1,9 @@
+# MSDA backward anatomy: phase stamps (diag build) + SQ counter pass on the microbench.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+cd $R && mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 120 python -u tools/msda_stamps.py 2>&1 | tee gpurun_out/r2e_stamps.log
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE --kernel-include-regex msda_bwd --output-format csv -d $R/gpurun_out/r2e_sq -o sq -- python3 $R/tools/msda_bench.py --bwd-only --iters 3 > gpurun_out/r2e_sq.log 2>&1
+echo "sq rc=$?"
+timeout -s KILL 120 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_INSTS_SALU SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE --kernel-include-regex msda_bwd --output-format csv -d $R/gpurun_out/r2e_lds -o lds -- python3 $R/tools/msda_bench.py --bwd-only --iters 3 > gpurun_out/r2e_lds.log 2>&1
+echo "lds rc=$?"
