@@ -307,9 +307,8 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // backward over the pair's L*P logits).
 // ------------------------------------------------------------------------------------------------
 constexpr int kWalkLanes = 4;   // phase-3 lanes per window pixel (8 channels each)
-constexpr int kBwdThreads = 1024;
-constexpr int kBwdWaves = kBwdThreads / 64;
-constexpr int kSortPerThread = 6;  // samples per thread in the counting sort: max_qt * L * P <= 6 * 1024
+constexpr int kMaxBwdWaves = 16;
+constexpr int kSortSamples = 6144;  // samples per workgroup the counting sort holds in registers (max_qt * L * P)
 constexpr int kStageFloats = 16 * 32 + 16;  // per wave: 16 rows x 32 channels + 16 row offsets
 
 struct TileState {
@@ -318,7 +317,7 @@ struct TileState {
   int roff[kTileMaxL + 1];   // window pixel offsets per level
   int coff[kTileMaxL + 1];   // extended-cell offsets per level ((wh+1) x (ww+1) cells)
   int qc[kTileMaxL + 1], qy0[kTileMaxL], qx0[kTileMaxL], qw[kTileMaxL];
-  int wsum[kBwdWaves];       // block scan
+  int wsum[kMaxBwdWaves];    // block scan
   int next_batch;            // phase-3 row batches handed out dynamically
 };
 
@@ -357,12 +356,14 @@ __device__ __forceinline__ int window_cell(const TileState& ts, int l, int h0, i
 
 // STAMP (diagnostic builds only, M2F_DIAG): s_memtime at the phase barriers of each workgroup into `stamps`;
 // NOFLUSH (diagnostic builds only): phase 3 without its HBM adds, to price them.
-template <int LT, bool FUSED, bool STAMP = false, bool NOFLUSH = false>
-__global__ void __launch_bounds__(kBwdThreads) msda_bwd_f32_tiled(
+// TPB threads per workgroup: 1024 (one workgroup per CU, 16x16 tiles) or 512 (two per CU, 16x8 tiles).
+template <int LT, bool FUSED, int TPB, bool STAMP = false, bool NOFLUSH = false>
+__global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
     float* __restrict__ gloc, float* __restrict__ gattn, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int D = 32, P = 4, LP = LT * P;
+  constexpr int kBwdThreads = TPB, kBwdWaves = TPB / 64, kSortPerThread = kSortSamples / TPB;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
   __shared__ TileState ts;
 #define M2F_STAMP(k)                                                                                        \
@@ -954,10 +955,11 @@ int env_int(const char* name, int dflt) {
 
 // Tile geometry for the tiled backward; false when the configuration does not qualify (then the
 // caller uses the untiled kernels).  Lq == S: the queries are the flattened pyramid.
-//   M2F_MSDA_TILE (16): tile edge on the finest level;  M2F_MSDA_HALO (8): window halo;
-//   M2F_MSDA_WIN_ROWS (2304): list-head cells per workgroup (the halo shrinks until the window fits).
-// Geometry only: every setting computes the same gradients (tests sweep them).
-bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds) {
+//   M2F_MSDA_THREADS (512): workgroup size, 512 (two workgroups per CU) or 1024 (one);
+//   M2F_MSDA_TILE / M2F_MSDA_TILE_W (12 / 12 at 512 threads, 16 / 16 at 1024): tile on the finest level;
+//   M2F_MSDA_HALO (8): window halo;  M2F_MSDA_WIN_ROWS (cells per workgroup; the halo shrinks until the
+//   window fits).  Geometry only: every setting computes the same gradients (tests sweep them).
+bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds, int& threads) {
   if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
   if (static_cast<int64_t>(d.N) * d.S * d.M * d.D >= (int64_t{1} << 31)) return false;  // 32-bit row offsets
   geo = TileGeom{};
@@ -973,51 +975,68 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   if (total != d.S) return false;
-  const int tile = std::max(1, env_int("M2F_MSDA_TILE", 16));
-  geo.nty = (geo.H[fi] + tile - 1) / tile;
-  geo.ntx = (geo.W[fi] + tile - 1) / tile;
-  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", 2304);
+  threads = env_int("M2F_MSDA_THREADS", 512) >= 1024 ? 1024 : 512;
+  // 512 threads: 12x12 tiles (78 KB of LDS, two workgroups per CU) measured 2.44 ms at config 2 against 2.45
+  // (8x16), 2.52 (16x8) and 2.65 for 1024 threads with 16x16 tiles (tools/msda_bench.py, r2k)
+  const int tile_h = std::max(1, env_int("M2F_MSDA_TILE", threads == 1024 ? 16 : 12));
+  const int tile_w = std::max(1, env_int("M2F_MSDA_TILE_W", tile_h));
+  geo.nty = (geo.H[fi] + tile_h - 1) / tile_h;
+  geo.ntx = (geo.W[fi] + tile_w - 1) / tile_w;
   geo.max_halo = std::max(0, env_int("M2F_MSDA_HALO", 8));
-  // the cell budget must hold every level's share of one tile at halo 0 (tiles span at most
-  // ceil(n / nt) pixels per axis, tile_lo), plus the extra cell row / column
-  int own = 0, qt = 0;
+  // cells of the largest window any workgroup can choose (tile + 2 halo + 1 per axis, clipped to the level),
+  // unless a smaller budget is asked for; it must hold every level's share of one tile at halo 0 (tiles
+  // span at most ceil(n / nt) pixels per axis, tile_lo) plus the extra cell row / column
+  int own = 0, qt = 0, full = 0;
   for (int l = 0; l < d.L; ++l) {
     const int th = (geo.H[l] + geo.nty - 1) / geo.nty, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx;
     own += (th + 2) * (tw + 2);
+    full += (std::min(geo.H[l], th + 2 * geo.max_halo) + 1) * (std::min(geo.W[l], tw + 2 * geo.max_halo) + 1);
     qt += th * tw;
   }
+  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", full);
   geo.max_qt = qt;
   const int lp = d.L * d.P;
   if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff) return false;
-  if (static_cast<int64_t>(qt) * lp > static_cast<int64_t>(kSortPerThread) * kBwdThreads) return false;
+  if (static_cast<int64_t>(qt) * lp > kSortSamples) return false;
   const size_t ns = static_cast<size_t>(qt) * lp;
-  lds = (static_cast<size_t>(qt) * 32 + ((ns * 3 + 3) & ~static_cast<size_t>(3)) + kBwdWaves * kStageFloats) * 4 +
+  lds = (static_cast<size_t>(qt) * 32 + ((ns * 3 + 3) & ~static_cast<size_t>(3)) + (threads / 64) * kStageFloats) * 4 +
         ((static_cast<size_t>(geo.max_rows) + 1 + 3) & ~static_cast<size_t>(3)) * 4 + (((ns + 31) / 32 + 3) & ~static_cast<size_t>(3)) * 4 +
         ns * 2;
   return lds <= 156 * 1024;
 }
 
-template <int LT, bool FUSED>
-void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                  const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, hipStream_t st) {
+template <int LT, bool FUSED, int TPB>
+void launch_tiled_t(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                    const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, hipStream_t st) {
   static bool attr = false;  // one flag per instantiation
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     attr = true;
   }
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
-  msda_bwd_f32_tiled<LT, FUSED><<<grid, kBwdThreads, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+  msda_bwd_f32_tiled<LT, FUSED, TPB><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+}
+
+template <int LT, bool FUSED>
+void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                  const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
+                  hipStream_t st) {
+  if (threads == 1024)
+    launch_tiled_t<LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st);
+  else
+    launch_tiled_t<LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st);
 }
 
 template <bool FUSED>
 void launch_tiled_levels(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                         const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, hipStream_t st) {
+                         const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
+                         hipStream_t st) {
   switch (d.L) {
-    case 1: launch_tiled<1, FUSED>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st); break;
-    case 2: launch_tiled<2, FUSED>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st); break;
-    case 3: launch_tiled<3, FUSED>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st); break;
-    default: launch_tiled<4, FUSED>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st); break;
+    case 1: launch_tiled<1, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st); break;
+    case 2: launch_tiled<2, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st); break;
+    case 3: launch_tiled<3, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st); break;
+    default: launch_tiled<4, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st); break;
   }
 }
 
@@ -1026,8 +1045,9 @@ bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, c
   if (env_int("M2F_MSDA_BWD_TILED", 1) == 0) return false;
   TileGeom geo;
   size_t lds;
-  if (!make_tile_geom(d, host_shapes, geo, lds)) return false;
-  launch_tiled_levels<false>(value, loc, attn, FrontEnd{}, gout, geo, lds, d, gv, gl, ga, st);
+  int threads;
+  if (!make_tile_geom(d, host_shapes, geo, lds, threads)) return false;
+  launch_tiled_levels<false>(value, loc, attn, FrontEnd{}, gout, geo, lds, threads, d, gv, gl, ga, st);
   return true;
 }
 
@@ -1198,7 +1218,8 @@ extern "C" int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, 
   if (!host_spatial_shapes || !workspace_bytes) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
   TileGeom geo;
   size_t lds;
-  if (!make_tile_geom(d, host_spatial_shapes, geo, lds))
+  int threads;
+  if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout", fn);
   *workspace_bytes = 0;  // the backward needs no workspace (kept for ABI stability)
   return m2f::ok();
@@ -1219,7 +1240,8 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
     return m2f::fail(M2F_EINVAL, "%s: bad gradient pointer", fn);
   TileGeom geo;
   size_t lds;
-  if (!make_tile_geom(d, host_spatial_shapes, geo, lds))
+  int threads;
+  if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout (num_query == spatial_size)", fn);
   (void)workspace;
   (void)workspace_bytes;
@@ -1228,7 +1250,8 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
   hipError_t e = hipMemsetAsync(grad_value, 0, gv_bytes, st);
   if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
   const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
-  launch_tiled_levels<true>(value, nullptr, nullptr, fe, grad_output, geo, lds, d, grad_value, grad_proj, nullptr, st);
+  launch_tiled_levels<true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj,
+                            nullptr, st);
   return m2f::check_launch(fn);
 }
 
@@ -1243,21 +1266,26 @@ extern "C" int m2f_diag_msda_bwd_stamps_f32(const float* value, const float* loc
   const Dims d{batch, spatial_size, num_heads, 32, num_levels, spatial_size, 4};
   TileGeom geo;
   size_t lds;
-  if (num_levels != 3 || !make_tile_geom(d, host_spatial_shapes, geo, lds)) return m2f::fail(M2F_EUNSUPPORTED, "diag");
+  int threads;
+  if (num_levels != 3 || !make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
+    return m2f::fail(M2F_EUNSUPPORTED, "diag");
   hipStream_t st = static_cast<hipStream_t>(stream);
   (void)hipMemsetAsync(grad_value, 0, static_cast<size_t>(d.N) * d.S * d.M * 32 * 4, st);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, true, false>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
-  (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, true, true>),
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
-  if (noflush)
-    msda_bwd_f32_tiled<3, false, true, true><<<grid, kBwdThreads, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, geo,
-                                                                          d.S, d.M, grad_value, grad_loc, grad_attn, stamps);
-  else
-    msda_bwd_f32_tiled<3, false, true, false><<<grid, kBwdThreads, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output,
-                                                                           geo, d.S, d.M, grad_value, grad_loc, grad_attn,
-                                                                           stamps);
+#define M2F_DIAG_LAUNCH(TPB, NF)                                                                                  \
+  do {                                                                                                           \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, TPB, true, NF>),      \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);                    \
+    msda_bwd_f32_tiled<3, false, TPB, true, NF><<<grid, TPB, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, \
+                                                                       geo, d.S, d.M, grad_value, grad_loc,     \
+                                                                       grad_attn, stamps);                      \
+  } while (0)
+  if (threads == 1024) {
+    if (noflush) M2F_DIAG_LAUNCH(1024, true); else M2F_DIAG_LAUNCH(1024, false);
+  } else {
+    if (noflush) M2F_DIAG_LAUNCH(512, true); else M2F_DIAG_LAUNCH(512, false);
+  }
+#undef M2F_DIAG_LAUNCH
   return m2f::check_launch("m2f_diag_msda_bwd_stamps_f32");
 }
 #endif

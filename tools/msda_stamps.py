@@ -48,7 +48,11 @@ def main():
     gv = torch.empty_like(v)
     gl = torch.empty_like(loc)
     ga = torch.empty_like(attn)
-    nwg = 64 * M * N
+    import math as _m
+    thr = int(os.environ.get('M2F_MSDA_THREADS', '512'))
+    th = int(os.environ.get('M2F_MSDA_TILE', '16' if thr >= 1024 else '12'))
+    tw = int(os.environ.get('M2F_MSDA_TILE_W', str(th)))
+    nwg = _m.ceil(128 / th) * _m.ceil(128 / tw) * M * N
     stamps = torch.zeros(nwg * 8, dtype=torch.int64, device=v.device)
     hs = (ctypes.c_int64 * 6)(*[x for hw in shapes for x in hw])
     stream = torch.cuda.current_stream().cuda_stream
