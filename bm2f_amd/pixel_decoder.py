@@ -26,7 +26,7 @@ from .msda import MSDeformAttn, attach_host_shapes
 from . import conv_ops, linear_ops
 from .norm_ops import add_layernorm, group_norm_act
 from .position_encoding import PositionEmbeddingSine
-from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill, configurable, get_norm
+from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill, configurable, get_norm, register
 
 
 # encoder layers hand their residual inputs through the projection / FFN autograd nodes so gradient sums
@@ -194,7 +194,7 @@ class MSDeformAttnTransformerEncoderOnly(nn.Module):
         return memory, spatial_shapes, level_start_index
 
 
-@SEM_SEG_HEADS_REGISTRY.register()
+@register(lambda: SEM_SEG_HEADS_REGISTRY)
 class MSDeformAttnPixelDecoder(nn.Module):
     """Deformable-encoder pixel decoder (msdeformattn.py:164-358)."""
 

@@ -3,8 +3,13 @@
 When detectron2 is importable its real ``configurable`` / ``Conv2d`` / ``ShapeSpec`` / ``get_norm`` and
 ``SEM_SEG_HEADS_REGISTRY`` are used, so ``build_pixel_decoder`` (reference pixel_decoder/fpn.py:21-33) and
 ``build_transformer_decoder`` (transformer_decoder/maskformer_transformer_decoder.py:22-27) find the
-modules exactly as they find the reference's.  Without detectron2 (this image) the same names are
-provided here with the same calling conventions:
+modules exactly as they find the reference's.  The transformer-decoder registry is the reference's own
+``TRANSFORMER_DECODER_REGISTRY`` object whenever its module
+(``mask2former.modeling.transformer_decoder.maskformer_transformer_decoder``, :16) is loaded when a bm2f
+class is defined -- as it is when the reference's ``transformer_decoder/__init__.py`` imports bm2f in place of
+its own decoder.  :func:`register` replaces a same-name entry (the reference's class
+registered first) instead of raising, so both import orders work.  Without detectron2 (this image) the same
+names are provided here with the same calling conventions:
 
 * ``configurable``: ``Cls(cfg, *args)`` routes through ``Cls.from_config(cfg, *args)``; explicit
   keyword construction works unchanged.
@@ -14,6 +19,7 @@ provided here with the same calling conventions:
 from __future__ import annotations
 
 import functools
+import sys
 from collections import namedtuple
 
 import torch.nn.functional as F
@@ -104,8 +110,60 @@ except Exception:  # noqa: BLE001
 
     SEM_SEG_HEADS_REGISTRY = Registry("SEM_SEG_HEADS")
 
-# Same name and role as mask2former/modeling/transformer_decoder/maskformer_transformer_decoder.py:16
-TRANSFORMER_DECODER_REGISTRY = Registry("TRANSFORMER_MODULE")
+REFERENCE_TD_MODULE = "mask2former.modeling.transformer_decoder.maskformer_transformer_decoder"
+
+# Same name and role as mask2former/modeling/transformer_decoder/maskformer_transformer_decoder.py:16; used
+# when the reference's module is not loaded
+_LOCAL_TD_REGISTRY = Registry("TRANSFORMER_MODULE")
+
+
+def transformer_decoder_registry():
+    """The reference's TRANSFORMER_DECODER_REGISTRY if its module is loaded, else bm2f's own."""
+    mod = sys.modules.get(REFERENCE_TD_MODULE)
+    reg = getattr(mod, "TRANSFORMER_DECODER_REGISTRY", None) if mod is not None else None
+    return reg if reg is not None else _LOCAL_TD_REGISTRY
+
+
+def _entries(registry):
+    # detectron2 / fvcore Registry and the local one keep their map in ``_obj_map``
+    return getattr(registry, "_obj_map", None)
+
+
+def register(registry_fn):
+    """Class decorator: register into ``registry_fn()`` (resolved now, at class definition), replacing an
+    entry of the same name -- e.g. the reference's own MSDeformAttnPixelDecoder when its module was imported
+    first -- instead of raising "already registered"."""
+    def deco(cls):
+        _register_replacing(registry_fn(), cls)
+        return cls
+    return deco
+
+
+def _register_replacing(registry, cls):
+    entries = _entries(registry)
+    if entries is not None and cls.__name__ in entries:
+        entries[cls.__name__] = cls
+    else:
+        registry.register(cls)
+
+
+def install():
+    """(Re)register the bm2f classes into the registries visible now: call after importing the reference's
+    modules in an order where bm2f was imported first."""
+    from .pixel_decoder import MSDeformAttnPixelDecoder
+    from .transformer_decoder import MultiScaleMaskedTransformerDecoder
+    from .video_decoder import VideoMultiScaleMaskedTransformerDecoder
+    _register_replacing(SEM_SEG_HEADS_REGISTRY, MSDeformAttnPixelDecoder)
+    for cls in (MultiScaleMaskedTransformerDecoder, VideoMultiScaleMaskedTransformerDecoder):
+        _register_replacing(transformer_decoder_registry(), cls)
+        if transformer_decoder_registry() is not _LOCAL_TD_REGISTRY:
+            _register_replacing(_LOCAL_TD_REGISTRY, cls)
+
+
+def __getattr__(name):
+    if name == "TRANSFORMER_DECODER_REGISTRY":
+        return transformer_decoder_registry()
+    raise AttributeError(name)
 
 
 def build_pixel_decoder(cfg, input_shape):
@@ -121,7 +179,7 @@ def build_pixel_decoder(cfg, input_shape):
 def build_transformer_decoder(cfg, in_channels, mask_classification=True):
     """reference transformer_decoder/maskformer_transformer_decoder.py:22-27"""
     name = cfg.MODEL.MASK_FORMER.TRANSFORMER_DECODER_NAME
-    return TRANSFORMER_DECODER_REGISTRY.get(name)(cfg, in_channels, mask_classification)
+    return transformer_decoder_registry().get(name)(cfg, in_channels, mask_classification)
 
 
 def c2_xavier_fill(module: nn.Module) -> None:
@@ -132,5 +190,5 @@ def c2_xavier_fill(module: nn.Module) -> None:
 
 
 __all__ = ["Registry", "configurable", "ShapeSpec", "Conv2d", "get_norm", "SEM_SEG_HEADS_REGISTRY",
-           "TRANSFORMER_DECODER_REGISTRY", "build_pixel_decoder", "build_transformer_decoder", "c2_xavier_fill",
-           "HAVE_DETECTRON2"]
+           "TRANSFORMER_DECODER_REGISTRY", "transformer_decoder_registry", "register", "install",
+           "build_pixel_decoder", "build_transformer_decoder", "c2_xavier_fill", "HAVE_DETECTRON2"]

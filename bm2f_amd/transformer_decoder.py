@@ -25,7 +25,7 @@ from torch.nn import functional as F
 
 from . import decoder_ops
 from .position_encoding import PositionEmbeddingSine
-from .registry import TRANSFORMER_DECODER_REGISTRY, Conv2d, c2_xavier_fill, configurable
+from .registry import Conv2d, c2_xavier_fill, configurable, register, transformer_decoder_registry
 
 
 def _get_activation_fn(activation):
@@ -177,7 +177,7 @@ def _migrate_static_query(module, state_dict, prefix, local_metadata):
                 "Please upgrade your models. Applying automatic conversion now ...")
 
 
-@TRANSFORMER_DECODER_REGISTRY.register()
+@register(transformer_decoder_registry)
 class MultiScaleMaskedTransformerDecoder(nn.Module):
     _version = 2
 

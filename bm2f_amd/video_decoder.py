@@ -12,11 +12,11 @@ from torch import nn
 
 from . import decoder_ops
 from .position_encoding import PositionEmbeddingSine3D
-from .registry import TRANSFORMER_DECODER_REGISTRY, configurable
+from .registry import configurable, register, transformer_decoder_registry
 from .transformer_decoder import MultiScaleMaskedTransformerDecoder
 
 
-@TRANSFORMER_DECODER_REGISTRY.register()
+@register(transformer_decoder_registry)
 class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder):
     _version = 2
 
