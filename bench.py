@@ -130,7 +130,10 @@ ENTRIES = {
         a[2] * a[3] * a[4] * a[5] * a[6] * (4 if a[1] == 0 else 2) + a[2] * a[3] * a[11] * 4, 0)),
     "m2f_masked_attn_fwd": ("masked_attn_fwd", "hbm", lambda a: _attn_bytes(a, True)),
     "m2f_masked_attn_bwd": ("masked_attn_bwd", "hbm", lambda a: _attn_bytes(a, False)),
-    "m2f_mask_heads_fwd": ("mask_einsum_fwd", "mfma", lambda a: (0, 2 * a[4] * a[5] * a[6] * a[7] * a[8])),
+    # (dtype, embed, feats, B, Q, C, T, H, W, th, tw, masks, bits, nwords): feats read + masks written
+    "m2f_mask_heads_fwd": ("mask_heads_fwd", "hbm", lambda a: (
+        2 * a[3] * a[6] * a[7] * a[8] * (a[5] + a[4]) + 2 * a[3] * a[4] * a[5] + 4 * a[3] * a[4] * a[13],
+        2 * a[3] * a[4] * a[5] * a[6] * a[7] * a[8])),
     "m2f_gemm_f32x3_nt": ("x3_gemm_nt", "mfma", lambda a: _x3(a[11], a[12], a[13])),
     "m2f_gemm_f32x3_nt_add": ("x3_gemm_nt", "mfma", lambda a: _x3(a[14], a[15], a[16])),
     "m2f_gemm_f32x3_tn": ("x3_gemm_tn", "mfma", lambda a: _x3(a[7], a[8], a[9])),
@@ -144,7 +147,7 @@ MFMA_NOTE = {
     "x3_gemm_tn": "as x3_gemm_nt (weight gradients, split over rows, fixed-order slab sums)",
     "x3_conv": "as x3_gemm_nt (implicit-GEMM conv, 1x1 and 3x3)",
     "x3_conv_wgrad": "as x3_gemm_nt (1x1 conv weight gradients)",
-    "mask_einsum_fwd": "bqc,bchw->bqhw on bf16/f16 MFMA with the fused bitmask epilogue",
+    "mask_heads_fwd": "bqc,bchw->bqhw on bf16/f16 MFMA with the fused bitmask epilogue (HBM-bound: mfma_tflops)",
 }
 
 
@@ -191,9 +194,13 @@ def roofline_entry(fam, k, bound):
     t = k["total_ms"] * 1e-3
     if bound == "hbm":
         ach = k["bytes"] / t / 1e9
-        return {"kernel": fam, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(ach / HBM_PEAK_GBS, 4), "mean_launch_ms": round(k["mean_ms"], 4),
-                "ms_per_step": round(k["ms_per_step"], 3)}
+        ent = {"kernel": fam, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": round(ach / HBM_PEAK_GBS, 4), "mean_launch_ms": round(k["mean_ms"], 4),
+               "ms_per_step": round(k["ms_per_step"], 3)}
+        if k["flops"] and fam in MFMA_NOTE:
+            ent["mfma_tflops"] = round(k["flops"] / t / 1e12, 1)
+            ent["note"] = MFMA_NOTE[fam]
+        return ent
     if fam.startswith("x3"):
         ach = 6 * k["flops"] / t / 1e12
         return {"kernel": fam, "bound": "mfma", "achieved": round(ach, 1), "peak": BF16_PEAK_TF, "unit": "TFLOP/s",

@@ -46,11 +46,12 @@ __global__ void __launch_bounds__(kT) gn_stats(const float* __restrict__ x, int6
   const f4* p = reinterpret_cast<const f4*>(x + ng * span);
   double s = 0.0, q = 0.0;
   for (int64_t i = v0 + threadIdx.x; i < v1; i += kT) {
+    // squares and sums in fp64: E[x^2] - E[x]^2 cancels catastrophically for |mean| >> std if the squares
+    // are rounded to fp32 first (x = randn + 100: fp32 squares carry 6e-4 absolute error each)
     const f4 v = p[i];
-    const float fs = (v.x + v.y) + (v.z + v.w);
-    const float fq = (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
-    s += fs;
-    q += fq;
+    const double a = v.x, b = v.y, c = v.z, d = v.w;
+    s += (a + b) + (c + d);
+    q += (a * a + b * b) + (c * c + d * d);
   }
   s = block_sum(s, red);
   q = block_sum(q, red);

@@ -989,7 +989,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   int own = 0, qt = 0, full = 0;
   for (int l = 0; l < d.L; ++l) {
     const int th = (geo.H[l] + geo.nty - 1) / geo.nty, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx;
-    own += (th + 2) * (tw + 2);
+    own += (std::min(geo.H[l], th + 1) + 1) * (std::min(geo.W[l], tw + 1) + 1);  // clipped like `full`
     full += (std::min(geo.H[l], th + 2 * geo.max_halo) + 1) * (std::min(geo.W[l], tw + 2 * geo.max_halo) + 1);
     qt += th * tw;
   }

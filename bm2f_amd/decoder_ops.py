@@ -212,6 +212,20 @@ class _FoldState:
         self.to_feats = to_feats
 
 
+def _folded_backward(ctx, grad):
+    (e,) = ctx.saved_tensors
+    fold = ctx.fold
+    f = fold.feats_lp
+    B, C, N = f.shape
+    g = grad.to(f.dtype).reshape(B, -1, N)
+    de = torch.bmm(g, f.transpose(1, 2)).to(ctx.edtype) if ctx.needs_input_grad[0] else None
+    tok = None
+    if ctx.needs_input_grad[1]:
+        fold.state.items.append((e, g))
+        tok = g.new_empty(0)
+    return de, tok
+
+
 class _FoldedMaskEinsum(Function):
     @staticmethod
     def forward(ctx, embed, token, fold):
@@ -225,17 +239,47 @@ class _FoldedMaskEinsum(Function):
 
     @staticmethod
     def backward(ctx, grad):
-        (e,) = ctx.saved_tensors
-        fold = ctx.fold
+        return (*_folded_backward(ctx, grad), None)
+
+
+class _FoldedMaskHeads(Function):
+    """The einsum on the hand-written MFMA kernel (csrc/mask_heads.hip) with, when ``size`` is given, the
+    next cross-attention's bitmask from the same launch (+ the row fix); backward as _FoldedMaskEinsum."""
+
+    @staticmethod
+    def forward(ctx, embed, token, fold, size):
         f = fold.feats_lp
-        B, C, N = f.shape
-        g = grad.to(f.dtype).reshape(B, -1, N)
-        de = torch.bmm(g, f.transpose(1, 2)).to(ctx.edtype) if ctx.needs_input_grad[0] else None
-        tok = None
-        if ctx.needs_input_grad[1]:
-            fold.state.items.append((e, g))
-            tok = g.new_empty(0)
-        return de, tok, None
+        e = embed.to(f.dtype).contiguous()
+        if e.data_ptr() % 16:
+            e = e.clone()
+        B, C, _ = f.shape
+        T, H, W = fold.frames_hw
+        Q = e.shape[1]
+        out = torch.empty(fold.out_shape(Q), dtype=f.dtype, device=f.device)
+        if size is not None:
+            h, w = int(size[0]), int(size[1])
+            keys = T * h * w
+            nw = num_words(keys)
+            bits = torch.zeros((B, Q, nw), dtype=torch.int32, device=f.device)
+            bp = bits.data_ptr()
+        else:
+            h = w = nw = 0
+            bits = torch.empty((0,), dtype=torch.int32, device=f.device)
+            bp = None
+        st = _stream(f)
+        _native.call("m2f_mask_heads_fwd", _code(f.dtype), e.data_ptr(), f.data_ptr(), B, Q, C, T, H, W, h, w,
+                     out.data_ptr(), bp, nw, st)
+        if size is not None:
+            _native.call("m2f_mask_row_fix", bp, B * Q, nw, keys, st)
+        ctx.mark_non_differentiable(bits)
+        ctx.fold = fold
+        ctx.edtype = embed.dtype
+        ctx.save_for_backward(e)
+        return out, bits
+
+    @staticmethod
+    def backward(ctx, grad, _grad_bits):
+        return (*_folded_backward(ctx, grad), None, None)
 
 
 class MaskFeatureFold:
@@ -257,8 +301,36 @@ class MaskFeatureFold:
     def out_shape(self, q):
         return (self.feats_lp.shape[0], q) + self._tail
 
+    @property
+    def frames_hw(self):
+        return self._tail if len(self._tail) == 3 else (1,) + self._tail
+
     def __call__(self, embed):
         return _FoldedMaskEinsum.apply(embed, self.token, self)
+
+    def fused_ok(self, num_queries, size=None) -> bool:
+        """Shapes / dtypes the mask-heads kernel takes (m2f_mask_heads_fwd's constraints)."""
+        f = self.feats_lp
+        T, H, W = self.frames_hw
+        if not (f.is_cuda and f.dtype in (torch.bfloat16, torch.float16) and f.is_contiguous()
+                and f.shape[1] % 32 == 0 and W % 8 == 0 and num_queries <= 256 and f.data_ptr() % 16 == 0):
+            return False
+        if size is None:
+            return True
+        h, w = int(size[0]), int(size[1])
+        s = H // h if h > 0 else 0
+        return s >= 2 and s % 2 == 0 and s * h == H and s * w == W and 128 % s == 0
+
+
+def mask_heads(fold: MaskFeatureFold, embed: torch.Tensor, size=None):
+    """One prediction head's masks and (``size`` given) the next cross-attention's bitmask:
+    ``fold(embed)`` + :func:`attn_mask_bits` (reference :442-449 and :400), in one kernel where the shapes
+    allow (the pyramid's exact 2/4/8x reductions in bf16 / fp16), else as those two steps."""
+    if fold.fused_ok(embed.shape[1], size):
+        out, bits = _FoldedMaskHeads.apply(embed, fold.token, fold, size)
+        return out, (bits if size is not None else None)
+    out = fold(embed)
+    return out, (attn_mask_bits(out, size) if size is not None else None)
 
 
 def image_mask_fold(mask_features, mask_features_lp=None):

@@ -42,18 +42,53 @@ __all__ = [
 _HOST_ATTR = "_bm2f_host_shapes"
 
 
-def attach_host_shapes(spatial_shapes: torch.Tensor, shapes: Sequence[Tuple[int, int]]) -> torch.Tensor:
+_LSI_ATTR = "_bm2f_level_starts"
+
+
+def _prefix_starts(shapes):
+    starts, acc = [], 0
+    for h, w in shapes:
+        starts.append(acc)
+        acc += h * w
+    return tuple(starts)
+
+
+def attach_host_shapes(spatial_shapes: torch.Tensor, shapes: Sequence[Tuple[int, int]],
+                       level_start_index: torch.Tensor = None) -> torch.Tensor:
     """Record the host-side (H, W) list on a device ``spatial_shapes`` tensor.
 
     The kernels only need the device tensor; the host copy lets the backward pick its spatially tiled
-    grad_value accumulation without a device->host sync.  Results are identical either way.
+    grad_value accumulation without a device->host sync.  Results are identical either way.  The tiled and
+    fused kernels take the level starts as the prefix sums of these shapes (include/bm2f.h), so the list is
+    checked against the tensor here, once (one device->host copy), and ``level_start_index`` -- given here or
+    met later by a backward -- must be those prefix sums; a mismatch raises instead of silently disagreeing
+    with the untiled path, which reads the device level_start_index.
     """
-    setattr(spatial_shapes, _HOST_ATTR, tuple((int(h), int(w)) for h, w in shapes))
+    shapes = tuple((int(h), int(w)) for h, w in shapes)
+    got = tuple(tuple(int(v) for v in row) for row in spatial_shapes.detach().cpu().tolist())
+    if got != shapes:
+        raise ValueError(f"attach_host_shapes: spatial_shapes holds {got}, not {shapes}")
+    setattr(spatial_shapes, _HOST_ATTR, shapes)
+    if level_start_index is not None:
+        _check_level_starts(level_start_index, shapes)
     return spatial_shapes
 
 
-def _host_shapes(spatial_shapes: torch.Tensor):
-    return getattr(spatial_shapes, _HOST_ATTR, None)
+def _check_level_starts(level_start_index: torch.Tensor, shapes) -> None:
+    want = _prefix_starts(shapes)
+    if getattr(level_start_index, _LSI_ATTR, None) == want:
+        return
+    got = tuple(int(v) for v in level_start_index.detach().cpu().tolist())
+    if got != want:
+        raise ValueError(f"level_start_index {got} is not the prefix sum {want} of the attached spatial shapes")
+    setattr(level_start_index, _LSI_ATTR, want)   # checked once per tensor
+
+
+def _host_shapes(spatial_shapes: torch.Tensor, level_start_index: torch.Tensor = None):
+    hs = getattr(spatial_shapes, _HOST_ATTR, None)
+    if hs is not None and level_start_index is not None:
+        _check_level_starts(level_start_index, hs)
+    return hs
 
 
 def _check(t: torch.Tensor, name: str) -> None:
@@ -112,7 +147,7 @@ def ms_deform_attn_forward(value, spatial_shapes, level_start_index, sampling_lo
         raise RuntimeError("spatial_shapes and level_start_index must be int64")
     N, S, M, D, L, Lq, P = _dims(value, spatial_shapes, sampling_loc)
     out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
-    host = _host_shape_buffer(_host_shapes(spatial_shapes))
+    host = _host_shape_buffer(_host_shapes(spatial_shapes, level_start_index))
     _native.call(f"m2f_msda_fwd_{sfx}", _ptr(value), _ptr(spatial_shapes), _ptr(level_start_index),
                  _ptr(sampling_loc), _ptr(attn_weight), N, S, M, D, L, Lq, P, int(im2col_step),
                  ctypes.cast(host, ctypes.c_void_p) if host is not None else None, _ptr(out), _stream(value.device))
@@ -132,7 +167,7 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     grad_value = torch.empty_like(value)
     grad_loc = torch.empty_like(sampling_loc)
     grad_attn = torch.empty_like(attn_weight)
-    host = _host_shape_buffer(_host_shapes(spatial_shapes))
+    host = _host_shape_buffer(_host_shapes(spatial_shapes, level_start_index))
     _native.call(f"m2f_msda_bwd_{sfx}", _ptr(value), _ptr(spatial_shapes), _ptr(level_start_index),
                  _ptr(sampling_loc), _ptr(attn_weight), _ptr(grad_output), N, S, M, D, L, Lq, P, int(im2col_step),
                  ctypes.cast(host, ctypes.c_void_p) if host is not None else None,
@@ -147,8 +182,8 @@ class MSDeformAttnFunction(Function):
     def forward(ctx, value, value_spatial_shapes, value_level_start_index, sampling_locations, attention_weights,
                 im2col_step):
         ctx.im2col_step = im2col_step
-        ctx.host_shapes = _host_shapes(value_spatial_shapes)
-        output = ms_deform_attn_forward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
+        ctx.host_shapes = _host_shapes(value_spatial_shapes, value_level_start_index)
+        output =ms_deform_attn_forward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
                                         attention_weights, ctx.im2col_step)
         ctx.save_for_backward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
                               attention_weights)
@@ -158,8 +193,10 @@ class MSDeformAttnFunction(Function):
     @once_differentiable
     def backward(ctx, grad_output):
         value, shapes, lsi, loc, attn = ctx.saved_tensors
-        if ctx.host_shapes is not None and _host_shapes(shapes) is None:
-            attach_host_shapes(shapes, ctx.host_shapes)
+        if ctx.host_shapes is not None:
+            # unpacked saved tensors are new objects: restore the tags the forward checked
+            setattr(shapes, _HOST_ATTR, ctx.host_shapes)
+            setattr(lsi, _LSI_ATTR, _prefix_starts(ctx.host_shapes))
         grad_value, grad_loc, grad_attn = ms_deform_attn_backward(
             value, shapes, lsi, loc, attn, grad_output.contiguous(), ctx.im2col_step)
         return grad_value, None, None, grad_loc, grad_attn, None
@@ -279,8 +316,9 @@ class MSDeformAttn(nn.Module):
                 reference_points.shape[-1]))
         return loc, attn
 
-    def _fusable(self, query, reference_points, input_flatten, input_spatial_shapes, input_padding_mask):
-        hs = _host_shapes(input_spatial_shapes)
+    def _fusable(self, query, reference_points, input_flatten, input_spatial_shapes, input_padding_mask,
+                 input_level_start_index=None):
+        hs = _host_shapes(input_spatial_shapes, input_level_start_index)
         return (_fused_enabled() and hs is not None and input_padding_mask is None and query.is_cuda
                 and query.dtype == torch.float32 and input_flatten.dtype == torch.float32
                 and self.d_model // self.n_heads == 32 and self.n_points == 4 and 1 <= self.n_levels <= 4
@@ -294,7 +332,8 @@ class MSDeformAttn(nn.Module):
         ``src + pos`` and whose residual is ``src`` (msdeformattn.py:115-119).  On the fused path the two
         input projections are one autograd node (:class:`linear_ops.EncoderInProjF32`) and the returned
         ``src`` carries the residual's gradient into that node's GEMM epilogues."""
-        if (self._fusable(src, reference_points, src, input_spatial_shapes, input_padding_mask)
+        if (self._fusable(src, reference_points, src, input_spatial_shapes, input_padding_mask,
+                          input_level_start_index)
                 and (pos is None or (pos.dtype == torch.float32 and pos.dim() == 3 and pos.shape[0] in (1, src.shape[0])
                                      and pos.shape[1:] == src.shape[1:]))
                 and linear_ops.residual_fusable(src, self.value_proj)):
@@ -315,7 +354,8 @@ class MSDeformAttn(nn.Module):
                 input_padding_mask=None):
         N, Len_q, _ = query.shape
         N, Len_in, _ = input_flatten.shape
-        if self._fusable(query, reference_points, input_flatten, input_spatial_shapes, input_padding_mask):
+        if self._fusable(query, reference_points, input_flatten, input_spatial_shapes, input_padding_mask,
+                         input_level_start_index):
             # one GEMM for both sampling projections; softmax + locations happen inside the MSDA kernels
             # fp32 linears on the MFMA GEMMs (linear_ops): bias in the epilogue, bias gradient in the
             # weight-gradient GEMM

@@ -171,8 +171,8 @@ class MSDeformAttnTransformerEncoderOnly(nn.Module):
         hit = self._shape_cache.get(key)
         if hit is None:
             st = torch.as_tensor(host_shapes, dtype=torch.long, device=device)
-            attach_host_shapes(st, host_shapes)
             lsi = torch.cat((st.new_zeros((1,)), st.prod(1).cumsum(0)[:-1]))
+            attach_host_shapes(st, host_shapes, lsi)     # checked once per shape set (cached)
             hit = (st, lsi)
             self._shape_cache[key] = hit
         return hit

@@ -330,8 +330,8 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         mask_embed = self.mask_embed(decoder_output)
         if fold is None:
             fold = decoder_ops.image_mask_fold(mask_features, self._lowp_features(mask_features))
-        outputs_mask = fold(mask_embed)
-        attn_mask = decoder_ops.attn_mask_bits(outputs_mask, attn_mask_target_size) if need_mask else None
+        outputs_mask, attn_mask = decoder_ops.mask_heads(fold, mask_embed,
+                                                         attn_mask_target_size if need_mask else None)
         return outputs_class, outputs_mask, attn_mask
 
     @torch.jit.unused

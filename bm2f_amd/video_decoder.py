@@ -95,6 +95,6 @@ class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder
         decoder_output = self.decoder_norm(output)
         outputs_class = self.class_embed(decoder_output)
         mask_embed = self.mask_embed(decoder_output)
-        outputs_mask = fold(mask_embed)  # (b, q, t, h, w): einsum "bqc,btchw->bqthw" (:449)
-        attn_mask = decoder_ops.attn_mask_bits(outputs_mask, size) if need_mask else None
+        # (b, q, t, h, w): einsum "bqc,btchw->bqthw" (:449) and the per-frame resized bitmask (:453-458)
+        outputs_mask, attn_mask = decoder_ops.mask_heads(fold, mask_embed, size if need_mask else None)
         return outputs_class, outputs_mask, attn_mask

@@ -63,7 +63,10 @@ int m2f_abi_version(void);
  *   output           (N, Lq, M*D)
  * host_spatial_shapes: optional host copy of spatial_shapes (L*2 int64, may be NULL).  When given
  * and Lq == S (encoder self-attention over the flattened pyramid) the backward groups queries by
- * spatial tile and accumulates grad_value in LDS windows; results do not depend on it.
+ * spatial tile and accumulates grad_value in LDS windows; results agree with the untiled path up to
+ * the order of fp32 additions.  That path takes each level's start as the prefix sum of the host
+ * shapes: the caller guarantees spatial_shapes == host_spatial_shapes and level_start_index == their
+ * prefix sums (the Python layer checks both once per tensor, bm2f_amd/msda.py attach_host_shapes).
  * ------------------------------------------------------------------------------------------- */
 int m2f_msda_fwd_f32(const float* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
                      const float* sampling_loc, const float* attn_weight,
@@ -109,9 +112,9 @@ int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int proj_ld, c
                            int spatial_size, int num_heads, int channels, int num_levels, int num_query,
                            int num_point, float* output, void* stream);
 
-/* workspace (optional, m2f_msda_fused_bwd_workspace() bytes, 16-byte aligned): with it every workgroup
- * leaves its window's grad_value partial rows in the workspace and a combine pass adds them in a fixed
- * order (plain stores, deterministic); without it (NULL) the rows are added with float atomics. */
+/* grad_value rows are added with fp32 atomics from the tiled workgroups' LDS windows (each window row is
+ * flushed once; values repeat to within fp32 rounding, not bit for bit).  The workspace arguments are kept
+ * for ABI stability: m2f_msda_fused_bwd_workspace() reports 0 bytes and the workspace is not read. */
 int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, int batch, int spatial_size, int num_heads,
                                  int channels, int num_levels, int num_point, int64_t* workspace_bytes);
 int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
@@ -134,6 +137,21 @@ int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, c
  * ------------------------------------------------------------------------------------------- */
 int m2f_attn_mask_bits(const void* logits, int dtype, int batch, int num_queries, int frames, int in_h,
                        int in_w, int out_h, int out_w, int row_fix, uint32_t* bits, int nwords, void* stream);
+
+/* Mask head with the bitmask epilogue (reference :437-452; video_..._decoder.py:444-461):
+ *   masks[b, q, t, n] = dtype( sum_c embed[b, q, c] * feats[b, c, t, n] )      (n = y * width + x)
+ * embed (B, Q, C), feats (B, C, frames, height, width), masks (B, Q, frames, height, width), all of `dtype`
+ * (bf16 or f16; fp32 accumulation).  With target_h > 0 it also writes into `bits` (zeroed, (B, Q, nwords))
+ * the blocked bits m2f_attn_mask_bits would compute from `masks` for (target_h, target_w) before its row
+ * fix; height / target_h = width / target_w must be an even integer dividing 128.  Constraints: C % 32 == 0,
+ * width % 8 == 0, Q <= 256, 16-byte aligned operands. */
+int m2f_mask_heads_fwd(int dtype, const void* embed, const void* feats, int batch, int num_queries, int channels,
+                       int frames, int height, int width, int target_h, int target_w, void* masks, uint32_t* bits,
+                       int nwords, void* stream);
+
+/* Fully-masked-row fix (:400) after m2f_mask_heads_fwd: each of `rows` bit rows whose `keys` bits are all set
+ * is cleared. */
+int m2f_mask_row_fix(uint32_t* bits, int rows, int nwords, int keys, void* stream);
 
 /* Work split of the masked attention for these sizes: keys are processed in `num_chunks` ranges of
  * `chunk_len`; the forward / backward need the returned fp32 workspace sizes (0 when one chunk). */

@@ -47,3 +47,24 @@ def test_group_norm_act_vs_fp64(device, shape, groups, relu, affine):
     y2 = group_norm_act(x2, norm, relu)
     y2.backward(g)
     assert torch.equal(y, y2) and torch.equal(x.grad, x2.grad)
+
+
+@pytest.mark.parametrize("offset", [100.0, 1000.0])
+def test_group_norm_large_mean(device, offset):
+    """|mean| >> std: the statistics are fp64 sums of fp64 squares, so the variance does not
+    cancel; what is left is the fp32 rounding of x itself and of y = x a + b', which torch's fp32 GroupNorm
+    shares -- the bar is "no worse than torch fp32 (+50%)" next to an absolute 1e-4 / 1e-3 vs fp64."""
+    torch.manual_seed(7)
+    norm = nn.GroupNorm(32, 256).to(device)
+    x = (torch.randn(2, 256, 32, 32, device=device) + offset).requires_grad_()
+    y = group_norm_act(x, norm, False)
+    g = torch.randn_like(y)
+    y.backward(g)
+    xd = x.detach().double().requires_grad_()
+    yd = F.group_norm(xd, 32, norm.weight.double(), norm.bias.double(), norm.eps)
+    yd.backward(g.double())
+    xt = x.detach().clone().requires_grad_()
+    yt = F.group_norm(xt, 32, norm.weight, norm.bias, norm.eps)
+    yt.backward(g)
+    assert _rel(y, yd) < max(1.5 * _rel(yt, yd), 1e-6) and _rel(y, yd) < 1e-4 * offset / 100
+    assert _rel(x.grad, xd.grad) < max(1.5 * _rel(xt.grad, xd.grad), 1e-5) and _rel(x.grad, xd.grad) < 1e-3

@@ -1,0 +1,136 @@
+"""Mask-heads kernel (csrc/mask_heads.hip) on the GPU: the einsum ``bqc,bchw->bqhw`` / ``bqc,btchw->bqthw``
+(reference mask2former_transformer_decoder.py:442, video_..._decoder.py:449) within one dtype ulp of the exact
+product of the same operands rounded once, and the fused attention bitmask bit-exact against the reference's
+resize + sigmoid + threshold + row fix (:446-449, :400 via oracle/decoder_ref.ref_attn_bool) applied to the
+kernel's own logits, and against the standalone m2f_attn_mask_bits kernel."""
+import pytest
+import torch
+
+from oracle.decoder_ref import ref_attn_bool, unpack_bits
+
+pytestmark = pytest.mark.gpu
+
+DT = {"f16": torch.float16, "bf16": torch.bfloat16}
+ULP = {"f16": 2.0 ** -10, "bf16": 2.0 ** -7}
+
+
+def _case(device, B, Q, C, T, H, W, dt, seed=0):
+    g = torch.Generator(device=device).manual_seed(seed)
+    e = torch.randn(B, Q, C, device=device, generator=g)
+    f = torch.randn(B, C, T, H, W, device=device, generator=g) / C ** 0.5
+    if Q > 6:
+        f[:, 0] = 1.0 / C ** 0.5          # a constant channel: rows that are blocked everywhere
+        e[-1, 3] = 0.0
+        e[-1, 3, 0] = -40.0               # logits -2.5 everywhere -> a fully blocked row, cleared by the fix
+        e[0, 4] = 0.0                     # logits exactly 0: sigmoid 0.5, not blocked
+        e[0, 5] *= 1e-3                   # logits straddling 0
+        e[0, 6] *= 3e-2
+    return e.to(DT[dt]), f.to(DT[dt])
+
+
+def _fold(f, T):
+    from bm2f_amd import decoder_ops
+    B, C = f.shape[:2]
+    tail = f.shape[3:] if T == 1 else f.shape[2:]
+    return decoder_ops.MaskFeatureFold(f, f.reshape(B, C, -1), tuple(tail), lambda df, shape: df.view(shape))
+
+
+def _check_logits(out, e, f, dt):
+    """Within one dtype ulp of the exact (fp64) product of the same operands rounded once.  (An fp32 GEMM
+    rounded to the dtype is itself up to 1 ulp off that, so it is not the yardstick: the two may sit 2 ulp
+    apart near a binade edge, as measured with tools/dbg_mask_heads.py.)"""
+    B, C = f.shape[:2]
+    ref = torch.bmm(e.double(), f.double().reshape(B, C, -1)).to(out.dtype).view(out.shape)
+    d = (out.float() - ref.float()).abs()
+    bound = ref.float().abs() * ULP[dt] + 1e-6
+    assert bool((d <= bound).all()), f"logits beyond 1 ulp: max {d.max().item():.3g}"
+    assert (d > 0).float().mean().item() < 0.01
+
+
+CASES = [  # B, Q, C, T, H, W, target
+    (2, 100, 256, 1, 64, 64, (32, 32)),
+    (2, 100, 256, 1, 64, 64, (16, 16)),
+    (2, 100, 256, 1, 64, 64, (8, 8)),
+    (1, 200, 256, 1, 64, 96, (16, 24)),     # 7 query tiles, ragged column chunk
+    (2, 37, 64, 1, 40, 48, (5, 6)),         # odd row count with the offset pairing, partial tiles
+    (1, 20, 256, 3, 24, 40, (12, 20)),      # video: 3 frames, frame-major keys
+    (1, 20, 256, 3, 24, 40, (6, 10)),
+    (1, 20, 256, 3, 24, 48, (3, 6)),
+    (2, 7, 32, 1, 16, 16, None),            # einsum only
+]
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "x".join(map(str, c[:6])) + f"-{c[6]}")
+def test_mask_heads_exact(device, dt, case):
+    from bm2f_amd import decoder_ops
+    B, Q, C, T, H, W, size = case
+    e, f = _case(device, B, Q, C, T, H, W, dt)
+    fold = _fold(f, T)
+    assert fold.fused_ok(Q, size)
+    out, bits = decoder_ops.mask_heads(fold, e, size)
+    torch.cuda.synchronize()
+    want_shape = (B, Q, H, W) if T == 1 else (B, Q, T, H, W)
+    assert out.shape == want_shape and out.dtype == DT[dt]
+    _check_logits(out, e, f, dt)
+    if size is None:
+        assert bits is None
+        return
+    keys = T * size[0] * size[1]
+    got = unpack_bits(bits, keys)
+    want = ref_attn_bool(out, size)
+    assert torch.equal(got, want), f"{(got != want).sum().item()} mask bits differ"
+    assert torch.equal(bits, decoder_ops.attn_mask_bits(out, size))   # tail bits included
+    if Q > 6:
+        assert not got[-1, 3].any()                # the fully blocked row was cleared
+        nofix = ref_attn_bool(out, size, row_fix=False)
+        assert nofix[-1, 3].all()
+
+
+def test_mask_heads_full_size(device):
+    """1024^2 input: 256^2 mask features, Q = 100, the three pyramid targets, bf16."""
+    from bm2f_amd import decoder_ops
+    e, f = _case(device, 2, 100, 256, 1, 256, 256, "bf16", seed=3)
+    fold = _fold(f, 1)
+    for size in [(32, 32), (64, 64), (128, 128)]:
+        out, bits = decoder_ops.mask_heads(fold, e, size)
+        _check_logits(out, e, f, "bf16")
+        assert torch.equal(unpack_bits(bits, size[0] * size[1]), ref_attn_bool(out, size))
+
+
+def test_mask_heads_fallback_shapes(device):
+    """Shapes the kernel does not take (non-integer ratio, fp32) go through bmm + m2f_attn_mask_bits."""
+    from bm2f_amd import decoder_ops
+    e, f = _case(device, 1, 10, 32, 1, 50, 70, "bf16")
+    fold = _fold(f, 1)
+    assert not fold.fused_ok(10, (13, 17))
+    out, bits = decoder_ops.mask_heads(fold, e, (13, 17))
+    assert torch.equal(unpack_bits(bits, 13 * 17), ref_attn_bool(out, (13, 17)))
+    f32 = _fold(f.float(), 1)
+    assert not f32.fused_ok(10, (25, 35))
+
+
+def test_mask_heads_backward(device):
+    """Gradients through the fused forward equal those of the bmm-forward fold (same backward)."""
+    from bm2f_amd import decoder_ops
+    e0, f0 = _case(device, 2, 100, 256, 1, 32, 32, "bf16", seed=5)
+    grads = []
+    for fused in (True, False):
+        e = e0.float().clone().requires_grad_()
+        f = f0.float().clone().requires_grad_()
+        fold = decoder_ops.MaskFeatureFold(f, f.detach().to(torch.bfloat16).reshape(2, 256, -1), (32, 32),
+                                           lambda df, shape: df.view(shape))
+        outs = []
+        for size in [(16, 16), (8, 8), None]:
+            if fused:
+                o, _ = decoder_ops.mask_heads(fold, e * (1 + len(outs)), size)
+            else:
+                o = fold(e * (1 + len(outs)))
+            outs.append(o)
+        sum((o.float() * (i + 1)).sum() for i, o in enumerate(outs)).backward()
+        grads.append((e.grad, f.grad, [o.detach() for o in outs]))
+    (ge1, gf1, o1), (ge2, gf2, o2) = grads
+    for a, b in zip(o1, o2):
+        assert ((a.float() - b.float()).abs() <= b.float().abs() * 2 * ULP["bf16"] + 1e-6).all()   # 1 ulp each
+    assert torch.equal(ge1, ge2)
+    assert torch.equal(gf1, gf2)
