@@ -29,7 +29,10 @@ __device__ __forceinline__ void tap_shift(int T, int tap, int& dy, int& dx) {
   dx = T == 9 ? tap % 3 - 1 : 0;
 }
 
-// Bs[c][p][n][16] (swizzled rows, NP rows) for the conv GEMM: k = tap * Ca + ci_a, c = k / 16.
+// Bs[c][p][n][16] (swizzled rows, NP rows) for the conv GEMM.  Chunk c holds channels 16 (c / T) .. +15 of
+// tap c % T: the taps of one channel group are adjacent in k, so the pixel rows a block loads for one tap are
+// re-read by the next taps from L1/L2 (tap-major k swept all channels per tap: the 3x3 forward then fetched
+// its input about ten times from HBM, r02_a).
 // mode 0 (forward):  n = co, Ca = Ci, value W[co][ci][tap]
 // mode 1 (dgrad):    n = ci, Ca = Co, value W[co][ci][T-1-tap]
 __global__ void __launch_bounds__(256) x3_conv_presplit(const float* __restrict__ Wt, int Co, int Ci, int T, int mode,
@@ -41,7 +44,7 @@ __global__ void __launch_bounds__(256) x3_conv_presplit(const float* __restrict_
   bf8 pl[3][2];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int k = c * 16 + j, tap = k / Ca, ca = k - tap * Ca;
+    const int tap = c % T, ca = (c / T) * 16 + j;
     float v = 0.f;
     if (n < Nn && tap < T) {
       const int co = mode == 0 ? n : ca, ci = mode == 0 ? ca : n, tp = mode == 0 ? tap : T - 1 - tap;
@@ -79,7 +82,23 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
   __bf16(*sb)[CHUNK] = reinterpret_cast<__bf16(*)[CHUNK]>(smem);
 
   const int HW = H * W;
-  const int n = blockIdx.z, n20 = blockIdx.y * BN, p0 = blockIdx.x * 128;
+  // 3x3: 1-D grid with the grouped XCD remap (runs of 16 pixel tiles = 8 rows at W = 256 per XCD), so the
+  // rows a tap shares with the neighbouring tiles are fetched into one L2 instead of three (fetch 4.5 -> 1.6 GB
+  // per launch at config 2).  1x1 has no such reuse and keeps the 3-D grid (its 252 VGPRs leave no room for
+  // the index math: it spilled and ran 2.9x slower)
+  int n, n20, p0;
+  if constexpr (T == 9) {
+    const int np = HW / 128, nct = (Cout + BN - 1) / BN;
+    const int id = xcd_group_remap(blockIdx.x, gridDim.x, 16);
+    const int pt = id % np, rest = id / np;
+    n = rest / nct;
+    n20 = (rest - n * nct) * BN;
+    p0 = pt * 128;
+  } else {
+    n = blockIdx.z;
+    n20 = blockIdx.y * BN;
+    p0 = blockIdx.x * 128;
+  }
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int pix = p0 + w * 32 + li, py = pix / W, px = pix - py * W;
@@ -93,7 +112,10 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
   };
   auto gload = [&](Regs& r, int c) {
     const int cc = min(c, nk - 1);
-    const int tap = cc / cpt, ci0 = (cc - tap * cpt) * kBK + lh * 8;
+    // channel-group major for 3x3; 1x1 keeps the old form (its allocation sits at 252 VGPRs: the compiler
+    // spilled 53 on the equivalent cc * 16)
+    const int tap = T == 9 ? cc % T : cc / cpt;
+    const int ci0 = (T == 9 ? cc / T : cc - tap * cpt) * kBK + lh * 8;
     int dy, dx;
     tap_shift(T, tap, dy, dx);
     const int yy = py + dy, xx = px + dx;
@@ -113,7 +135,7 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
     for (int u = 0; u < NBL; ++u) *reinterpret_cast<bf8*>(&sb[buf][(tid + u * NT) * 8]) = r.b[u];
   };
   auto asplit = [&](const Regs& r, int c, bf8 (&fa)[3]) {
-    const int tap = c / cpt;
+    const int tap = T == 9 ? c % T : c / cpt;
     int dy, dx;
     tap_shift(T, tap, dy, dx);
     const int yy = py + dy, xx = px + dx;
@@ -469,11 +491,14 @@ extern "C" int m2f_conv_f32x3(const float* I, const float* Wt, const float* bias
   x3_conv_presplit<<<m2f::ceil_div(static_cast<int64_t>(nchunks) * NP, 256), 256, 0, st>>>(Wt, Co, Ci, T, mode, NP,
                                                                                           nchunks, Bs);
   if ((rc = m2f::check_launch(fn))) return rc;
-  const dim3 grid((H * W) / 128, (Nn + 255) / 256, N);
-  if (T == 9)
-    x3_conv_kernel<9><<<grid, 256, 0, st>>>(I, Ca, H, W, Bs, NP, bias, O, Nn);
-  else
+  if (T == 9) {
+    const int64_t nblk = static_cast<int64_t>((H * W) / 128) * ((Nn + 255) / 256) * N;
+    if (nblk > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many tiles", fn);
+    x3_conv_kernel<9><<<static_cast<unsigned>(nblk), 256, 0, st>>>(I, Ca, H, W, Bs, NP, bias, O, Nn);
+  } else {
+    const dim3 grid((H * W) / 128, (Nn + 255) / 256, N);
     x3_conv_kernel<1><<<grid, 256, 0, st>>>(I, Ca, H, W, Bs, NP, bias, O, Nn);
+  }
   return m2f::check_launch(fn);
 }
 

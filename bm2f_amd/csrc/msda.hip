@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // ------------------------------------------------------------------------------------------------
 // fp32 backward, spatially tiled: encoder self-attention (Lq == S, query i = pyramid position i).
 //
-// Workgroup = (spatial tile, head m, image n), 1024 threads.  A tile is the same normalised rectangle on
+// Workgroup = (spatial tile, head m, image n), 512 threads (two per CU).  A tile is the same normalised rectangle on
 // every level (level l's tile ty spans rows [ty*H_l/nty, (ty+1)*H_l/nty)), so its queries at every level
 // sample the same neighbourhood of every level.
 //
@@ -356,7 +356,7 @@ __device__ __forceinline__ int window_cell(const TileState& ts, int l, int h0, i
 
 // STAMP (diagnostic builds only, M2F_DIAG): s_memtime at the phase barriers of each workgroup into `stamps`;
 // NOFLUSH (diagnostic builds only): phase 3 without its HBM adds, to price them.
-// TPB threads per workgroup: 1024 (one workgroup per CU, 16x16 tiles) or 512 (two per CU, 16x8 tiles).
+// TPB threads per workgroup: 512 (two workgroups per CU, 12x12 tiles; the default) or 1024 (one, 16x16 tiles).
 template <int LT, bool FUSED, int TPB, bool STAMP = false, bool NOFLUSH = false>
 __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,

@@ -33,6 +33,16 @@ __device__ __forceinline__ int xcd_remap(int id, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + id / 8;
 }
 
+// grouped XCD remap: blocks are dealt to XCDs round-robin (b % 8), so consecutive block ids cover one group
+// of 8*G logical tiles at a time (the chip streams one contiguous region, spread over all HBM channels) and
+// XCD b % 8 gets the contiguous run of G tiles inside it (neighbouring tiles share one L2).  Bijective:
+// the partial last group keeps identity order.
+__device__ __forceinline__ int xcd_group_remap(int b, int nwg, int G) {
+  const int span = 8 * G, group = b / span, within = b - group * span;
+  if ((group + 1) * span > nwg) return b;
+  return group * span + (within & 7) * G + (within >> 3);
+}
+
 // x -> (h, m, l) exactly (x = h + m + l to the last fp32 bit); non-finite x keeps h = x, m = l = 0
 __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l) {
   h = static_cast<__bf16>(x);
