@@ -140,12 +140,10 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
     tap_shift(T, tap, dy, dx);
     const int yy = py + dy, xx = px + dx;
     const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
+    float v[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      __bf16 h, m, l;
-      split3(ok ? r.a[e] : 0.f, h, m, l);
-      fa[0][e] = h; fa[1][e] = m; fa[2][e] = l;
-    }
+    for (int e = 0; e < 8; ++e) v[e] = ok ? r.a[e] : 0.f;
+    split8(v, fa);
   };
 
   f16v acc[TJ];
@@ -287,19 +285,18 @@ __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __re
 #pragma unroll
     for (int u = 0; u < NJ; ++u) {
       const int job = tid + u * NT, half = job / BN, cl = job % BN;
-      bf8 h, mm, l;
+      float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float v = live ? r.b[u][e >> 2][e & 3] : 0.f;
-        if (csum) csb[u] += v;
-        __bf16 x, y, z;
-        split3(v, x, y, z);
-        h[e] = x; mm[e] = y; l[e] = z;
+        v[e] = live ? r.b[u][e >> 2][e & 3] : 0.f;
+        if (csum) csb[u] += v[e];
       }
+      bf8 pl[3];
+      split8(v, pl);
       const int off = cl * 16 + ((half ^ swz(cl)) * 8);
-      *reinterpret_cast<bf8*>(&sb[buf][off]) = h;
-      *reinterpret_cast<bf8*>(&sb[buf][BN * 16 + off]) = mm;
-      *reinterpret_cast<bf8*>(&sb[buf][2 * BN * 16 + off]) = l;
+      *reinterpret_cast<bf8*>(&sb[buf][off]) = pl[0];
+      *reinterpret_cast<bf8*>(&sb[buf][BN * 16 + off]) = pl[1];
+      *reinterpret_cast<bf8*>(&sb[buf][2 * BN * 16 + off]) = pl[2];
     }
   };
   auto asplit = [&](const Regs& r, int c, bf8 (&fa)[3]) {
@@ -326,11 +323,8 @@ __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __re
       if (dx > 0 && x0 + 8 >= W) v[7] = 0.f;  // right of the row
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      __bf16 h, mm, l;
-      split3(rok ? v[e] : 0.f, h, mm, l);
-      fa[0][e] = h; fa[1][e] = mm; fa[2][e] = l;
-    }
+    for (int e = 0; e < 8; ++e) v[e] = rok ? v[e] : 0.f;
+    split8(v, fa);
   };
 
   f16v acc[TJ];

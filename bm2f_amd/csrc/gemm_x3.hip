@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(256) x3_presplit(const float* __restrict__ B, 
   }
 }
 
-template <int BN, int NW, int EPI>
+template <int BN, int NW, int EPI, bool KFULL>
 __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restrict__ A, int64_t lda,
                                                        const __bf16* __restrict__ Bs, int NP,
                                                        const float* __restrict__ bias,
@@ -144,12 +144,10 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
   };
   auto asplit = [&](const Regs& r, int c, bf8 (&fa)[3]) {
     const int k = c * kBK + lh * 8;
+    float x[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      __bf16 h, m, l;
-      split3(k + e < K ? r.a[e >> 2][e & 3] : 0.f, h, m, l);
-      fa[0][e] = h; fa[1][e] = m; fa[2][e] = l;
-    }
+    for (int e = 0; e < 8; ++e) x[e] = KFULL || k + e < K ? r.a[e >> 2][e & 3] : 0.f;
+    split8(x, fa);
   };
 
   f16v acc[TJ];
@@ -179,26 +177,28 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
     }
   };
 
+  // Pipeline: global loads two chunks ahead in two register sets (unrolled by 2 so the sets are static);
+  // chunk c+1 is written to the other LDS buffer and split into the other fragment set while chunk c's
+  // MFMAs drain; one barrier per chunk.  Branch-free (past the end the loads are clamped to the last chunk
+  // and the stores go to the buffer no one reads again), so the split can interleave with the MFMAs
+  // (a three-deep ring measured slower: 217 VGPRs).
   Regs r0, r1;
-  bf8 fa[3];
+  bf8 fa[3], fb[3];
   gload(r0, 0);
   gload(r1, 1);
   bstore(r0, 0);
   asplit(r0, 0, fa);
   __syncthreads();
-  // iteration c: loads for c+2 into the set chunk c used; chunk c+1 (other set) to LDS + split
-  auto step = [&](int c, Regs& cur, Regs& nxt) {
-    if (c + 2 < nk) gload(cur, c + 2);
-    chunk_mfma(c & 1, fa);
-    if (c + 1 < nk) {
-      bstore(nxt, (c + 1) & 1);
-      asplit(nxt, c + 1, fa);
-    }
+  auto step = [&](int c, Regs& cur, const Regs& nxt, const bf8 (&fc)[3], bf8 (&fn)[3]) {
+    gload(cur, c + 2);
+    chunk_mfma(c & 1, fc);
+    bstore(nxt, (c + 1) & 1);
+    asplit(nxt, c + 1, fn);
     __syncthreads();
   };
   for (int c = 0; c < nk; c += 2) {
-    step(c, r0, r1);
-    if (c + 1 < nk) step(c + 1, r1, r0);
+    step(c, r0, r1, fa, fb);
+    if (c + 1 < nk) step(c + 1, r1, r0, fb, fa);
   }
 
   // ---- epilogue -----------------------------------------------------------------------------------
@@ -265,8 +265,11 @@ int launch_nt(int epi, const float* A, int64_t lda, const __bf16* Bs, int NP, co
   const int64_t nwg = static_cast<int64_t>((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (nwg > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "m2f_gemm_f32x3_nt: too many tiles");
   const dim3 grid(static_cast<unsigned>(nwg)), block(64 * NW);
-#define M2F_X3NT(E) x3_nt_kernel<BN, NW, E><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, \
-                                                       M, N, K)
+#define M2F_X3NT(E)                                                                                            \
+  (K % kBK == 0 ? x3_nt_kernel<BN, NW, E, true><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, \
+                                                                       C, ldc, M, N, K)                           \
+                : x3_nt_kernel<BN, NW, E, false><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, D1, D2,     \
+                                                                        ldd, C, ldc, M, N, K))
   switch (epi) {
     case kNone: M2F_X3NT(kNone); break;
     case kBias: M2F_X3NT(kBias); break;
@@ -303,7 +306,7 @@ int64_t nt_workspace(int N, int K) {
 // column x 8 rows: one 16-byte store per plane).  Two-deep register prefetch, one barrier per chunk.
 // C tiles leave through a per-wave LDS image as float4 rows (transposed when the operands were swapped).
 // ---------------------------------------------------------------------------------------------------
-template <int NW>
+template <int NW, bool MFULL, int CSUM>   // MFULL: every chunk is 16 full rows; CSUM: 0 none, 1 of A, 2 of B
 __global__ void __launch_bounds__(64 * NW, 2) x3_tn_kernel(const float* __restrict__ A, int64_t lda,
                                                            const float* __restrict__ B, int64_t ldb, int M, int N1,
                                                            int N2, int rows_per_split, int trans_out,
@@ -331,8 +334,8 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_tn_kernel(const float* __restri
   const int acol = min(n10 + w * 32 + li, N1 - 1);
   const float* ap = A + acol;
   const int nk = r1 > r0 ? (r1 - r0 + kBK - 1) / kBK : 0;
-  const bool csum_a = colsum_slab != nullptr && !colsum_b && b2 == 0;
-  const bool csum_b = colsum_slab != nullptr && colsum_b && b1 == 0;
+  const bool csum_a = CSUM == 1 && b2 == 0;
+  const bool csum_b = CSUM == 2 && b1 == 0;
 
   struct Regs {
     float a[8];
@@ -360,31 +363,29 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_tn_kernel(const float* __restri
       const int job = tid + u * NT;
       if (JOBS % NT != 0 && job >= JOBS) continue;
       const int half = job / BN, col = job % BN;
-      bf8 h, mm, l;
+      float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float v = m + half * 8 + e < r1 ? r.b[u][e] : 0.f;
-        if (csum_b) csb[u] += v;
-        __bf16 x, y, z;
-        split3(v, x, y, z);
-        h[e] = x; mm[e] = y; l[e] = z;
+        v[e] = MFULL || m + half * 8 + e < r1 ? r.b[u][e] : 0.f;
+        if constexpr (CSUM == 2) csb[u] += csum_b && c < nk ? v[e] : 0.f;
       }
+      bf8 pl[3];
+      split8(v, pl);
       const int off = col * 16 + ((half ^ swz(col)) * 8);
-      *reinterpret_cast<bf8*>(&sb[buf][off]) = h;
-      *reinterpret_cast<bf8*>(&sb[buf][BN * 16 + off]) = mm;
-      *reinterpret_cast<bf8*>(&sb[buf][2 * BN * 16 + off]) = l;
+      *reinterpret_cast<bf8*>(&sb[buf][off]) = pl[0];
+      *reinterpret_cast<bf8*>(&sb[buf][BN * 16 + off]) = pl[1];
+      *reinterpret_cast<bf8*>(&sb[buf][2 * BN * 16 + off]) = pl[2];
     }
   };
   auto asplit = [&](const Regs& r, int c, bf8 (&fa)[3]) {
     const int m = r0 + c * kBK + lh * 8;
+    float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const float v = m + e < r1 ? r.a[e] : 0.f;
-      if (csum_a) csa += v;
-      __bf16 h, mm, l;
-      split3(v, h, mm, l);
-      fa[0][e] = h; fa[1][e] = mm; fa[2][e] = l;
+      v[e] = MFULL || m + e < r1 ? r.a[e] : 0.f;
+      if constexpr (CSUM == 1) csa += csum_a && c < nk ? v[e] : 0.f;
     }
+    split8(v, fa);
   };
 
   f16v acc[TJ];
@@ -414,25 +415,26 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_tn_kernel(const float* __restri
   };
 
   if (nk > 0) {
+    // as the NT pipeline: branch-free steps with two fragment sets.  Past the slab's end the loads are
+    // clamped in-bounds and the rows zeroed (m >= r1), so the extra chunk a step splits contributes nothing
+    // and its colsum terms are 0; its stores go to the buffer no one reads again.
     Regs r0s, r1s;
-    bf8 fa[3];
+    bf8 fa[3], fb[3];
     gload(r0s, 0);
-    if (nk > 1) gload(r1s, 1);
+    gload(r1s, 1);
     bstore(r0s, 0, 0);
     asplit(r0s, 0, fa);
     __syncthreads();
-    auto step = [&](int c, Regs& cur, Regs& nxt) {
-      if (c + 2 < nk) gload(cur, c + 2);
-      chunk_mfma(c & 1, fa);
-      if (c + 1 < nk) {
-        bstore(nxt, c + 1, (c + 1) & 1);
-        asplit(nxt, c + 1, fa);
-      }
+    auto step = [&](int c, Regs& cur, const Regs& nxt, const bf8 (&fc)[3], bf8 (&fn)[3]) {
+      gload(cur, c + 2);
+      chunk_mfma(c & 1, fc);
+      bstore(nxt, c + 1, (c + 1) & 1);
+      asplit(nxt, c + 1, fn);
       __syncthreads();
     };
     for (int c = 0; c < nk; c += 2) {
-      step(c, r0s, r1s);
-      if (c + 1 < nk) step(c + 1, r1s, r0s);
+      step(c, r0s, r1s, fa, fb);
+      if (c + 1 < nk) step(c + 1, r1s, r0s, fb, fa);
     }
   }
 
@@ -621,12 +623,21 @@ extern "C" int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, in
   const unsigned grid = static_cast<unsigned>(p.splits * p.tiles);
   // slab orientation is always [N1][N2] (the caller's): transposed store when swapped
   if (M > 0) {
-    if (p.nw == 3)
-      x3_tn_kernel<3><<<grid, 192, 0, st>>>(a, la, b, lb, M, p.n1, p.n2, p.rows, p.swap ? 1 : 0, slab,
-                                            colsum ? cslab : nullptr, p.swap ? 1 : 0);
-    else
-      x3_tn_kernel<4><<<grid, 256, 0, st>>>(a, la, b, lb, M, p.n1, p.n2, p.rows, p.swap ? 1 : 0, slab,
-                                            colsum ? cslab : nullptr, p.swap ? 1 : 0);
+    float* cs = colsum ? cslab : nullptr;
+    const int csum = colsum ? (p.swap ? 2 : 1) : 0;
+    const bool mfull = M % kBK == 0;
+#define M2F_TN(NWV, MF, CS)                                                                                        \
+  x3_tn_kernel<NWV, MF, CS><<<grid, 64 * NWV, 0, st>>>(a, la, b, lb, M, p.n1, p.n2, p.rows, p.swap ? 1 : 0, slab, cs, \
+                                                       p.swap ? 1 : 0)
+#define M2F_TN_CS(NWV, MF) \
+  (csum == 0 ? M2F_TN(NWV, MF, 0) : csum == 1 ? M2F_TN(NWV, MF, 1) : M2F_TN(NWV, MF, 2))
+    if (p.nw == 3) {
+      if (mfull) M2F_TN_CS(3, true); else M2F_TN_CS(3, false);
+    } else {
+      if (mfull) M2F_TN_CS(4, true); else M2F_TN_CS(4, false);
+    }
+#undef M2F_TN_CS
+#undef M2F_TN
     if (int rc = m2f::check_launch(fn)) return rc;
   }
   const int64_t n = static_cast<int64_t>(N1) * N2;

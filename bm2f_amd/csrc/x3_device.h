@@ -53,6 +53,33 @@ __device__ __forceinline__ void split3(float x, __bf16& h, __bf16& m, __bf16& l)
   if (!isfinite(x)) { m = static_cast<__bf16>(0.f); l = static_cast<__bf16>(0.f); }
 }
 
+// split3 of 8 consecutive values into the three bf8 planes of an MFMA operand, a pair of values per
+// v_cvt_pk_bf16_f32 and back-conversions by shifts / masks of the packed word: 15 VALU per pair, no
+// branches (so the compiler can interleave it with the MFMAs of the previous chunk).  Non-finite x: the
+// remainder x - h is NaN exactly then, and is replaced by 0 (h = x, m = l = 0, as split3).
+__device__ __forceinline__ void split8(const float (&x)[8], bf8 (&fa)[3]) {
+  using u4 = unsigned __attribute__((ext_vector_type(4)));
+  using b2 = __bf16 __attribute__((ext_vector_type(2)));
+  u4 h, m, l;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const float x0 = x[2 * p], x1 = x[2 * p + 1];
+    const unsigned hp = __builtin_bit_cast(unsigned, b2{static_cast<__bf16>(x0), static_cast<__bf16>(x1)});
+    float r0 = x0 - __uint_as_float(hp << 16), r1 = x1 - __uint_as_float(hp & 0xffff0000u);
+    r0 = r0 == r0 ? r0 : 0.f;
+    r1 = r1 == r1 ? r1 : 0.f;
+    const unsigned mp = __builtin_bit_cast(unsigned, b2{static_cast<__bf16>(r0), static_cast<__bf16>(r1)});
+    const float s0 = r0 - __uint_as_float(mp << 16), s1 = r1 - __uint_as_float(mp & 0xffff0000u);
+    const unsigned lp = __builtin_bit_cast(unsigned, b2{static_cast<__bf16>(s0), static_cast<__bf16>(s1)});
+    h[p] = hp;
+    m[p] = mp;
+    l[p] = lp;
+  }
+  fa[0] = __builtin_bit_cast(bf8, h);
+  fa[1] = __builtin_bit_cast(bf8, m);
+  fa[2] = __builtin_bit_cast(bf8, l);
+}
+
 // B images are rows of 16 bf16 (32 B) with the two 16-B halves swapped on rows whose bit 3 is set: the
 // dense image is then conflict-free for the 32x32x16 operand read (ds_read_b128 lane groups
 // {0-3,12-15,20-27}, ... cover all 64 banks once)
