@@ -134,6 +134,13 @@ ENTRIES = {
     "m2f_mask_heads_fwd": ("mask_heads_fwd", "hbm", lambda a: (
         2 * a[3] * a[6] * a[7] * a[8] * (a[5] + a[4]) + 2 * a[3] * a[4] * a[5] + 4 * a[3] * a[4] * a[13],
         2 * a[3] * a[4] * a[5] * a[6] * a[7] * a[8])),
+    # (dtype, g, f, B, Q, C, n, de, ws, wsb, stream): G and F read once
+    "m2f_mask_heads_bwd_embed": ("mask_heads_bwd_embed", "hbm", lambda a: (
+        2 * a[3] * a[6].value * (a[4] + a[5]) + 2 * a[3] * a[4] * a[5], 2 * a[3] * a[4] * a[5] * a[6].value)),
+    # (dtype, ptrs, H, et, B, Q, QP, C, n, out_dtype, df, stream): the heads' G read once, df written once
+    "m2f_mask_heads_bwd_feats": ("mask_heads_bwd_feats", "hbm", lambda a: (
+        2 * a[2] * a[4] * a[5] * a[8].value + (4 if a[9] == 0 else 2) * a[4] * a[7] * a[8].value,
+        2 * a[2] * a[4] * a[5] * a[7] * a[8].value)),
     "m2f_gemm_f32x3_nt": ("x3_gemm_nt", "mfma", lambda a: _x3(a[11], a[12], a[13])),
     "m2f_gemm_f32x3_nt_add": ("x3_gemm_nt", "mfma", lambda a: _x3(a[14], a[15], a[16])),
     "m2f_gemm_f32x3_tn": ("x3_gemm_tn", "mfma", lambda a: _x3(a[7], a[8], a[9])),
@@ -148,6 +155,8 @@ MFMA_NOTE = {
     "x3_conv": "as x3_gemm_nt (implicit-GEMM conv, 1x1 and 3x3)",
     "x3_conv_wgrad": "as x3_gemm_nt (1x1 conv weight gradients)",
     "mask_heads_fwd": "bqc,bchw->bqhw on bf16/f16 MFMA with the fused bitmask epilogue (HBM-bound: mfma_tflops)",
+    "mask_heads_bwd_embed": "d embed = G F^T on bf16/f16 MFMA, split over HW (HBM-bound: mfma_tflops)",
+    "mask_heads_bwd_feats": "d features = sum_h E_h^T G_h on bf16/f16 MFMA over the heads in place (HBM-bound)",
 }
 
 

@@ -35,6 +35,9 @@ _SIGNATURES = {
     "m2f_attn_mask_bits": [_p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _i, _p],
     "m2f_mask_heads_fwd": [_i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _i, _p],
     "m2f_mask_row_fix": [_p, _i, _i, _i, _p],
+    "m2f_mask_heads_bwd_workspace": [_i, _i, _l, _p],
+    "m2f_mask_heads_bwd_embed": [_i, _p, _p, _i, _i, _i, _l, _p, _p, _l, _p],
+    "m2f_mask_heads_bwd_feats": [_i, _p, _i, _p, _i, _i, _i, _i, _l, _i, _p, _p],
     "m2f_masked_attn_plan": [_i, _i, _i, _i, _p, _p, _p, _p],
     "m2f_masked_attn_fwd": [_i, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _f, _p, _p, _p, _l, _p],
     "m2f_masked_attn_bwd": [_i, _p, _p, _p, _p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _f, _p, _p, _p, _p,

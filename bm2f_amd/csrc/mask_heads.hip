@@ -274,6 +274,225 @@ __global__ void __launch_bounds__(256) mask_row_fix_kernel(uint32_t* __restrict_
   for (int i = lane; i < nwords; i += 64) r[i] = 0u;
 }
 
+// ---- backward --------------------------------------------------------------------------------------------
+// d embed = G F^T per head (G = d masks (B, Q, N), F = features (B, C, N), both N-contiguous).  Split over
+// N: grid (splits, B); each block computes the whole (QT*32) x 256 partial of its N range into
+// part[b][split][q][c] (fp32, q < Q), summed in a fixed order by mask_de_reduce_kernel.  4 waves, wave w:
+// channels 64 w .. 64 w + 63 (two 32-tiles) x all query tiles.  Per 32-deep k step the block's G slab
+// (QT*32 rows x 32) is staged once in LDS (rows padded to 80 B: conflict-free 16-byte A reads) and shared
+// by the waves; each wave's F fragments (its own channels) load straight from global memory.  Two steps of
+// global loads in flight in registers, LDS double-buffered, one barrier per step.  HBM-bound.
+constexpr int kDeThreads = 256, kDeK = 32, kDePitch = kDeK + 8;
+
+template <typename T, int QT>
+__global__ void __launch_bounds__(kDeThreads, 2) mask_de_kernel(const T* __restrict__ G, const T* __restrict__ F,
+                                                               int Q, int64_t N, int64_t ks, int splits,
+                                                               float* __restrict__ part) {
+  using E = MhElt<T>;
+  constexpr int C = 256, QP = 32 * QT;
+  constexpr int GP = QP * (kDeK / 8);                 // 16-byte G pieces per step
+  constexpr int GPT = (GP + kDeThreads - 1) / kDeThreads;
+  __shared__ __attribute__((aligned(16))) T sg[2][QP * kDePitch];
+  const int s = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  const int64_t k0 = s * ks, k1 = min(N, k0 + ks);
+  const int nsteps = static_cast<int>((k1 - k0 + kDeK - 1) / kDeK);
+  const T* gb = G + static_cast<int64_t>(b) * Q * N;
+  const T* f = F + static_cast<int64_t>(b) * C * N + static_cast<int64_t>(64 * w + li) * N + lh * 8;
+  struct Stage {
+    s8 g[GPT];
+    s8 f[2][2];   // [c-tile][k16 half]
+  };
+  // past the range (the tail of the last split, or the steps past nsteps) pieces are zero: k1 is a multiple of 16
+  auto load = [&](Stage& st, int step) {
+    const int64_t kb = k0 + static_cast<int64_t>(step) * kDeK;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+      const int p = tid + u * kDeThreads, row = p >> 2, kp = (p & 3) * 8;
+      st.g[u] = s8{0, 0, 0, 0, 0, 0, 0, 0};
+      if ((GP % kDeThreads == 0 || p < GP) && row < Q && kb + kp < k1)
+        st.g[u] = *reinterpret_cast<const s8*>(gb + static_cast<int64_t>(row) * N + kb + kp);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        st.f[j][h] = s8{0, 0, 0, 0, 0, 0, 0, 0};
+        if (kb + 16 * h < k1) st.f[j][h] = *reinterpret_cast<const s8*>(f + static_cast<int64_t>(32 * j) * N + kb + 16 * h);
+      }
+  };
+  auto gstore = [&](int buf, const Stage& st) {
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+      const int p = tid + u * kDeThreads;
+      if (GP % kDeThreads == 0 || p < GP) *reinterpret_cast<s8*>(&sg[buf][(p >> 2) * kDePitch + (p & 3) * 8]) = st.g[u];
+    }
+  };
+  f16v acc[QT][2];
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[qt][j][e] = 0.f;
+  auto compute = [&](int buf, const Stage& st) {
+    const T* base = &sg[buf][0];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int qt = 0; qt < QT; ++qt) {
+        const s8 a = *reinterpret_cast<const s8*>(base + (32 * qt + li) * kDePitch + 16 * h + 8 * lh);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[qt][j] = E::mma(a, st.f[j][h], acc[qt][j]);
+      }
+  };
+  Stage s0, s1;
+  load(s0, 0);
+  load(s1, 1);
+  gstore(0, s0);
+  __syncthreads();
+  // step t: compute on buffer t & 1 with F fragments of stage t; stage t + 1 goes to the other buffer,
+  // stage t + 2 is loaded into the set stage t used (unrolled by 2: static sets)
+  auto stepf = [&](int t, Stage& cur, Stage& nxt) {
+    compute(t & 1, cur);
+    gstore((t + 1) & 1, nxt);
+    load(cur, t + 2);
+    __syncthreads();
+  };
+  for (int t = 0; t < nsteps; t += 2) {
+    stepf(t, s0, s1);
+    if (t + 1 < nsteps) stepf(t + 1, s1, s0);
+  }
+  // C map of 32x32x16: lane column li (c), rows (e & 3) + 8 (e >> 2) + 4 lh (q)
+  float* out = part + (static_cast<int64_t>(b) * splits + s) * Q * C + 64 * w + li;
+#pragma unroll
+  for (int qt = 0; qt < QT; ++qt)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int q = 32 * qt + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        if (q < Q) out[static_cast<int64_t>(q) * C + 32 * j] = acc[qt][j][e];
+      }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) mask_de_reduce_kernel(const float* __restrict__ part, int splits,
+                                                            int64_t per_b, int64_t total, T* __restrict__ de) {
+  const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i >= total) return;
+  const int64_t b = i / per_b, r = i - b * per_b;
+  const float* p = part + b * splits * per_b + r;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 3 < splits; s += 4) {
+    a0 += p[(s + 0) * per_b];
+    a1 += p[(s + 1) * per_b];
+    a2 += p[(s + 2) * per_b];
+    a3 += p[(s + 3) * per_b];
+  }
+  for (; s < splits; ++s) a0 += p[s * per_b];
+  de[i] = MhElt<T>::from_f((a0 + a1) + (a2 + a3));
+}
+
+// d features = sum over heads h of E_h^T G_h, one pass over the heads' G (no concatenation):
+// df[b, c, n] = sum_{h, q} Et[b, c, h * QP + q] G_h[b, q, n], Et the embeds transposed and zero-padded to QP
+// (a multiple of 16) queries per head.  Block = (image, 128 columns of n), 4 waves, wave w: channels
+// 64 w .. 64 w + 63 (two 32-tiles) x the four 32-column tiles.  Per k-step (16 queries of one head) the G
+// rows are staged in LDS (rows padded to 320 B: the transposed ds_read_b64_tr_b16 of the B operand is
+// conflict-free), double-buffered with the next two steps' global loads in registers; the A fragments
+// (Et rows, L2-resident) load straight from global memory.  fp32 accumulation, one rounding to T.
+constexpr int kDfCols = 128, kDfPitch = kDfCols + 32, kDfMaxHeads = 16;
+
+struct DfHeads {
+  const void* g[kDfMaxHeads];
+};
+
+template <typename T, typename O>   // O: the features' dtype (T, or fp32 when autocast made T a copy)
+__global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T* __restrict__ Et, int H, int Q,
+                                                         int QP, int64_t N, int ncol, O* __restrict__ df) {
+  using E = MhElt<T>;
+  constexpr int C = 256;
+  constexpr int EPP = 16 / static_cast<int>(sizeof(O));       // output elements per 16-byte piece
+  __shared__ __attribute__((aligned(16))) T sg[2][16 * kDfPitch];
+  __shared__ __attribute__((aligned(16))) O so[4][32][32 + EPP];
+  const int cc = blockIdx.x % ncol, b = blockIdx.x / ncol;
+  const int64_t n0 = static_cast<int64_t>(cc) * kDfCols;
+  const int cw = static_cast<int>(min<int64_t>(kDfCols, N - n0));
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  const int KP = H * QP, nsteps = KP / 16, spq = QP / 16;
+  // staging: thread -> (k row tid >> 4, 8 columns (tid & 15) * 8) of the step's 16 x 128 G slab
+  const int sr = tid >> 4, scol = (tid & 15) * 8;
+  const bool cok = scol < cw;
+  auto gload = [&](int st) -> s8 {
+    s8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int h = st / spq, q = (st - h * spq) * 16 + sr;
+    if (cok && q < Q && st < nsteps)
+      v = *reinterpret_cast<const s8*>(static_cast<const T*>(heads.g[h]) + (static_cast<int64_t>(b) * Q + q) * N +
+                                       n0 + scol);
+    return v;
+  };
+  auto gstore = [&](int buf, s8 v) { *reinterpret_cast<s8*>(&sg[buf][sr * kDfPitch + scol]) = v; };
+  const T* et = Et + (static_cast<int64_t>(b) * C + 64 * w + li) * KP + lh * 8;
+  f16v acc[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[j][t][e] = 0.f;
+  const int gq = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  s8 r0 = gload(0), r1 = gload(1);
+  gstore(0, r0);
+  __syncthreads();
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    const s8 r2 = gload(st + 2);  // steps st + 1 (r1) and st + 2 (r2) in flight
+    s8 af[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) af[j] = *reinterpret_cast<const s8*>(et + static_cast<int64_t>(32 * j) * KP + st * 16);
+    const T* base = &sg[buf][0];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int col = 32 * t + 16 * (gq & 1) + 4 * pp;
+      const s4 lo = tr_read(base + (8 * lh + qq) * kDfPitch + col);
+      const s4 hi = tr_read(base + (8 * lh + 4 + qq) * kDfPitch + col);
+      const s8 bf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j][t] = E::mma(af[j], bf, acc[j][t]);
+    }
+    gstore(buf ^ 1, r1);
+    r1 = r2;
+    __syncthreads();
+  }
+  // epilogue: per 32x32 tile through the wave's LDS image, 16-byte stores (one rounding to O)
+  O* out = df + static_cast<int64_t>(b) * C * N + n0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        if constexpr (sizeof(O) == 4) so[w][(e & 3) + 8 * (e >> 2) + 4 * lh][li] = acc[j][t][e];
+        else so[w][(e & 3) + 8 * (e >> 2) + 4 * lh][li] = E::from_f(acc[j][t][e]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int u = 0; u < 32 * 32 / EPP / 64; ++u) {
+        const int piece = lane + 64 * u, row = piece / (32 / EPP), ce = (piece % (32 / EPP)) * EPP;
+        const int col = 32 * t + ce;
+        if (col < cw)
+          *reinterpret_cast<s8*>(out + static_cast<int64_t>(64 * w + 32 * j + row) * N + col) =
+              *reinterpret_cast<const s8*>(&so[w][row][ce]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
 template <typename T>
 int launch_mask_heads(const MhArgs& a, int QT, hipStream_t st, unsigned grid) {
   switch (QT) {
@@ -334,4 +553,95 @@ extern "C" int m2f_mask_row_fix(uint32_t* bits, int rows, int nwords, int keys, 
     return m2f::fail(M2F_EINVAL, "m2f_mask_row_fix: bad arguments");
   mask_row_fix_kernel<<<(rows + 3) / 4, 256, 0, static_cast<hipStream_t>(stream)>>>(bits, rows, nwords, keys);
   return m2f::check_launch("m2f_mask_row_fix");
+}
+
+namespace {
+int64_t de_splits(int64_t N) {
+  // ~512 blocks at bs16 (two per CU), k ranges of whole 16-steps
+  const int64_t target = 32;
+  int64_t ks = (N + target - 1) / target;
+  ks = (ks + 15) / 16 * 16;
+  return ks < 16 ? 16 : ks;
+}
+
+template <typename T>
+int launch_de(const void* G, const void* F, int B, int Q, int64_t N, float* part, void* de, hipStream_t st) {
+  const int64_t ks = de_splits(N);
+  const int splits = static_cast<int>((N + ks - 1) / ks);
+  const dim3 grid(splits, B);
+  const T* g = static_cast<const T*>(G);
+  const T* f = static_cast<const T*>(F);
+  switch ((Q + 31) / 32) {
+#define M2F_DE(N_) case N_: mask_de_kernel<T, N_><<<grid, kDeThreads, 0, st>>>(g, f, Q, N, ks, splits, part); break;
+    M2F_DE(1) M2F_DE(2) M2F_DE(3) M2F_DE(4)
+#undef M2F_DE
+    default: return m2f::fail(M2F_EUNSUPPORTED, "m2f_mask_heads_bwd_embed: %d queries (at most 128)", Q);
+  }
+  const int64_t per_b = static_cast<int64_t>(Q) * 256, total = per_b * B;
+  mask_de_reduce_kernel<T><<<m2f::ceil_div(total, 256), 256, 0, st>>>(part, splits, per_b, total, static_cast<T*>(de));
+  return M2F_OK;
+}
+}  // namespace
+
+extern "C" int m2f_mask_heads_bwd_workspace(int batch, int num_queries, int64_t n, int64_t* workspace_bytes) {
+  if (batch <= 0 || num_queries <= 0 || n <= 0 || !workspace_bytes)
+    return m2f::fail(M2F_EINVAL, "m2f_mask_heads_bwd_workspace: bad arguments");
+  const int64_t ks = de_splits(n), splits = (n + ks - 1) / ks;
+  *workspace_bytes = splits * batch * static_cast<int64_t>(num_queries) * 256 * 4;
+  return m2f::ok();
+}
+
+extern "C" int m2f_mask_heads_bwd_embed(int dtype, const void* grad_masks, const void* feats, int batch,
+                                        int num_queries, int channels, int64_t n, void* grad_embed, void* workspace,
+                                        int64_t workspace_bytes, void* stream) {
+  const char* fn = "m2f_mask_heads_bwd_embed";
+  if (!grad_masks || !feats || !grad_embed || !workspace) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (dtype != M2F_BF16 && dtype != M2F_F16) return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  if (channels != 256 || n % 16 || num_queries <= 0 || num_queries > 128 || batch <= 0)
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs 256 channels, n %% 16 == 0, 1..128 queries", fn);
+  if (!m2f::aligned(grad_masks, 16) || !m2f::aligned(feats, 16)) return m2f::fail(M2F_EINVAL, "%s: alignment", fn);
+  int64_t need = 0;
+  m2f_mask_heads_bwd_workspace(batch, num_queries, n, &need);
+  if (workspace_bytes < need) return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld", fn,
+                                               static_cast<long long>(workspace_bytes), static_cast<long long>(need));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(workspace);
+  const int rc = dtype == M2F_BF16 ? launch_de<__bf16>(grad_masks, feats, batch, num_queries, n, part, grad_embed, st)
+                                   : launch_de<_Float16>(grad_masks, feats, batch, num_queries, n, part, grad_embed, st);
+  if (rc) return rc;
+  return m2f::check_launch(fn);
+}
+
+extern "C" int m2f_mask_heads_bwd_feats(int dtype, const void* const* grad_masks, int heads, const void* embed_t,
+                                        int batch, int num_queries, int padded_queries, int channels, int64_t n,
+                                        int out_dtype, void* grad_feats, void* stream) {
+  const char* fn = "m2f_mask_heads_bwd_feats";
+  if (!grad_masks || !embed_t || !grad_feats) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (dtype != M2F_BF16 && dtype != M2F_F16) return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  if (heads <= 0 || heads > kDfMaxHeads || channels != 256 || n % 8 || padded_queries % 16 ||
+      padded_queries < num_queries || num_queries <= 0 || batch <= 0)
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs 1..%d heads, 256 channels, n %% 8 == 0, padded queries %% 16", fn,
+                     kDfMaxHeads);
+  DfHeads h{};
+  for (int i = 0; i < heads; ++i) {
+    if (!grad_masks[i] || !m2f::aligned(grad_masks[i], 16)) return m2f::fail(M2F_EINVAL, "%s: head %d pointer", fn, i);
+    h.g[i] = grad_masks[i];
+  }
+  if (!m2f::aligned(embed_t, 16) || !m2f::aligned(grad_feats, 16)) return m2f::fail(M2F_EINVAL, "%s: alignment", fn);
+  const int ncol = static_cast<int>((n + kDfCols - 1) / kDfCols);
+  const int64_t nblk = static_cast<int64_t>(ncol) * batch;
+  if (nblk > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many workgroups", fn);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (out_dtype != dtype && out_dtype != M2F_F32) return m2f::fail(M2F_EUNSUPPORTED, "%s: out dtype %d", fn, out_dtype);
+  const unsigned g = static_cast<unsigned>(nblk);
+#define M2F_DF(T, O) \
+  mask_df_kernel<T, O><<<g, 256, 0, st>>>(h, static_cast<const T*>(embed_t), heads, num_queries, padded_queries, n, ncol, \
+                                          static_cast<O*>(grad_feats))
+  if (dtype == M2F_BF16) {
+    if (out_dtype == M2F_F32) M2F_DF(__bf16, float); else M2F_DF(__bf16, __bf16);
+  } else {
+    if (out_dtype == M2F_F32) M2F_DF(_Float16, float); else M2F_DF(_Float16, _Float16);
+  }
+#undef M2F_DF
+  return m2f::check_launch(fn);
 }

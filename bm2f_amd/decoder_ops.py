@@ -178,7 +178,8 @@ class _FoldGate(Function):
     """Identity gate between the mask features and every folded einsum.  Its output is an empty token
     the einsums take as an input, so autograd runs this backward only after every einsum's backward
     has run (each stashes its embed and incoming gradient on the fold); it then returns
-    d feats = sum_i E_i^T G_i as one GEMM with fp32 accumulation over K = sum_i Q_i."""
+    d feats = sum_i E_i^T G_i with fp32 accumulation over K = sum_i Q_i and one rounding: on the HIP kernel
+    that reads the heads' gradients in place (bf16 / fp16), else as one GEMM over their concatenation."""
 
     @staticmethod
     def forward(ctx, feats, state):
@@ -193,9 +194,13 @@ class _FoldGate(Function):
         if not items:
             return None, None
         shape, dtype = ctx.feats_meta
-        e = items[0][0] if len(items) == 1 else torch.cat([it[0] for it in items], dim=1)   # (B, K, C)
-        g = items[0][1] if len(items) == 1 else torch.cat([it[1] for it in items], dim=1)   # (B, K, N)
+        es, gs = [it[0] for it in items], [it[1] for it in items]
         del items
+        if _fold_fusable(es, gs, dtype):
+            return state.to_feats(mask_heads_bwd_feats(es, gs, dtype), shape), None
+        e = es[0] if len(es) == 1 else torch.cat(es, dim=1)   # (B, K, C)
+        g = gs[0] if len(gs) == 1 else torch.cat(gs, dim=1)   # (B, K, N)
+        del es, gs
         et = e.transpose(1, 2)
         if g.is_cuda and g.dtype != dtype:
             df = torch.bmm(et, g, out_dtype=dtype)      # fp32 accumulate, one rounding to the feats' dtype
@@ -212,13 +217,63 @@ class _FoldState:
         self.to_feats = to_feats
 
 
+def _bwd_fusable(f, g) -> bool:
+    """Shapes / dtypes of the mask-head backward kernels (csrc/mask_heads.hip)."""
+    B, C, N = f.shape
+    return (f.is_cuda and f.dtype in (torch.bfloat16, torch.float16) and g.dtype == f.dtype and C == 256
+            and N % 16 == 0 and g.shape[1] <= 128 and f.is_contiguous() and g.is_contiguous()
+            and f.data_ptr() % 16 == 0 and g.data_ptr() % 16 == 0)
+
+
+def _fold_fusable(es, gs, out_dtype) -> bool:
+    g0 = gs[0]
+    return (len(gs) <= 16 and g0.is_cuda and g0.dtype in (torch.bfloat16, torch.float16)
+            and out_dtype in (torch.float32, g0.dtype) and es[0].shape[2] == 256 and g0.shape[2] % 8 == 0
+            and all(g.shape == g0.shape and g.dtype == g0.dtype and g.is_contiguous() and g.data_ptr() % 16 == 0
+                    for g in gs)
+            and all(e.shape == es[0].shape and e.dtype == g0.dtype for e in es))
+
+
+def mask_heads_bwd_embed(g, f):
+    """d embed = g f^T: g (B, Q, N), f (B, 256, N) in bf16 / fp16 -> (B, Q, 256) in that dtype."""
+    B, C, N = f.shape
+    Q = g.shape[1]
+    wb = ctypes.c_int64()
+    _native.call("m2f_mask_heads_bwd_workspace", B, Q, ctypes.c_int64(N), ctypes.byref(wb))
+    ws = torch.empty((max(wb.value, 4) // 4,), dtype=torch.float32, device=g.device)
+    de = torch.empty((B, Q, C), dtype=g.dtype, device=g.device)
+    _native.call("m2f_mask_heads_bwd_embed", _code(g.dtype), g.data_ptr(), f.data_ptr(), B, Q, C, ctypes.c_int64(N),
+                 de.data_ptr(), ws.data_ptr(), ctypes.c_int64(wb.value), _stream(g))
+    return de
+
+
+def mask_heads_bwd_feats(es, gs, out_dtype):
+    """sum_h e_h^T g_h over the heads: e_h (B, Q, 256), g_h (B, Q, N) -> (B, 256, N) in out_dtype, without
+    concatenating the heads' gradients (the kernel takes their pointers)."""
+    B, Q, C = es[0].shape
+    N = gs[0].shape[2]
+    H = len(es)
+    QP = (Q + 15) // 16 * 16
+    et = torch.zeros((B, H, QP, C), dtype=es[0].dtype, device=es[0].device)
+    et[:, :, :Q] = torch.stack(es, 1)
+    et = et.permute(0, 3, 1, 2).reshape(B, C, H * QP).contiguous()
+    ptrs = (ctypes.c_void_p * H)(*[g.data_ptr() for g in gs])
+    df = torch.empty((B, C, N), dtype=out_dtype, device=gs[0].device)
+    _native.call("m2f_mask_heads_bwd_feats", _code(gs[0].dtype), ctypes.cast(ptrs, ctypes.c_void_p), H, et.data_ptr(),
+                 B, Q, QP, C, ctypes.c_int64(N), _code(out_dtype), df.data_ptr(), _stream(gs[0]))
+    return df
+
+
 def _folded_backward(ctx, grad):
     (e,) = ctx.saved_tensors
     fold = ctx.fold
     f = fold.feats_lp
     B, C, N = f.shape
-    g = grad.to(f.dtype).reshape(B, -1, N)
-    de = torch.bmm(g, f.transpose(1, 2)).to(ctx.edtype) if ctx.needs_input_grad[0] else None
+    g = grad.to(f.dtype).reshape(B, -1, N).contiguous()
+    de = None
+    if ctx.needs_input_grad[0]:
+        de = mask_heads_bwd_embed(g, f) if _bwd_fusable(f, g) else torch.bmm(g, f.transpose(1, 2))
+        de = de.to(ctx.edtype)
     tok = None
     if ctx.needs_input_grad[1]:
         fold.state.items.append((e, g))

@@ -153,6 +153,23 @@ int m2f_mask_heads_fwd(int dtype, const void* embed, const void* feats, int batc
  * is cleared. */
 int m2f_mask_row_fix(uint32_t* bits, int rows, int nwords, int keys, void* stream);
 
+/* Mask-head einsum backward (autograd of :442 / video :449), dtype bf16 or f16, fp32 accumulation.
+ * m2f_mask_heads_bwd_embed: grad_embed (B, Q, 256) = dtype( grad_masks (B, Q, n) . feats (B, 256, n)^T ), split
+ *   over n with fp32 partials summed in a fixed order; workspace from m2f_mask_heads_bwd_workspace.
+ *   Needs n % 16 == 0, Q <= 256.
+ * m2f_mask_heads_bwd_feats: grad_feats (B, 256, n) = out_dtype( sum_h embed_h^T . grad_masks_h ) over `heads`
+ *   heads' gradients (an array of device pointers, each (B, Q, n), no concatenation); embed_t is the
+ *   heads' embeds transposed, (B, 256, heads * padded_queries) with zero rows past Q in each head's
+ *   padded_queries (a multiple of 16) slots.  out_dtype = dtype, or M2F_F32 when the features are fp32
+ *   (autocast's copy): one rounding either way.  heads <= 16, n % 8 == 0. */
+int m2f_mask_heads_bwd_workspace(int batch, int num_queries, int64_t n, int64_t* workspace_bytes);
+int m2f_mask_heads_bwd_embed(int dtype, const void* grad_masks, const void* feats, int batch, int num_queries,
+                             int channels, int64_t n, void* grad_embed, void* workspace, int64_t workspace_bytes,
+                             void* stream);
+int m2f_mask_heads_bwd_feats(int dtype, const void* const* grad_masks, int heads, const void* embed_t, int batch,
+                             int num_queries, int padded_queries, int channels, int64_t n, int out_dtype,
+                             void* grad_feats, void* stream);
+
 /* Work split of the masked attention for these sizes: keys are processed in `num_chunks` ranges of
  * `chunk_len`; the forward / backward need the returned fp32 workspace sizes (0 when one chunk). */
 int m2f_masked_attn_plan(int batch, int num_queries, int num_keys, int num_heads, int* chunk_len,

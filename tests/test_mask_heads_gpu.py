@@ -110,6 +110,72 @@ def test_mask_heads_fallback_shapes(device):
     assert not f32.fused_ok(10, (25, 35))
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("B,Q,N", [(2, 100, 4096), (1, 7, 1040), (2, 37, 65536), (1, 128, 2064), (3, 65, 512)])
+def test_mask_heads_bwd_embed(device, dt, B, Q, N):
+    """d embed = G F^T (split over N, fp32 partials summed in a fixed order): within one dtype ulp of the
+    exact product rounded once, plus the fp32 accumulation error sqrt(N) 2^-24 sum|g f| that any fp32 GEMM
+    has on results that cancel (measured: torch's fp32 bmm is off by more there, tools/dbg_mask_bwd.py)."""
+    from bm2f_amd import decoder_ops
+    gen = torch.Generator(device=device).manual_seed(Q + N)
+    g = torch.randn(B, Q, N, device=device, generator=gen).to(DT[dt])
+    f = (torch.randn(B, 256, N, device=device, generator=gen) / 16).to(DT[dt])
+    de = decoder_ops.mask_heads_bwd_embed(g, f)
+    ref = torch.bmm(g.double(), f.double().transpose(1, 2)).to(DT[dt])
+    mag = torch.bmm(g.float().abs(), f.float().abs().transpose(1, 2))
+    d = (de.float() - ref.float()).abs()
+    bound = ref.float().abs() * ULP[dt] + mag * (N ** 0.5 * 2.0 ** -24) + 1e-6
+    assert bool((d <= bound).all()), f"max {d.max().item():.3g}"
+    assert decoder_ops._bwd_fusable(f, g)
+    assert not decoder_ops._bwd_fusable(f, torch.empty(B, 129, N, device=device, dtype=DT[dt]))  # -> torch.bmm
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("H,B,Q,N,out", [(10, 2, 100, 4096, "f32"), (10, 2, 100, 4096, "same"), (1, 1, 7, 200, "f32"),
+                                         (3, 2, 37, 1000, "same"), (16, 1, 20, 520, "f32")])
+def test_mask_heads_bwd_feats(device, dt, H, B, Q, N, out):
+    """d feats = sum_h E_h^T G_h over the heads' gradient buffers in place: fp32 output within fp32
+    accumulation error of the fp64 sum, dtype output within one ulp of it rounded once."""
+    from bm2f_amd import decoder_ops
+    gen = torch.Generator(device=device).manual_seed(H * 1000 + N)
+    es = [torch.randn(B, Q, 256, device=device, generator=gen).to(DT[dt]) for _ in range(H)]
+    gs = [torch.randn(B, Q, N, device=device, generator=gen).to(DT[dt]) for _ in range(H)]
+    odt = torch.float32 if out == "f32" else DT[dt]
+    assert decoder_ops._fold_fusable(es, gs, odt)
+    df = decoder_ops.mask_heads_bwd_feats(es, gs, odt)
+    ref = sum(torch.bmm(e.double().transpose(1, 2), g.double()) for e, g in zip(es, gs))
+    mag = sum(torch.bmm(e.float().abs().transpose(1, 2), g.float().abs()) for e, g in zip(es, gs))
+    acc_err = mag * ((H * Q) ** 0.5 * 2.0 ** -24)
+    if out == "f32":
+        assert bool(((df.double() - ref).abs() <= acc_err + ref.abs() * 2.0 ** -23 + 1e-6).all())
+    else:
+        r = ref.to(odt)
+        d = (df.float() - r.float()).abs()
+        assert bool((d <= r.float().abs() * ULP[dt] + acc_err + 1e-6).all()), f"max {d.max().item():.3g}"
+
+
+def test_mask_heads_backward_vs_fp64(device):
+    """Three heads through the fold (fused forward + the backward kernels) against fp64 autograd of the
+    einsums: embed and (fp32) feature gradients."""
+    from bm2f_amd import decoder_ops
+    e0, f0 = _case(device, 2, 100, 256, 1, 32, 32, "bf16", seed=7)
+    e = e0.float().clone().requires_grad_()
+    f = f0.float().clone().requires_grad_()
+    fold = decoder_ops.MaskFeatureFold(f, f.detach().to(torch.bfloat16).reshape(2, 256, -1), (32, 32),
+                                       lambda df, shape: df.view(shape))
+    # scales 1, 2, 4: exact in bf16, so the kernels see exactly ed * 2^i
+    outs = [decoder_ops.mask_heads(fold, e * 2 ** i, size)[0] for i, size in enumerate([(16, 16), (8, 8), None])]
+    gl = [torch.randn_like(o.float()) for o in outs]
+    sum((o.float() * gg).sum() for o, gg in zip(outs, gl)).backward()
+    ed = e0.double().requires_grad_()
+    fd = f0.double().requires_grad_()
+    od = [torch.einsum("bqc,bchw->bqhw", ed * 2 ** i, fd[:, :, 0]) for i in range(3)]
+    # the kernels see the bf16-rounded incoming gradients, as the reference's autocast GEMMs would
+    sum((o * gg.to(torch.bfloat16).double()).sum() for o, gg in zip(od, gl)).backward()
+    assert ((e.grad.double() - ed.grad).abs().max() / ed.grad.abs().max()).item() < 1e-2   # bf16 rounding of d embed
+    assert ((f.grad.double() - fd.grad).abs().max() / fd.grad.abs().max()).item() < 1e-4
+
+
 def test_mask_heads_backward(device):
     """Gradients through the fused forward equal those of the bmm-forward fold (same backward)."""
     from bm2f_amd import decoder_ops
