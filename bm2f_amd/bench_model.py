@@ -41,16 +41,43 @@ class FrozenBNConv(nn.Module):
         self.register_buffer("running_var", torch.ones(cout))
         self.eps = 1e-5
 
+    def _consts(self):
+        """(scale, shift) of the frozen BN, fp32; computed once per device (the buffers never change)."""
+        c = getattr(self, "_bn_consts", None)
+        if c is None or c[0].device != self.weight.device:
+            scale = self.weight * (self.running_var + self.eps).rsqrt()
+            c = (scale.contiguous(), (self.bias - self.running_mean * scale).contiguous())
+            self._bn_consts = c
+        return c
+
     def conv_shift(self, x):
         """(conv(x) with the BN scale folded into the weights, per-channel BN shift)."""
-        scale = self.weight * (self.running_var + self.eps).rsqrt()
-        shift = self.bias - self.running_mean * scale
-        w = self.conv.weight * scale.view(-1, 1, 1, 1)
+        scale, shift = self._consts()
+        w = _ScaledWeight.apply(self.conv.weight, scale, x.dtype)
         return F.conv2d(x, w, None, self.conv.stride, self.conv.padding), shift
 
     def forward(self, x):
         y, shift = self.conv_shift(x)
         return y + shift.view(1, -1, 1, 1).to(y.dtype)
+
+
+class _ScaledWeight(torch.autograd.Function):
+    """w * scale[co] in the conv's input dtype in one pass (autocast would multiply, then cast), and the
+    weight gradient back in fp32 in one pass."""
+
+    @staticmethod
+    def forward(ctx, w, scale, dtype):
+        out = torch.empty(w.shape, dtype=dtype, device=w.device)
+        torch.mul(w, scale.view(-1, 1, 1, 1), out=out)
+        ctx.save_for_backward(scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        (scale,) = ctx.saved_tensors
+        gw = torch.empty(grad.shape, dtype=torch.float32, device=grad.device)
+        torch.mul(grad, scale.view(-1, 1, 1, 1), out=gw)
+        return gw, None, None
 
 
 class _BiasAct(torch.autograd.Function):

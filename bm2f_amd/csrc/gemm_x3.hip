@@ -583,8 +583,10 @@ extern "C" int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B
   x3_presplit<<<m2f::ceil_div(static_cast<int64_t>(nchunks) * NP, 256), 256, 0, st>>>(B, ldb, b_kn, N, K, NP, nchunks, Bs);
   if (int rc = m2f::check_launch(fn)) return rc;
   const int epi = (bias ? kBias : 0) | (relu ? kRelu : 0) | (mask ? kMask : 0) | (D1 ? kAdd : 0);
-  // 128-row blocks of 4 waves; 96-wide columns for N = 3 * 96 k (the 288-wide sampling projection), else 128
-  int cfg = (N % 128 != 0 && N % 96 == 0) ? 1 : 0;
+  // 96-wide columns of 4 waves for N = 3 * 96 k (the 288-wide sampling projection), else 128-wide columns
+  // of 8 waves (256 rows share one B chunk: 0.285 vs 0.321 ms at K = N = 256, 0.913 vs 0.949 at K = 1024,
+  // equal at N = 1024; tools/gemm_x3_bench.py, r2af)
+  int cfg = (N % 128 != 0 && N % 96 == 0) ? 1 : 3;
   if (const char* e = std::getenv("M2F_GEMM_X3_NT_CFG")) cfg = std::atoi(e);
   switch (cfg) {
     case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
