@@ -307,7 +307,7 @@ int64_t nt_workspace(int N, int K) {
 // C tiles leave through a per-wave LDS image as float4 rows (transposed when the operands were swapped).
 // ---------------------------------------------------------------------------------------------------
 template <int NW, bool MFULL, int CSUM>   // MFULL: every chunk is 16 full rows; CSUM: 0 none, 1 of A, 2 of B
-__global__ void __launch_bounds__(64 * NW, 2) x3_tn_kernel(const float* __restrict__ A, int64_t lda,
+__global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) x3_tn_kernel(const float* __restrict__ A, int64_t lda,
                                                            const float* __restrict__ B, int64_t ldb, int M, int N1,
                                                            int N2, int rows_per_split, int trans_out,
                                                            float* __restrict__ slab, float* __restrict__ colsum_slab,
@@ -526,12 +526,18 @@ TnPlan tn_plan(int M, int N1, int N2) {
   p.swap = N2 > N1;
   p.n1 = p.swap ? N2 : N1;
   p.n2 = p.swap ? N1 : N2;
-  p.nw = 4;  // 3 (96-row tiles, exact for 288) measured slower: fewer threads share the B staging
-  if (const char* e = std::getenv("M2F_GEMM_X3_TN_NW")) p.nw = std::atoi(e) == 3 ? 3 : 4;
+  // 8 waves (256 C rows share each B chunk, one block per CU) when the rows tile exactly: -4 % at 256 x 256,
+  // -9 % at 1024 x 256 (tools/gemm_x3_bench.py, r2ah); else 4 (8 waves lose at 288 rows: 0.60 vs 0.49 ms);
+  // 3 (96-row tiles, exact for 288) measured slower: fewer threads share the B staging
+  p.nw = p.n1 % 256 == 0 ? 8 : 4;
+  if (const char* e = std::getenv("M2F_GEMM_X3_TN_NW")) {
+    const int v = std::atoi(e);
+    p.nw = v == 3 ? 3 : v == 8 ? 8 : 4;
+  }
   p.tiles = ((p.n1 + 32 * p.nw - 1) / (32 * p.nw)) * ((p.n2 + 255) / 256);
   // ~512 blocks (2 per CU); 768 when the last row tile is partial (the 288-wide sampling projection:
   // 0.52 vs 0.65 ms at M = 344064; full tiles measured best at 512, tools/gemm_x3_bench.py)
-  int target = p.n1 % (32 * p.nw) ? 768 : 512;
+  int target = (p.n1 % (32 * p.nw) ? 768 : 512) / (p.nw >= 8 ? 2 : 1);   // 8 waves: one block per CU
   if (const char* e = std::getenv("M2F_GEMM_X3_TN_BLOCKS")) target = std::max(1, std::atoi(e));
   int splits = (target + p.tiles - 1) / p.tiles;
   const int max_splits = (M + 8 * kBK - 1) / (8 * kBK);       // >= 8 chunks per block
@@ -635,6 +641,8 @@ extern "C" int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, in
   (csum == 0 ? M2F_TN(NWV, MF, 0) : csum == 1 ? M2F_TN(NWV, MF, 1) : M2F_TN(NWV, MF, 2))
     if (p.nw == 3) {
       if (mfull) M2F_TN_CS(3, true); else M2F_TN_CS(3, false);
+    } else if (p.nw == 8) {
+      if (mfull) M2F_TN_CS(8, true); else M2F_TN_CS(8, false);
     } else {
       if (mfull) M2F_TN_CS(4, true); else M2F_TN_CS(4, false);
     }
