@@ -12,7 +12,6 @@ function, one op fewer per conv).  Optimizer: AdamW + full-model grad-norm clipp
 """
 from __future__ import annotations
 
-import os
 import types
 
 import torch
@@ -237,10 +236,6 @@ class MaskFormerR50(nn.Module):
         self.sem_seg_head = MaskFormerHead(cfg, self.backbone.output_shape())
         self.register_buffer("pixel_mean", torch.tensor(PIXEL_MEAN).view(-1, 1, 1), False)
         self.register_buffer("pixel_std", torch.tensor(PIXEL_STD).view(-1, 1, 1), False)
-        # backbone memory format: NHWC lets MIOpen run its NHWC kernels without NCHW<->NHWC transposes
-        self.channels_last = os.environ.get("M2F_CHANNELS_LAST", "0") == "1"
-        if self.channels_last:
-            self.backbone.to(memory_format=torch.channels_last)
 
     @property
     def pixel_decoder(self):
@@ -252,8 +247,6 @@ class MaskFormerR50(nn.Module):
 
     def forward(self, images):
         x = (images - self.pixel_mean) / self.pixel_std
-        if self.channels_last:
-            x = x.contiguous(memory_format=torch.channels_last)
         return self.sem_seg_head(self.backbone(x))
 
 

@@ -196,6 +196,9 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
     asplit(nxt, c + 1, fn);
     __syncthreads();
   };
+  // (hipcc sinks the split of a pair's second chunk into the conditional second step, next to its MFMAs;
+  // unconditional pairs with the split kept before the barrier, with or without sched_group_barrier
+  // interleaving, measured 3-11 % slower here -- the opposite of the TN kernel below, r2am)
   for (int c = 0; c < nk; c += 2) {
     step(c, r0, r1, fa, fb);
     if (c + 1 < nk) step(c + 1, r1, r0, fb, fa);
@@ -341,16 +344,38 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) x3_tn_kernel(const f
     float a[8];
     float b[NJ][8];
   };
-  // rows >= r1 are clamped in-bounds here and zeroed when split (never waited on at the load)
+  // rows >= r1 are clamped in-bounds here and zeroed when split (never waited on at the load).  MFULL: the
+  // chunk's first row is clamped instead (a chunk past the slab's end is never multiplied), so every load
+  // is a wave-uniform row base (SGPRs) plus a per-lane 32-bit offset fixed for the kernel plus the
+  // wave-uniform e * ld: one VALU add per load instead of a clamped 64-bit multiply-add
+  const uint32_t aoff = static_cast<uint32_t>(lh * 8 * lda + acol);
+  uint32_t boff8[NJ];
+#pragma unroll
+  for (int u = 0; u < NJ; ++u) {
+    const int job = min(tid + u * NT, JOBS - 1), half = job / BN, col = min(n20 + job % BN, N2 - 1);
+    boff8[u] = static_cast<uint32_t>(half * 8 * ldb + col);
+  }
   auto gload = [&](Regs& r, int c) {
     const int m = r0 + c * kBK;
+    if constexpr (MFULL) {
+      const int64_t mb = min(m, M - kBK);
+      const float* arow = A + mb * lda;
+      const float* brow = B + mb * ldb;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) r.a[e] = ap[static_cast<int64_t>(min(m + lh * 8 + e, M - 1)) * lda];
+      for (int e = 0; e < 8; ++e) r.a[e] = arow[aoff + static_cast<uint32_t>(e * lda)];
 #pragma unroll
-    for (int u = 0; u < NJ; ++u) {
-      const int job = min(tid + u * NT, JOBS - 1), half = job / BN, col = min(n20 + job % BN, N2 - 1);
+      for (int u = 0; u < NJ; ++u)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) r.b[u][e] = B[static_cast<int64_t>(min(m + half * 8 + e, M - 1)) * ldb + col];
+        for (int e = 0; e < 8; ++e) r.b[u][e] = brow[boff8[u] + static_cast<uint32_t>(e * ldb)];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) r.a[e] = ap[static_cast<int64_t>(min(m + lh * 8 + e, M - 1)) * lda];
+#pragma unroll
+      for (int u = 0; u < NJ; ++u) {
+        const int job = min(tid + u * NT, JOBS - 1), half = job / BN, col = min(n20 + job % BN, N2 - 1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) r.b[u][e] = B[static_cast<int64_t>(min(m + half * 8 + e, M - 1)) * ldb + col];
+      }
     }
   };
   float csa = 0.f, csb[NJ];
@@ -430,12 +455,20 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) x3_tn_kernel(const f
       chunk_mfma(c & 1, fc);
       bstore(nxt, c + 1, (c + 1) & 1);
       asplit(nxt, c + 1, fn);
+      // keep the splits of the next chunk on this side of the barrier (hipcc otherwise moves them past it,
+      // next to their MFMAs): -3..-7 % at the encoder shapes (r2am; a sched_group_barrier MFMA/VALU
+      // interleave on top measured worse)
+      __builtin_amdgcn_sched_barrier(0);
       __syncthreads();
     };
-    for (int c = 0; c < nk; c += 2) {
+    // both steps of a pair unconditional, the odd last chunk peeled: a conditional second step would let
+    // hipcc sink the pair's second split into it
+    int c = 0;
+    for (; c + 1 < nk; c += 2) {
       step(c, r0s, r1s, fa, fb);
-      if (c + 1 < nk) step(c + 1, r1s, r0s, fb, fa);
+      step(c + 1, r1s, r0s, fb, fa);
     }
+    if (c < nk) step(c, r0s, r1s, fa, fb);
   }
 
   // ---- epilogue: slab[split] is [N1][N2] (or [N2][N1] when trans_out) --------------------------------

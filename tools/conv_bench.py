@@ -26,18 +26,26 @@ def timeit(fn, iters=5):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="shapes whose name contains this")
+    ap.add_argument("--x3-only", action="store_true", help="skip the MIOpen timings (A/B runs)")
+    a = ap.parse_args()
     dev = torch.device("cuda")
     shapes = [("layer_1 3x3", 16, 256, 256, 256, 256, 3, False), ("adapter_1 1x1", 16, 256, 256, 256, 256, 1, False),
               ("mask_features 1x1", 16, 256, 256, 256, 256, 1, True), ("input_proj res3", 16, 512, 256, 128, 128, 1, True),
               ("input_proj res4", 16, 1024, 256, 64, 64, 1, True), ("input_proj res5", 16, 2048, 256, 32, 32, 1, True)]
     for name, N, Ci, Co, H, W, k, b in shapes:
+        if a.only not in name:
+            continue
         conv = nn.Conv2d(Ci, Co, k, padding=k // 2, bias=b).to(dev)
         x = torch.randn(N, Ci, H, W, device=dev, requires_grad=True)
         g = torch.randn(N, Co, H, W, device=dev)
         fl = 2.0 * N * H * W * Ci * Co * k * k
         res = {}
-        for eng, fn in (("miopen", lambda: conv(x)), ("x3", lambda: conv_ops.conv2d(x, conv)),
-                        ("x3+tn", lambda: conv_ops.conv2d(x, conv))):
+        engines = (("miopen", lambda: conv(x)), ("x3", lambda: conv_ops.conv2d(x, conv)),
+                   ("x3+tn", lambda: conv_ops.conv2d(x, conv)))
+        for eng, fn in engines[2:] if a.x3_only else engines:
             conv_ops.WGRAD3 = "tn" if eng == "x3+tn" else "miopen"
             tf = timeit(fn)
             y = fn()

@@ -30,6 +30,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=16 * 21504)
     ap.add_argument("--cfgs", default="0,2,3", help="M2F_GEMM_X3_NT_CFG values to time")
+    ap.add_argument("--x3-only", action="store_true", help="time only the x3 engine (A/B runs)")
     a = ap.parse_args()
     M = a.rows
     dev = torch.device("cuda")
@@ -43,10 +44,11 @@ def main():
         fl = 2.0 * M * N * K
         ref = x[sub].double() @ w.double().t() + b.double()
         res = {}
-        res["blas"] = (timeit(lambda: torch.nn.functional.linear(x, w, b)),
-                       rel(torch.nn.functional.linear(x, w, b)[sub], ref))
-        res["exact"] = (timeit(lambda: linear_ops.gemm_nt(x, w, b, engine="exact")),
-                        rel(linear_ops.gemm_nt(x, w, b, engine="exact")[sub], ref))
+        if not a.x3_only:
+            res["blas"] = (timeit(lambda: torch.nn.functional.linear(x, w, b)),
+                           rel(torch.nn.functional.linear(x, w, b)[sub], ref))
+            res["exact"] = (timeit(lambda: linear_ops.gemm_nt(x, w, b, engine="exact")),
+                            rel(linear_ops.gemm_nt(x, w, b, engine="exact")[sub], ref))
         res["x3"] = (timeit(lambda: linear_ops.gemm_nt(x, w, b, engine="x3")),
                      rel(linear_ops.gemm_nt(x, w, b, engine="x3")[sub], ref))
         for c in [c for c in a.cfgs.split(",") if c]:
@@ -60,19 +62,20 @@ def main():
         wt = w.t().contiguous()
         ref = g[sub].double() @ w.double()
         mk = torch.randn(M, K, device=dev)
-        res = {"blas": (timeit(lambda: g @ w), rel((g @ w)[sub], ref)),
-               "exact": (timeit(lambda: linear_ops.gemm_nt(g, wt, engine="exact")),
-                         rel(linear_ops.gemm_nt(g, wt, engine="exact")[sub], ref)),
-               "x3": (timeit(lambda: linear_ops.gemm_nt(g, w, engine="x3", b_kn=True)),
+        res = {"x3": (timeit(lambda: linear_ops.gemm_nt(g, w, engine="x3", b_kn=True)),
                       rel(linear_ops.gemm_nt(g, w, engine="x3", b_kn=True)[sub], ref)),
-               "exactmask": (timeit(lambda: linear_ops.gemm_nt(g, wt, mask=mk, engine="exact")), 0.0),
                "x3mask": (timeit(lambda: linear_ops.gemm_nt(g, w, mask=mk, engine="x3", b_kn=True)), 0.0)}
+        if not a.x3_only:
+            res["blas"] = (timeit(lambda: g @ w), rel((g @ w)[sub], ref))
+            res["exact"] = (timeit(lambda: linear_ops.gemm_nt(g, wt, engine="exact")),
+                            rel(linear_ops.gemm_nt(g, wt, engine="exact")[sub], ref))
+            res["exactmask"] = (timeit(lambda: linear_ops.gemm_nt(g, wt, mask=mk, engine="exact")), 0.0)
         print(f"dgrad M={M} K={N} N={K}: " + "  ".join(f"{k} {t:.3f}ms {fl / t / 1e9:.0f}TF err {e:.1e}" for k, (t, e) in res.items()), flush=True)
         del mk
         ref = g.double().t() @ x.double()
         refb = g.double().sum(0)
-        res = {"blas": (timeit(lambda: (g.t() @ x, g.sum(0))), rel(g.t() @ x, ref))}
-        for eng in ("exact", "x3"):
+        res = {} if a.x3_only else {"blas": (timeit(lambda: (g.t() @ x, g.sum(0))), rel(g.t() @ x, ref))}
+        for eng in (("x3",) if a.x3_only else ("exact", "x3")):
             dw, db = linear_ops.gemm_tn(g, x, colsum=True, engine=eng)
             res[eng] = (timeit(lambda: linear_ops.gemm_tn(g, x, colsum=True, engine=eng)), rel(dw, ref))
             res[eng + "_bias"] = (0.0, rel(db, refb))
