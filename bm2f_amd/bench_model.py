@@ -12,6 +12,7 @@ function, one op fewer per conv).  Optimizer: AdamW + full-model grad-norm clipp
 """
 from __future__ import annotations
 
+import ctypes
 import types
 
 import torch
@@ -80,10 +81,15 @@ class _ScaledWeight(torch.autograd.Function):
 
 
 class _BiasAct(torch.autograd.Function):
-    """y = relu(x + r + bias[c]) in place on x (bias: frozen BN shift, no gradient)."""
+    """y = relu(x + r + bias[c]) in place on x (bias: frozen BN shift, no gradient).
+
+    ``nout`` > 1 returns y plus nout - 1 aliases of it, one per consumer (a block output feeds the next
+    block's first conv, its shortcut / identity path and, at a stage end, the pixel decoder): the backward
+    then receives each consumer's gradient separately and forms sum * (y > 0) in one pass
+    (m2f_relu_bwd_sum) instead of the engine's accumulating adds followed by threshold_backward."""
 
     @staticmethod
-    def forward(ctx, x, r, bias):
+    def forward(ctx, x, r, bias, nout):
         from . import _native
         code = {torch.bfloat16: 2, torch.float32: 0}[x.dtype]
         cl = 0 if x.is_contiguous() else 1
@@ -93,17 +99,31 @@ class _BiasAct(torch.autograd.Function):
         ctx.mark_dirty(x)
         ctx.save_for_backward(x)
         ctx.has_r = r is not None
-        return x
+        if nout == 1:
+            return x
+        return (x,) + tuple(x.view(x.shape) for _ in range(nout - 1))
 
     @staticmethod
-    def backward(ctx, grad):
+    def backward(ctx, *grads):
+        from . import _native
         (y,) = ctx.saved_tensors
-        g = torch.ops.aten.threshold_backward(grad, y, 0)  # ReLU's own backward: one pass
-        return g, (g if ctx.has_r else None), None
+        gs = [g for g in grads if g is not None]
+        if len(gs) == 1:
+            g = torch.ops.aten.threshold_backward(gs[0], y, 0)  # ReLU's own backward: one pass
+        elif (y.is_contiguous() and len(gs) <= 4 and y.numel() % 8 == 0
+              and all(t.dtype == y.dtype and t.is_contiguous() for t in gs)):
+            g = torch.empty_like(y, memory_format=torch.contiguous_format)
+            ptrs = (ctypes.c_void_p * len(gs))(*[t.data_ptr() for t in gs])
+            _native.call("m2f_relu_bwd_sum", ptrs, len(gs), y.data_ptr(), g.data_ptr(), y.numel(),
+                         {torch.bfloat16: 2, torch.float32: 0}[y.dtype], torch.cuda.current_stream(y.device).cuda_stream)
+        else:
+            g = torch.ops.aten.threshold_backward(sum(gs), y, 0)
+        return g, (g if ctx.has_r else None), None, None
 
 
-def bias_act(x, bias, residual=None):
-    """relu(x + residual + bias[c]) (NCHW); one fused pass on a HIP device."""
+def bias_act(x, bias, residual=None, nout=1):
+    """relu(x + residual + bias[c]) (NCHW); one fused pass on a HIP device.  nout > 1: a tuple of nout
+    handles of the result, one per consumer (see _BiasAct)."""
     hw = x.shape[2] * x.shape[3]
     cl = torch.channels_last
     ok = ((x.is_contiguous() and hw % 8 == 0 and (residual is None or residual.is_contiguous()))
@@ -111,11 +131,12 @@ def bias_act(x, bias, residual=None):
               and (residual is None or residual.is_contiguous(memory_format=cl))))
     if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and ok
             and (residual is None or residual.dtype == x.dtype)):
-        return _BiasAct.apply(x, residual, bias.float().contiguous())
+        return _BiasAct.apply(x, residual, bias.float().contiguous(), nout)
     y = x + bias.view(1, -1, 1, 1).to(x.dtype)
     if residual is not None:
         y = y + residual
-    return F.relu(y)
+    y = F.relu(y)
+    return y if nout == 1 else (y,) * nout
 
 
 class _MaxPool3s2(torch.autograd.Function):
@@ -161,16 +182,18 @@ class Bottleneck(nn.Module):
         self.conv2 = FrozenBNConv(cb, cb, 3, stride, 1)
         self.conv3 = FrozenBNConv(cb, cout, 1, 1)
 
-    def forward(self, x):
-        out = bias_act(*self.conv1.conv_shift(x))
+    def forward(self, x, nout=1):
+        """x: the input, or handles of it (conv, residual path[, others]); nout handles of the output."""
+        xc, xr = (x[0], x[1]) if isinstance(x, tuple) else (x, x)
+        out = bias_act(*self.conv1.conv_shift(xc))
         out = bias_act(*self.conv2.conv_shift(out))
         out, shift = self.conv3.conv_shift(out)
         if self.shortcut is not None:
-            sc, sc_shift = self.shortcut.conv_shift(x)
+            sc, sc_shift = self.shortcut.conv_shift(xr)
             shift = shift + sc_shift
         else:
-            sc = x
-        return bias_act(out, shift, sc)
+            sc = xr
+        return bias_act(out, shift, sc, nout)
 
 
 class ResNet50(nn.Module):
@@ -196,9 +219,15 @@ class ResNet50(nn.Module):
         x = bias_act(*self.stem.conv_shift(x))
         x = max_pool_stem(x)
         out = {}
-        for name in self.stage_names:
-            x = getattr(self, name)(x)
-            out[name] = x
+        # each block output is handed on as one handle per consumer (conv, residual path, and at a stage
+        # end the pixel decoder) so its ReLU backward sums their gradients in one pass
+        for si, name in enumerate(self.stage_names):
+            blocks = list(getattr(self, name))
+            for bi, blk in enumerate(blocks):
+                last = bi == len(blocks) - 1
+                nout = (1 if si == len(self.stage_names) - 1 else 3) if last else 2
+                x = blk(x, nout)
+            out[name] = x[-1] if isinstance(x, tuple) else x
         return out
 
 

@@ -63,6 +63,73 @@ extern "C" int m2f_bias_act_nchw(void* x, const void* residual, const float* bia
 }
 
 // ---------------------------------------------------------------------------------------------------
+// ReLU backward over the gradients of several consumers of one activation (a residual block's output feeds
+// the next block's first conv, its shortcut / identity path and, at a stage end, the pixel decoder):
+//     out = (g_0 + ... + g_{k-1}) * (y > 0)
+// one pass (k + 1 reads, one write) instead of the autograd engine's k - 1 accumulating adds and a separate
+// threshold_backward.  The sum is formed in fp32 in consumer order and rounded once.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kMaxReluGrads = 4;
+
+struct ReluGrads {
+  const void* g[kMaxReluGrads];
+};
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) relu_bwd_sum_kernel(ReluGrads gs, int ng, const T* __restrict__ y,
+                                                           T* __restrict__ out, int64_t nvec) {
+  using VT = Vec<T, V>;
+  const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i >= nvec) return;
+  float acc[V];
+  const VT g0 = reinterpret_cast<const VT*>(gs.g[0])[i];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = static_cast<float>(g0.v[e]);
+  for (int k = 1; k < ng; ++k) {
+    const VT gk = reinterpret_cast<const VT*>(gs.g[k])[i];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] += static_cast<float>(gk.v[e]);
+  }
+  const VT yy = reinterpret_cast<const VT*>(y)[i];
+  VT o;
+#pragma unroll
+  for (int e = 0; e < V; ++e) o.v[e] = static_cast<T>(static_cast<float>(yy.v[e]) > 0.f ? acc[e] : 0.f);
+  reinterpret_cast<VT*>(out)[i] = o;
+}
+
+}  // namespace
+
+extern "C" int m2f_relu_bwd_sum(const void* const* grads, int ngrads, const void* y, void* out, int64_t n, int dtype,
+                                void* stream) {
+  const char* fn = "m2f_relu_bwd_sum";
+  if (!grads || ngrads < 1 || ngrads > kMaxReluGrads || !y || !out || n < 0)
+    return m2f::fail(M2F_EINVAL, "%s: bad arguments (1 <= grads <= %d)", fn, kMaxReluGrads);
+  if (dtype != M2F_BF16 && dtype != M2F_F32) return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  const int V = dtype == M2F_BF16 ? 8 : 4;
+  ReluGrads gs{};
+  bool aligned = m2f::aligned(y, 16) && m2f::aligned(out, 16);
+  for (int k = 0; k < ngrads; ++k) {
+    if (!grads[k]) return m2f::fail(M2F_EINVAL, "%s: null gradient %d", fn, k);
+    gs.g[k] = grads[k];
+    aligned = aligned && m2f::aligned(grads[k], 16);
+  }
+  if (n % V || !aligned) return m2f::fail(M2F_EUNSUPPORTED, "%s: needs n %% %d == 0 and 16-byte aligned tensors", fn, V);
+  const int64_t nvec = n / V;
+  if (nvec == 0) return m2f::ok();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = m2f::ceil_div(nvec, 256);
+  if (dtype == M2F_BF16)
+    relu_bwd_sum_kernel<__bf16, 8><<<grid, 256, 0, st>>>(gs, ngrads, static_cast<const __bf16*>(y),
+                                                         static_cast<__bf16*>(out), nvec);
+  else
+    relu_bwd_sum_kernel<float, 4><<<grid, 256, 0, st>>>(gs, ngrads, static_cast<const float*>(y),
+                                                        static_cast<float*>(out), nvec);
+  return m2f::check_launch(fn);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // The benchmark backbone's stem max pool, kernel 3, stride 2, padding 1 (detectron2 BasicStem), NCHW.
 // Forward: torch's max_pool2d_with_indices rule (first maximum in window order, NaN wins), the winner
 // kept as a 1-byte window position (0..8) instead of an int64 flat index.  Backward: each input pixel

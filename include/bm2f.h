@@ -277,6 +277,13 @@ int m2f_conv_f32x3_wgrad(const float* grad_out, const float* I, float* dW_tck, f
 int m2f_bias_act_nchw(void* x, const void* residual, const float* bias, int64_t N, int C, int64_t HW, int dtype,
                       int channels_last, void* stream);
 
+/* ReLU backward over the summed gradients of up to 4 consumers of one activation y (the benchmark
+ * backbone's block outputs): out = (grads[0] + ... + grads[ngrads-1]) * (y > 0), summed in fp32 in the given
+ * order and rounded once; bf16 (M2F_BF16) or fp32, contiguous, n % 8 (bf16) / % 4 (fp32), 16-byte aligned.
+ * Replaces the autograd engine's accumulating adds plus torch's threshold_backward (one pass, k + 1 reads). */
+int m2f_relu_bwd_sum(const void* const* grads, int ngrads, const void* y, void* out, int64_t n, int dtype,
+                     void* stream);
+
 /* The benchmark backbone's stem max pool (kernel 3, stride 2, padding 1; detectron2 BasicStem; not on the
  * reference's hot path), NCHW, dtype M2F_BF16 or M2F_F32, planes = N*C, output (H-1)/2+1 x (W-1)/2+1.
  * m2f_maxpool3s2_fwd: torch's max_pool2d_with_indices rule (first maximum in window order, NaN wins); the

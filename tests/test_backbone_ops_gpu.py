@@ -30,6 +30,32 @@ def test_bias_act_matches_unfused(device, dtype, residual):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("nout,unused", [(2, None), (3, None), (3, 1)])
+def test_bias_act_fork_sums_consumer_grads(device, dtype, nout, unused):
+    """bias_act(..., nout): one handle per consumer; the backward (m2f_relu_bwd_sum) gives sum_k g_k * (y > 0)
+    with the sum formed in fp32 in consumer order and rounded once (bit-exact against that torch sum), to x
+    and the residual; an unused handle contributes nothing."""
+    torch.manual_seed(nout)
+    x = torch.randn(2, 64, 16, 24, device=device, dtype=dtype)
+    r = torch.randn_like(x)
+    b = torch.randn(64, device=device)
+    xa, ra = x.clone().requires_grad_(), r.clone().requires_grad_()
+    hs = bias_act(xa.clone(), b, ra, nout)
+    assert len(hs) == nout and all(h.data_ptr() == hs[0].data_ptr() for h in hs)
+    gs = [torch.randn_like(hs[0]) for _ in range(nout)]
+    loss = sum((h.float() * g.float()).sum() for k, (h, g) in enumerate(zip(hs, gs)) if k != unused)
+    loss.backward()
+    y = hs[0].detach()
+    tot = None
+    for k, g in enumerate(gs):
+        if k != unused:
+            tot = g.float() if tot is None else tot + g.float()
+    want = torch.where(y > 0, tot, torch.zeros_like(tot)).to(dtype)
+    torch.testing.assert_close(xa.grad, want, rtol=0, atol=0)
+    torch.testing.assert_close(ra.grad, want, rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("H,W", [(16, 24), (7, 9), (1, 1), (2, 3), (5, 16), (1, 8)])
 def test_stem_maxpool_matches_torch(device, dtype, H, W):
     """The stem max pool (csrc/eltwise.hip, 1-byte winners) against F.max_pool2d(3, 2, 1): forward and

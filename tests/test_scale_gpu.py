@@ -303,10 +303,13 @@ def test_config5_video_decoder_full_size_vs_torch_ops(device):
 # ------------------------------------------------------------------------------------------------------
 def test_ddp_rccl_world1_matches_unwrapped(device, tmp_path):
     """torch.distributed backend "nccl" (RCCL) at world size 1, file-store rendezvous: MaskFormerR50 wrapped by
-    bench_model.wrap_ddp takes two AdamW steps at 256^2 under AMP bf16 beside the unwrapped model (same seed,
+    bench_model.wrap_ddp takes two AdamW steps at 256^2 under AMP bf16 beside two unwrapped copies (same seed,
     same inputs).  Every parameter gets a gradient through the reducer's hooks behind the custom autograd nodes
-    (_FoldGate, EncoderInProjF32, the in-place _BiasAct), equal to the unwrapped model's up to the library
-    convolutions' own run-to-run rounding (bf16 backward kernels with atomics), and the RCCL all-reduce runs."""
+    (_FoldGate, EncoderInProjF32, the in-place and forked _BiasAct), and the wrapped model's gradients differ
+    from an unwrapped copy's by no more than two unwrapped runs differ from each other: the step is not
+    bitwise repeatable (the MSDA backward's fp32 atomics, thousands of adds per coarse-level pixel, and the
+    bf16 library convolutions' split weight-gradient sums), so that run-to-run spread is the bar (x3, plus
+    1e-3 of the max), and the RCCL all-reduce runs."""
     import copy
 
     import torch.distributed as dist
@@ -315,27 +318,30 @@ def test_ddp_rccl_world1_matches_unwrapped(device, tmp_path):
     torch.manual_seed(0)
     base = MaskFormerR50(default_cfg()).to(device)
     ref_model = copy.deepcopy(base)
+    ref_model2 = copy.deepcopy(base)
     images = torch.randn(2, 3, 256, 256, device=device) * 57.0 + 117.0
     store = f"file://{tmp_path}/store"
     dist.init_process_group("nccl", init_method=store, rank=0, world_size=1, device_id=device)
     try:
         ddp = wrap_ddp(base, device)
-        opt_d, opt_r = make_optimizer(ddp), make_optimizer(ref_model)
+        opt_d, opt_r, opt_r2 = make_optimizer(ddp), make_optimizer(ref_model), make_optimizer(ref_model2)
         for step in range(2):
             ld = train_step(ddp, opt_d, images, torch.bfloat16)
             lr = train_step(ref_model, opt_r, images, torch.bfloat16)
+            train_step(ref_model2, opt_r2, images, torch.bfloat16)
             torch.testing.assert_close(ld, lr, rtol=1e-3, atol=1e-6)
             if step:
                 break  # the second step exercises the optimizer on the reduced gradients; its inputs differ slightly
-            for (n, pd_), (_, pr) in zip(ddp.module.named_parameters(), ref_model.named_parameters()):
+            worst = (0.0, "")
+            for (n, pd_), (_, pr), (_, pr2) in zip(ddp.module.named_parameters(), ref_model.named_parameters(),
+                                                   ref_model2.named_parameters()):
                 assert pd_.grad is not None and pr.grad is not None, n
                 scale = max(pr.grad.abs().max().item(), 1e-20)
                 err = (pd_.grad.float() - pr.grad.float()).abs().max().item() / scale
-                # hot path (pixel decoder + decoder): fp32 atomic order in the MSDA backward's flush only;
-                # the bf16 library convolutions of the benchmark backbone round their split weight-gradient
-                # sums in bf16 (measured up to 4e-2 of the max on the stem between two identical runs)
-                bar = 2e-1 if n.startswith("backbone.") else 1e-3
-                assert err < bar, f"{n}: {err}"
+                spread = (pr2.grad.float() - pr.grad.float()).abs().max().item() / scale
+                assert err <= 3 * spread + 1e-3, f"{n}: wrapped vs unwrapped {err}, unwrapped run-to-run {spread}"
+                worst = max(worst, (err, n))
+            print(f"largest wrapped-vs-unwrapped gradient difference: {worst[0]:.2e} of the max ({worst[1]})")
         # and the collective itself moved data over RCCL
         t = torch.full((1024,), 3.0, device=device)
         dist.all_reduce(t)
