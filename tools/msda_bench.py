@@ -48,6 +48,47 @@ def make_inputs(N, shapes, M=8, D=32, P=4, stress=False, device="cuda", seed=0, 
     return value, st, lsi, loc.contiguous(), attn, gout
 
 
+def fused_calls(value, shapes, gout, noise, M=8, P=4, seed=1):
+    """Forward / backward closures of the fused-front-end kernels (m2f_msda_fused_{fwd,bwd}_f32) on the
+    encoder layout: reference points at the pixel centres, offsets on the reference init rays (pixel units,
+    ms_deform_attn.py:_reset_parameters) plus N(0, noise) px, random logits."""
+    import ctypes
+    from bm2f_amd import _native
+    N, S = value.shape[:2]
+    L = len(shapes)
+    dev = value.device
+    g = torch.Generator(device=dev).manual_seed(seed)
+    refs = []
+    for h, w in shapes:
+        ys, xs = torch.meshgrid(torch.linspace(0.5, h - 0.5, h, device=dev),
+                                torch.linspace(0.5, w - 0.5, w, device=dev), indexing="ij")
+        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
+    ref = torch.cat(refs, 0)[None, :, None, :].expand(N, S, L, 2).contiguous()
+    th = torch.arange(M, device=dev) * (2 * math.pi / M)
+    grid = torch.stack([th.cos(), th.sin()], -1)
+    grid = grid / grid.abs().max(-1, keepdim=True)[0]
+    off = (grid.view(M, 1, 1, 2) * torch.arange(1, P + 1, device=dev).view(1, 1, P, 1)).expand(M, L, P, 2)
+    off = off[None, None] + noise * torch.randn(N, S, M, L, P, 2, device=dev, generator=g)
+    logits = torch.randn(N, S, M * L * P, device=dev, generator=g)
+    proj = torch.cat([off.reshape(N, S, -1), logits], -1).contiguous()
+    hs = msda._host_shape_buffer(shapes)
+    out = torch.empty(N, S, M * 32, device=dev)
+    gv = torch.empty_like(value)
+    gp = torch.empty_like(proj)
+    st = msda._stream(dev)
+    D = value.shape[-1]
+
+    def fwd():
+        _native.call("m2f_msda_fused_fwd_f32", msda._ptr(value), msda._ptr(proj), proj.stride(1), msda._ptr(ref),
+                     ref.stride(0), ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, S, P, msda._ptr(out), st)
+
+    def bwd():
+        _native.call("m2f_msda_fused_bwd_f32", msda._ptr(value), msda._ptr(proj), proj.stride(1), msda._ptr(ref),
+                     ref.stride(0), ctypes.cast(hs, ctypes.c_void_p), msda._ptr(gout), N, S, M, D, L, S, P,
+                     msda._ptr(gv), msda._ptr(gp), None, ctypes.c_int64(0), st)
+    return fwd, bwd
+
+
 def timeit(fn, iters):
     for _ in range(3):
         fn()
@@ -70,6 +111,7 @@ def main():
     ap.add_argument("--no-host-shapes", action="store_true")
     ap.add_argument("--noise", type=float, default=1.0, help="px std of the offsets around the init rays")
     ap.add_argument("--bwd-only", action="store_true")
+    ap.add_argument("--fused", action="store_true", help="the fused front-end kernels (the path the bench step runs)")
     a = ap.parse_args()
     r = a.res
     shapes = [(r // 32, r // 32), (r // 16, r // 16), (r // 8, r // 8)]
@@ -79,10 +121,15 @@ def main():
     per_img = (r / 1024) ** 2
     fwd_bytes = 68.81e6 * per_img * a.n
     bwd_bytes = 115.60e6 * per_img * a.n
-    tf = 0.0 if a.bwd_only else timeit(lambda: msda.ms_deform_attn_forward(v, st, lsi, loc, attn, 64), a.iters)
-    tb = timeit(lambda: msda.ms_deform_attn_backward(v, st, lsi, loc, attn, gout, 64), a.iters)
+    if a.fused:
+        fwd, bwd = fused_calls(v, shapes, gout, a.noise)
+    else:
+        fwd = lambda: msda.ms_deform_attn_forward(v, st, lsi, loc, attn, 64)  # noqa: E731
+        bwd = lambda: msda.ms_deform_attn_backward(v, st, lsi, loc, attn, gout, 64)  # noqa: E731
+    tf = 0.0 if a.bwd_only else timeit(fwd, a.iters)
+    tb = timeit(bwd, a.iters)
     tf = tf or float("nan")
-    print(f"N={a.n} res={r} stress={a.stress} noise={a.noise} env={ {k: v for k, v in os.environ.items() if k.startswith('M2F_')} }: fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
+    print(f"N={a.n} res={r} fused={a.fused} stress={a.stress} noise={a.noise} env={ {k: v for k, v in os.environ.items() if k.startswith('M2F_')} }: fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
           f"bwd {tb:.3f} ms ({bwd_bytes / tb / 1e6:.0f} GB/s alg)")
 
 

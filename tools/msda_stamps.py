@@ -30,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--n", type=int, default=16)
+    ap.add_argument("--lib", default=LIB, help="diagnostic library to load (default: the --build output)")
+    ap.add_argument("--noise", type=float, default=1.0)
     a = ap.parse_args()
     if a.build:
         build()
@@ -39,8 +41,8 @@ def main():
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from msda_bench import make_inputs
     shapes = [(32, 32), (64, 64), (128, 128)]
-    v, st, lsi, loc, attn, gout = make_inputs(a.n, shapes)
-    lib = ctypes.CDLL(LIB)
+    v, st, lsi, loc, attn, gout = make_inputs(a.n, shapes, noise=a.noise)
+    lib = ctypes.CDLL(a.lib)
     p, i = ctypes.c_void_p, ctypes.c_int
     fn = lib.m2f_diag_msda_bwd_stamps_f32
     fn.argtypes = [p, p, p, p, i, i, i, i, p, p, p, p, p, i, p]
