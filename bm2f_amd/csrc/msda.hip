@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 namespace m2f {
 std::string& last_error() {
@@ -447,13 +448,20 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         const float inv = 1.f / sum;
         const float2 rf = *reinterpret_cast<const float2*>(fe.ref + n * fe.ref_bs + (static_cast<int64_t>(q) * LT + l) * 2);
         const float* of = prow + (m * LP + l * P) * 2;
+        const float fW = static_cast<float>(W), fH = static_cast<float>(H);
+        const float iW = 1.f / fW, iH = 1.f / fH;
+        auto points = [&](auto pow2) {  // as msda_fused_fwd: exact reciprocals when W and H are powers of two
+          constexpr bool POW2 = decltype(pow2)::value;
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const float2 off = *reinterpret_cast<const float2*>(of + 2 * p);
-          lx[p] = rf.x + off.x / static_cast<float>(W);
-          ly[p] = rf.y + off.y / static_cast<float>(H);
-          av[p] = expf(lg[l * P + p] - mx) * inv;
-        }
+          for (int p = 0; p < P; ++p) {
+            const float2 off = *reinterpret_cast<const float2*>(of + 2 * p);
+            lx[p] = rf.x + div_norm(off.x, fW, iW, POW2);
+            ly[p] = rf.y + div_norm(off.y, fH, iH, POW2);
+            av[p] = expf(lg[l * P + p] - mx) * inv;
+          }
+        };
+        if (((W & (W - 1)) | (H & (H - 1))) == 0) points(std::true_type{});
+        else points(std::false_type{});
       } else {
         const int64_t kb = (nq * M + m) * LP + l * P;
 #pragma unroll
@@ -599,6 +607,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       for (int l = 0; l < LT; ++l) {
         const int H = geo.H[l], W = geo.W[l];
         const int lbase = ((n * S + geo.start[l]) * M + m) * D + 4 * j;
+        const int Wrs = W * rs;
         float st_l = 0.f, st_a = 0.f;
         // points in batches of PB: every corner load of a batch is issued before any of its math
         constexpr int PB = 2;
@@ -615,10 +624,12 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             h0s[pp] = h0; w0s[pp] = w0;
             const int y0 = min(max(h0, 0), H - 1), y1 = min(max(h0 + 1, 0), H - 1);
             const int x0 = min(max(w0, 0), W - 1), x1 = min(max(w0 + 1, 0), W - 1);
-            vb[pp][0] = ld4(value + lbase + (y0 * W + x0) * rs);
-            vb[pp][1] = ld4(value + lbase + (y0 * W + x1) * rs);
-            vb[pp][2] = ld4(value + lbase + (y1 * W + x0) * rs);
-            vb[pp][3] = ld4(value + lbase + (y1 * W + x1) * rs);
+            // one multiply per sample: corners 2-4 are 0 / 1 pixel right and 0 / 1 row down of corner 1
+            const int o1 = lbase + (y0 * W + x0) * rs, dx = x1 != x0 ? rs : 0, dy = y1 != y0 ? Wrs : 0;
+            vb[pp][0] = ld4(value + o1);
+            vb[pp][1] = ld4(value + o1 + dx);
+            vb[pp][2] = ld4(value + o1 + dy);
+            vb[pp][3] = ld4(value + o1 + dy + dx);
           }
 #pragma unroll
           for (int pp = 0; pp < PB; ++pp) {
@@ -798,7 +809,8 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
 // then gathers one head's value rows (2.75 MB per 1024^2 image, L2-resident) and a block's 32 queries
 // sample one compact neighbourhood of them (L1 reuse across the patch).  Needs Lq == S (encoder queries
 // are the pixels).
-template <int LT, bool TILED>
+// OFF32: every element offset of value / out fits 32 bits (checked on the host): 32-bit corner addressing.
+template <int LT, bool TILED, bool OFF32>
 __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ value, FrontEnd fe, TileGeom geo,
                                                       int64_t npairs, int S, int M, int Lq, float* __restrict__ out) {
   constexpr int D = 32, G = 8, P = 4, LP = LT * P;
@@ -839,13 +851,21 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
   const float* prow = fe.proj + nq * fe.ld;
   const float* rrow = fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * LT * 2;
   const float* lg = prow + M * LP * 2 + m * LP;
+  // softmax over the pair's L*P logits (ms_deform_attn.py:103-104), each exp computed once in the group:
+  // lane j owns logits j and j + 8, the group max is a DPP reduction (exact), and every lane gathers the
+  // twelve exps and sums them in logit order (the backward recomputes the same sum, msda_bwd_f32_tiled)
+  static_assert(LP <= 16, "two logits per lane of the 8-lane group");
+  const float l0 = j < LP ? lg[j] : -INFINITY, l1 = j + 8 < LP ? lg[j + 8] : -INFINITY;
+  const float mx = max8_dpp(fmaxf(l0, l1));
+  const float e0 = j < LP ? expf(l0 - mx) : 0.f, e1 = j + 8 < LP ? expf(l1 - mx) : 0.f;
+  const int gb = (threadIdx.x & 63) & ~(G - 1);
   float a[LP];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int k = 0; k < LP; ++k) { a[k] = lg[k]; mx = fmaxf(mx, a[k]); }
   float sum = 0.f;
 #pragma unroll
-  for (int k = 0; k < LP; ++k) { a[k] = expf(a[k] - mx); sum += a[k]; }
+  for (int k = 0; k < LP; ++k) {
+    a[k] = __shfl(k < 8 ? e0 : e1, gb + (k & 7));
+    sum += a[k];
+  }
   const float inv = 1.f / sum;
   const f4 z = {0.f, 0.f, 0.f, 0.f};
   f4 acc = z;
@@ -854,17 +874,36 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
     const int H = geo.H[l], W = geo.W[l];
     const int64_t lbase = ((n * S + geo.start[l]) * M + m) * D + 4 * j;
     const float2 rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
+    const float fW = static_cast<float>(W), fH = static_cast<float>(H);
+    const float iW = 1.f / fW, iH = 1.f / fH;
+    // the level's points; POW2 (W and H powers of two, wave-uniform): offsets scaled by the exact reciprocals
+    auto points = [&](auto pow2) {
+      constexpr bool POW2 = decltype(pow2)::value;
 #pragma unroll
-    for (int p = 0; p < P; ++p) {
-      const float2 off = *reinterpret_cast<const float2*>(prow + (m * LP + l * P + p) * 2);
-      const float sx = rf.x + off.x / static_cast<float>(W);
-      const float sy = rf.y + off.y / static_cast<float>(H);
-      const Corners k = make_corners(sx, sy, H, W, lbase, rs);
-      f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
-      v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
-      const f4 val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
-      acc += k.ok ? val * (a[l * P + p] * inv) : z;
-    }
+      for (int p = 0; p < P; ++p) {
+        const float2 off = *reinterpret_cast<const float2*>(prow + (m * LP + l * P + p) * 2);
+        const float sx = rf.x + div_norm(off.x, fW, iW, POW2);
+        const float sy = rf.y + div_norm(off.y, fH, iH, POW2);
+        f4 val;
+        bool ok;
+        if constexpr (OFF32) {
+          const Corners32 k = make_corners32(sx, sy, H, W, static_cast<int>(lbase), static_cast<int>(rs));
+          f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
+          v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
+          val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
+          ok = k.ok;
+        } else {
+          const Corners k = make_corners(sx, sy, H, W, lbase, rs);
+          f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
+          v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
+          val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
+          ok = k.ok;
+        }
+        acc += ok ? val * (a[l * P + p] * inv) : z;
+      }
+    };
+    if (((W & (W - 1)) | (H & (H - 1))) == 0) points(std::true_type{});
+    else points(std::false_type{});
   }
   *reinterpret_cast<f4*>(out + pair * D + 4 * j) = acc;
 }
@@ -1178,6 +1217,8 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
   if (!output || !m2f::aligned(output, 16)) return m2f::fail(M2F_EINVAL, "%s: bad output", fn);
   const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
   hipStream_t st = static_cast<hipStream_t>(stream);
+  // value and out hold N * Lq(=S) * M * 32 elements; 32-bit offsets when those fit
+  const bool off32 = static_cast<int64_t>(d.N) * std::max(d.S, d.Lq) * d.M * d.D < (int64_t{1} << 31);
   static const bool tiled_env = [] {
     const char* e = std::getenv("M2F_MSDA_FWD_TILED");
     return !(e && e[0] == '0');
@@ -1188,7 +1229,9 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
     const int64_t nb = T * d.M * d.N;
     if (nb > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many workgroups", fn);
     const unsigned tg = static_cast<unsigned>(nb);
-#define M2F_FFT(LT) msda_fused_fwd<LT, true><<<tg, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output)
+#define M2F_FFT(LT)                                                                                           \
+  (off32 ? msda_fused_fwd<LT, true, true><<<tg, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output)  \
+         : msda_fused_fwd<LT, true, false><<<tg, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output))
     switch (d.L) {
       case 1: M2F_FFT(1); break;
       case 2: M2F_FFT(2); break;
@@ -1199,7 +1242,9 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
     return m2f::check_launch(fn);
   }
   const unsigned grid = m2f::ceil_div(d.npairs(), 32);
-#define M2F_FF(LT) msda_fused_fwd<LT, false><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output)
+#define M2F_FF(LT)                                                                                            \
+  (off32 ? msda_fused_fwd<LT, false, true><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output) \
+         : msda_fused_fwd<LT, false, false><<<grid, 256, 0, st>>>(value, fe, geo, d.npairs(), d.S, d.M, d.Lq, output))
   switch (d.L) {
     case 1: M2F_FF(1); break;
     case 2: M2F_FF(2); break;

@@ -47,6 +47,45 @@ __device__ __forceinline__ Corners make_corners(float locx, float locy, int H, i
   return k;
 }
 
+// make_corners with 32-bit element offsets (callers guarantee every offset < 2^31): the 64-bit multiply-adds
+// of the general form are quarter-rate VALU sequences, four per sample
+struct Corners32 {
+  int o1, o2, o3, o4;
+  float w1, w2, w3, w4;
+  bool c1, c2, c3, c4;
+  bool ok;
+};
+
+__device__ __forceinline__ Corners32 make_corners32(float locx, float locy, int H, int W, int lbase, int rs) {
+  Corners32 k;
+  const float h = locy * H - 0.5f;
+  const float w = locx * W - 0.5f;
+  k.ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
+  const float hs = k.ok ? h : -2.f, ws = k.ok ? w : -2.f;
+  const float fh = floorf(hs), fw = floorf(ws);
+  const int h0 = static_cast<int>(fh), w0 = static_cast<int>(fw);
+  const float ly = hs - fh, lx = ws - fw, hy = 1.f - ly, hx = 1.f - lx;
+  k.w1 = hy * hx; k.w2 = hy * lx; k.w3 = ly * hx; k.w4 = ly * lx;
+  k.c1 = h0 >= 0 && w0 >= 0;
+  k.c2 = h0 >= 0 && w0 + 1 <= W - 1;
+  k.c3 = h0 + 1 <= H - 1 && w0 >= 0;
+  k.c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
+  const int y0 = min(max(h0, 0), H - 1), y1 = min(max(h0 + 1, 0), H - 1);
+  const int x0 = min(max(w0, 0), W - 1), x1 = min(max(w0 + 1, 0), W - 1);
+  // one multiply for the block: the other corners are 0 / 1 pixel right and 0 / 1 row down of corner 1
+  const int dx = x1 != x0 ? rs : 0, dy = y1 != y0 ? W * rs : 0;
+  k.o1 = lbase + (y0 * W + x0) * rs;
+  k.o2 = k.o1 + dx;
+  k.o3 = k.o1 + dy;
+  k.o4 = k.o3 + dx;
+  return k;
+}
+
+// x / d for the sampling-offset normalisation (ms_deform_attn.py:106-109, offset / (W, H)).  When d is a
+// power of two, x * (1 / d) is the same correctly rounded value (both are exact scalings of x by 2^-k), so
+// the IEEE division sequence (about ten VALU) is skipped; otherwise it is a true division.
+__device__ __forceinline__ float div_norm(float x, float d, float inv, bool pow2) { return pow2 ? x * inv : x / d; }
+
 __device__ __forceinline__ f4 ld4(const float* p) { return *reinterpret_cast<const f4*>(p); }
 
 constexpr int kTileMaxL = 4;
@@ -76,6 +115,14 @@ __device__ __forceinline__ float sum8_dpp(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  return v;
+}
+
+// max over each aligned group of 8 lanes (exact and order-free, unlike a sum)
+__device__ __forceinline__ float max8_dpp(float v) {
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)));
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
+  v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false)));
   return v;
 }
 
