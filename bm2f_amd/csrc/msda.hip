@@ -642,15 +642,16 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             const float hy = 1.f - ly, hx = 1.f - lx;
             const bool c1 = h0 >= 0 && w0 >= 0, c2 = h0 >= 0 && w0 + 1 <= W - 1;
             const bool c3 = h0 + 1 <= H - 1 && w0 >= 0, c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
-            // per-corner channel dots with g, summed over the group; everything else is scalar.  Corners
-            // outside the level are zeroed by a select on the loaded rows (branch-free: a branch here makes
-            // the compiler sink the load into it and wait for it alone)
-            const f4 t1 = g * (c1 ? vb[pp][0] : z), t2 = g * (c2 ? vb[pp][1] : z);
-            const f4 t3 = g * (c3 ? vb[pp][2] : z), t4 = g * (c4 ? vb[pp][3] : z);
-            const float d1 = sum8_dpp(t1.x + t1.y + t1.z + t1.w);
-            const float d2 = sum8_dpp(t2.x + t2.y + t2.z + t2.w);
-            const float d3 = sum8_dpp(t3.x + t3.y + t3.z + t3.w);
-            const float d4 = sum8_dpp(t4.x + t4.y + t4.z + t4.w);
+            // per-corner channel dots with g, summed over the group; everything else is scalar.  A corner
+            // outside the level contributes nothing (as the reference, which skips it): its (clamped, in-level)
+            // row is loaded unconditionally and its reduced dot is selected away -- one select per corner, not
+            // four on the loaded vector, and no branch (a branch here makes the compiler sink the load into it)
+            const f4 t1 = g * vb[pp][0], t2 = g * vb[pp][1], t3 = g * vb[pp][2], t4 = g * vb[pp][3];
+            const float r1 = sum8_dpp(t1.x + t1.y + t1.z + t1.w);
+            const float r2 = sum8_dpp(t2.x + t2.y + t2.z + t2.w);
+            const float r3 = sum8_dpp(t3.x + t3.y + t3.z + t3.w);
+            const float r4 = sum8_dpp(t4.x + t4.y + t4.z + t4.w);
+            const float d1 = c1 ? r1 : 0.f, d2 = c2 ? r2 : 0.f, d3 = c3 ? r3 : 0.f, d4 = c4 ? r4 : 0.f;
             const float pa = (hy * hx) * d1 + (hy * lx) * d2 + (ly * hx) * d3 + (ly * lx) * d4;
             const float px = a * (hy * (d2 - d1) + ly * (d4 - d3));
             const float py = a * (hx * (d3 - d1) + lx * (d4 - d2));
@@ -694,6 +695,20 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         if (j < LP) gl[j] = dq[3 * j + 2] * (myga0 - dot);
         if (j + 8 < LP) gl[j + 8] = dq[3 * (j + 8) + 2] * (myga1 - dot);
       }
+      // the query's descriptors become phase 3's corner-coefficient form {(1 - ly) a, ly a, lx}: a record
+      // visit then multiplies two LDS values instead of re-deriving both fractions (lane j: samples j, j + 8)
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int k = j + 8 * r;
+        if (k < LP) {
+          float* dk = desc + (qi * LP + k) * 3;
+          const float h = dk[0], w = dk[1], a = dk[2];
+          const float ly = h - floorf(h), lx = w - floorf(w);
+          dk[0] = (1.f - ly) * a;
+          dk[1] = ly * a;
+          dk[2] = lx;
+        }
+      }
     }
   }
   __syncthreads();
@@ -733,13 +748,13 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           int i = s0;
           for (; i + 1 < s1; i += 2) {
             const int sa = slots[i], sb = slots[i + 1];
-            const float ha = desc[3 * sa], wa = desc[3 * sa + 1], aa = desc[3 * sa + 2];
-            const float hb = desc[3 * sb], wb = desc[3 * sb + 1], ab = desc[3 * sb + 2];
+            // descriptors in coefficient form {(1 - ly) a, ly a, lx} (end of phase 2)
+            const float Aa = desc[3 * sa + ((c & 2) ? 1 : 0)], lxa = desc[3 * sa + 2];
+            const float Ab = desc[3 * sb + ((c & 2) ? 1 : 0)], lxb = desc[3 * sb + 2];
             const f4* ga = reinterpret_cast<const f4*>(gsh + (sa / LP) * D + CPL * jl);
             const f4* gb = reinterpret_cast<const f4*>(gsh + (sb / LP) * D + CPL * jl);
-            const float lya = ha - floorf(ha), lxa = wa - floorf(wa), lyb = hb - floorf(hb), lxb = wb - floorf(wb);
-            const float ca = ((c & 2) ? lya : 1.f - lya) * ((c & 1) ? lxa : 1.f - lxa) * aa;
-            const float cb = ((c & 2) ? lyb : 1.f - lyb) * ((c & 1) ? lxb : 1.f - lxb) * ab;
+            const float ca = Aa * ((c & 1) ? lxa : 1.f - lxa);
+            const float cb = Ab * ((c & 1) ? lxb : 1.f - lxb);
 #pragma unroll
             for (int k = 0; k < CPL / 4; ++k) {
               const f4 va = ga[k], vb2 = gb[k];
@@ -749,10 +764,9 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           }
           if (i < s1) {
             const int sa = slots[i];
-            const float ha = desc[3 * sa], wa = desc[3 * sa + 1], aa = desc[3 * sa + 2];
+            const float Aa = desc[3 * sa + ((c & 2) ? 1 : 0)], lxa = desc[3 * sa + 2];
             const f4* ga = reinterpret_cast<const f4*>(gsh + (sa / LP) * D + CPL * jl);
-            const float lya = ha - floorf(ha), lxa = wa - floorf(wa);
-            const float ca = ((c & 2) ? lya : 1.f - lya) * ((c & 1) ? lxa : 1.f - lxa) * aa;
+            const float ca = Aa * ((c & 1) ? lxa : 1.f - lxa);
 #pragma unroll
             for (int k = 0; k < CPL / 4; ++k) {
               const f4 va = ga[k];
