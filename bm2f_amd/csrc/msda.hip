@@ -586,7 +586,10 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortPerThread; ++r)
-      if (cell[r] >= 0) slots[cstart[cell[r]] + rank[r]] = static_cast<unsigned short>(tid + r * kBwdThreads);
+      if (cell[r] >= 0) {  // slot = query << 4 | sample-in-query (phase 3 then needs no division by L*P)
+        const int sid = tid + r * kBwdThreads, qs = sid / LP;
+        slots[cstart[cell[r]] + rank[r]] = static_cast<unsigned short>((qs << 4) | (sid - qs * LP));
+      }
   }
   __syncthreads();
   M2F_STAMP(2)
@@ -646,11 +649,9 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             // outside the level contributes nothing (as the reference, which skips it): its (clamped, in-level)
             // row is loaded unconditionally and its reduced dot is selected away -- one select per corner, not
             // four on the loaded vector, and no branch (a branch here makes the compiler sink the load into it)
-            const f4 t1 = g * vb[pp][0], t2 = g * vb[pp][1], t3 = g * vb[pp][2], t4 = g * vb[pp][3];
-            const float r1 = sum8_dpp(t1.x + t1.y + t1.z + t1.w);
-            const float r2 = sum8_dpp(t2.x + t2.y + t2.z + t2.w);
-            const float r3 = sum8_dpp(t3.x + t3.y + t3.z + t3.w);
-            const float r4 = sum8_dpp(t4.x + t4.y + t4.z + t4.w);
+            auto dot4 = [&](const f4& v) { return fmaf(g.w, v.w, fmaf(g.z, v.z, fmaf(g.y, v.y, g.x * v.x))); };
+            const float r1 = sum8_dpp(dot4(vb[pp][0])), r2 = sum8_dpp(dot4(vb[pp][1]));
+            const float r3 = sum8_dpp(dot4(vb[pp][2])), r4 = sum8_dpp(dot4(vb[pp][3]));
             const float d1 = c1 ? r1 : 0.f, d2 = c2 ? r2 : 0.f, d3 = c3 ? r3 : 0.f, d4 = c4 ? r4 : 0.f;
             const float pa = (hy * hx) * d1 + (hy * lx) * d2 + (ly * hx) * d3 + (ly * lx) * d4;
             const float px = a * (hy * (d2 - d1) + ly * (d4 - d3));
@@ -747,31 +748,33 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           // two records per step: their LDS reads overlap
           int i = s0;
           for (; i + 1 < s1; i += 2) {
-            const int sa = slots[i], sb = slots[i + 1];
+            const unsigned pa = slots[i], pb = slots[i + 1];
+            const unsigned qa = pa >> 4, qb = pb >> 4;
+            const unsigned sa = __umul24(qa, LP) + (pa & 15u), sb = __umul24(qb, LP) + (pb & 15u);
             // descriptors in coefficient form {(1 - ly) a, ly a, lx} (end of phase 2)
             const float Aa = desc[3 * sa + ((c & 2) ? 1 : 0)], lxa = desc[3 * sa + 2];
             const float Ab = desc[3 * sb + ((c & 2) ? 1 : 0)], lxb = desc[3 * sb + 2];
-            const f4* ga = reinterpret_cast<const f4*>(gsh + (sa / LP) * D + CPL * jl);
-            const f4* gb = reinterpret_cast<const f4*>(gsh + (sb / LP) * D + CPL * jl);
+            const f4* ga = reinterpret_cast<const f4*>(gsh + qa * D + CPL * jl);
+            const f4* gb = reinterpret_cast<const f4*>(gsh + qb * D + CPL * jl);
             const float ca = Aa * ((c & 1) ? lxa : 1.f - lxa);
             const float cb = Ab * ((c & 1) ? lxb : 1.f - lxb);
 #pragma unroll
-            for (int k = 0; k < CPL / 4; ++k) {
+            for (int k = 0; k < CPL / 4; ++k) {  // fma chains (pairs of channels pack into v_pk_fma_f32)
               const f4 va = ga[k], vb2 = gb[k];
-              acc[4 * k] += ca * va.x + cb * vb2.x; acc[4 * k + 1] += ca * va.y + cb * vb2.y;
-              acc[4 * k + 2] += ca * va.z + cb * vb2.z; acc[4 * k + 3] += ca * va.w + cb * vb2.w;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(cb, vb2[e], fmaf(ca, va[e], acc[4 * k + e]));
             }
           }
           if (i < s1) {
-            const int sa = slots[i];
+            const unsigned pa = slots[i], qa = pa >> 4, sa = __umul24(qa, LP) + (pa & 15u);
             const float Aa = desc[3 * sa + ((c & 2) ? 1 : 0)], lxa = desc[3 * sa + 2];
-            const f4* ga = reinterpret_cast<const f4*>(gsh + (sa / LP) * D + CPL * jl);
+            const f4* ga = reinterpret_cast<const f4*>(gsh + qa * D + CPL * jl);
             const float ca = Aa * ((c & 1) ? lxa : 1.f - lxa);
 #pragma unroll
             for (int k = 0; k < CPL / 4; ++k) {
               const f4 va = ga[k];
-              acc[4 * k] += ca * va.x; acc[4 * k + 1] += ca * va.y;
-              acc[4 * k + 2] += ca * va.z; acc[4 * k + 3] += ca * va.w;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(ca, va[e], acc[4 * k + e]);
             }
           }
         }
