@@ -416,12 +416,27 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   const int Qt = ts.qc[LT];
   const int nsamp = Qt * LP;
 
-  // ---- phase 0a: this head's grad_output rows of the tile's queries -> LDS (float4 per lane) --------
-  for (int idx = tid; idx < Qt * 8; idx += blockDim.x) {
-    const int qi = idx >> 3, j = idx & 7;
-    const int q = tile_query(ts, geo, qi);
-    const int64_t pair = (static_cast<int64_t>(n) * S + q) * M + m;
-    *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = ld4(gout + pair * D + 4 * j);
+  // ---- phase 0a: this head's grad_output rows of the tile's queries -> LDS (float4 per lane), the loads of
+  // a thread's rows issued together (a load-store loop waits out each load in turn) -----------------------
+  {
+    constexpr int kGPre = 3;  // max_qt * 8 <= 3 * TPB at the default geometries; the rest loops
+    f4 gpre[kGPre];
+#pragma unroll
+    for (int u = 0; u < kGPre; ++u) {
+      const int idx = min(tid + u * kBwdThreads, Qt * 8 - 1), qi = idx >> 3, j = idx & 7;
+      const int64_t pair = (static_cast<int64_t>(n) * S + tile_query(ts, geo, qi)) * M + m;
+      gpre[u] = ld4(gout + pair * D + 4 * j);
+    }
+#pragma unroll
+    for (int u = 0; u < kGPre; ++u) {
+      const int idx = tid + u * kBwdThreads;
+      if (idx < Qt * 8) *reinterpret_cast<f4*>(gsh + (idx >> 3) * D + 4 * (idx & 7)) = gpre[u];
+    }
+    for (int idx = tid + kGPre * kBwdThreads; idx < Qt * 8; idx += kBwdThreads) {
+      const int qi = idx >> 3, j = idx & 7;
+      const int64_t pair = (static_cast<int64_t>(n) * S + tile_query(ts, geo, qi)) * M + m;
+      *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = ld4(gout + pair * D + 4 * j);
+    }
   }
 
   // ---- phase 0b: sample descriptors (one lane per (query, level)) and the touched-corner boxes --------
