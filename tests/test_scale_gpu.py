@@ -328,10 +328,15 @@ def test_ddp_rccl_world1_matches_unwrapped(device, tmp_path):
         for step in range(2):
             ld = train_step(ddp, opt_d, images, torch.bfloat16)
             lr = train_step(ref_model, opt_r, images, torch.bfloat16)
-            train_step(ref_model2, opt_r2, images, torch.bfloat16)
-            torch.testing.assert_close(ld, lr, rtol=1e-3, atol=1e-6)
-            if step:
-                break  # the second step exercises the optimizer on the reduced gradients; its inputs differ slightly
+            lr2 = train_step(ref_model2, opt_r2, images, torch.bfloat16)
+            if step == 0:
+                torch.testing.assert_close(ld, lr, rtol=1e-3, atol=1e-6)
+            else:
+                # after one AdamW step the weights carry the first step's non-repeatable gradients (AdamW's first
+                # update is ~lr * sign(g), so near-zero gradients flip): the bar is the unwrapped runs' own spread
+                spread = (lr2 - lr).abs().item()
+                assert (ld - lr).abs().item() <= 4 * spread + 1e-3 * lr.abs().item(), (ld, lr, lr2)
+                break  # the second step exercises the optimizer on the reduced gradients
             worst = (0.0, "")
             for (n, pd_), (_, pr), (_, pr2) in zip(ddp.module.named_parameters(), ref_model.named_parameters(),
                                                    ref_model2.named_parameters()):
