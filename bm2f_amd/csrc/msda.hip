@@ -931,7 +931,10 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
           val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
           ok = k.ok;
         }
-        acc += ok ? val * (a[l * P + p] * inv) : z;
+        // a not-ok sample's corners are all zeroed above, so its weight can be folded to 0: one fma per channel
+        const float wa = ok ? a[l * P + p] * inv : 0.f;
+        acc.x = fmaf(val.x, wa, acc.x); acc.y = fmaf(val.y, wa, acc.y);
+        acc.z = fmaf(val.z, wa, acc.z); acc.w = fmaf(val.w, wa, acc.w);
       }
     };
     if (((W & (W - 1)) | (H & (H - 1))) == 0) points(std::true_type{});
