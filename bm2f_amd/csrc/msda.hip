@@ -920,9 +920,12 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
         bool ok;
         if constexpr (OFF32) {
           const Corners32 k = make_corners32(sx, sy, H, W, static_cast<int>(lbase), static_cast<int>(rs));
-          f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
-          v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
-          val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
+          const f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
+          // a corner outside the level gets weight 0 instead of a zeroed row (one select, not four): its clamped
+          // row is always another corner of the same sample, so the output is non-finite in exactly the
+          // elements where the reference's is (only Inf may read as NaN); finite inputs give the same sum
+          const float w1 = k.c1 ? k.w1 : 0.f, w2 = k.c2 ? k.w2 : 0.f, w3 = k.c3 ? k.w3 : 0.f, w4 = k.c4 ? k.w4 : 0.f;
+          val = w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
           ok = k.ok;
         } else {
           const Corners k = make_corners(sx, sy, H, W, lbase, rs);
