@@ -195,10 +195,10 @@ __global__ void __launch_bounds__(256) msda_fwd_f32_vec(
       const float2 xy = *reinterpret_cast<const float2*>(lp + 2 * kk);
       const float a = ap[kk];
       const Corners k = make_corners(xy.x, xy.y, H, W, lbase, rs);
-      f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
+      const f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
       const f4 z = {0.f, 0.f, 0.f, 0.f};
-      v1 = k.c1 ? v1 : z; v2 = k.c2 ? v2 : z; v3 = k.c3 ? v3 : z; v4 = k.c4 ? v4 : z;
-      const f4 val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
+      const f4 u1 = k.c1 ? v1 : z, u2 = k.c2 ? v2 : z, u3 = k.c3 ? v3 : z, u4 = k.c4 ? v4 : z;
+      const f4 val = k.w1 * u1 + k.w2 * u2 + k.w3 * u3 + k.w4 * u4;
       acc += k.ok ? val * a : z;
     }
   }
@@ -921,9 +921,10 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
         if constexpr (OFF32) {
           const Corners32 k = make_corners32(sx, sy, H, W, static_cast<int>(lbase), static_cast<int>(rs));
           const f4 v1 = ld4(value + k.o1), v2 = ld4(value + k.o2), v3 = ld4(value + k.o3), v4 = ld4(value + k.o4);
-          // a corner outside the level gets weight 0 instead of a zeroed row (one select, not four): its clamped
-          // row is always another corner of the same sample, so the output is non-finite in exactly the
-          // elements where the reference's is (only Inf may read as NaN); finite inputs give the same sum
+          // a corner outside the level of an in-range sample gets weight 0 instead of a zeroed row (one select,
+          // not four): its clamped row is always another corner of the same sample, so the output is non-finite
+          // in exactly the elements where the reference's is (only Inf may read as NaN); an out-of-range sample
+          // (clamped onto the level's first pixel) is dropped by the select on its sum below
           const float w1 = k.c1 ? k.w1 : 0.f, w2 = k.c2 ? k.w2 : 0.f, w3 = k.c3 ? k.w3 : 0.f, w4 = k.c4 ? k.w4 : 0.f;
           val = w1 * v1 + w2 * v2 + w3 * v3 + w4 * v4;
           ok = k.ok;
@@ -934,8 +935,9 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
           val = k.w1 * v1 + k.w2 * v2 + k.w3 * v3 + k.w4 * v4;
           ok = k.ok;
         }
-        // a not-ok sample's corners are all zeroed above, so its weight can be folded to 0: one fma per channel
-        const float wa = ok ? a[l * P + p] * inv : 0.f;
+        // a not-ok sample is dropped by one select on its sum, then one fma per channel
+        const float wa = a[l * P + p] * inv;
+        val = ok ? val : z;
         acc.x = fmaf(val.x, wa, acc.x); acc.y = fmaf(val.y, wa, acc.y);
         acc.z = fmaf(val.z, wa, acc.z); acc.w = fmaf(val.w, wa, acc.w);
       }

@@ -232,6 +232,48 @@ def test_tiled_backward_nonfinite_and_zero_grads(device):
     np.testing.assert_allclose(got[fin], want[fin], rtol=1e-3, atol=1e-5 * np.abs(want[fin]).max())
 
 
+def test_forward_nonfinite_values_like_oracle(device):
+    """Both forwards (the reference-API op and the fused front end) read a corner outside the level from a
+    clamped row and drop it by a zero weight, and drop a sample outside (-1, H) x (-1, W) by a select on its
+    sum.  With non-finite values on every level's first pixel (where out-of-range samples are clamped) and
+    one interior NaN, the outputs must be non-finite in exactly the oracle's elements and equal elsewhere."""
+    from bm2f_amd import msda
+    shapes = [(4, 4), (8, 8), (16, 16)]
+    value, st, lsi, loc, attn, _ = _pyramid_case(shapes, 2, 8, 0.25, 11)
+    for l0 in lsi.tolist():
+        value[:, l0, :, :3] = float("inf")
+    value[1, 40, 2, 7] = float("nan")
+    dst = msda.attach_host_shapes(st.to(device), shapes)
+    want = msda_ref.msda_forward(value.double(), st, lsi, loc.double(), attn.double())
+    got = msda.ms_deform_attn_forward(value.to(device), dst, lsi.to(device), loc.to(device), attn.to(device),
+                                      64).cpu().double().numpy().reshape(want.shape)
+    assert np.array_equal(np.isfinite(got), np.isfinite(want))
+    fin = np.isfinite(want)
+    np.testing.assert_allclose(got[fin], want[fin], rtol=1e-4, atol=1e-5 * np.abs(want[fin]).max())
+    # the fused front end on the same samples: proj = [offsets in pixels from the reference points | logits
+    # whose softmax is attn]
+    N, S, M, L, P = loc.shape[0], loc.shape[1], loc.shape[2], loc.shape[3], loc.shape[4]
+    refs = []
+    for h, w in shapes:
+        ys, xs = torch.meshgrid(torch.linspace(0.5, h - 0.5, h), torch.linspace(0.5, w - 0.5, w), indexing="ij")
+        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
+    ref = torch.cat(refs, 0)[None, :, None, :].expand(N, S, L, 2).contiguous()
+    norm = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32)
+    off = (loc - ref[:, :, None, :, None, :]) * norm[None, None, None, :, None, :]
+    logits = attn.reshape(N, S, M, L * P).log()
+    proj = torch.cat([off.reshape(N, S, -1), logits.reshape(N, S, -1)], -1).contiguous()
+    out = msda.MSDeformAttnFusedFunction.apply(value.to(device), proj.to(device), ref.to(device), shapes, P)
+    # the fused path recomputes loc and attn (softmax of log attn, ref + off / (W, H)) in fp32: same
+    # finite pattern as the oracle on the materialised tensors, values within the rounding of that round trip
+    sm = torch.softmax(logits, -1).reshape(attn.shape)
+    loc2 = ref[:, :, None, :, None, :] + off / norm[None, None, None, :, None, :]
+    want2 = msda_ref.msda_forward(value.double(), st, lsi, loc2.double(), sm.double())
+    got2 = out.cpu().double().numpy().reshape(want2.shape)
+    assert np.array_equal(np.isfinite(got2), np.isfinite(want2))
+    fin2 = np.isfinite(want2)
+    np.testing.assert_allclose(got2[fin2], want2[fin2], rtol=1e-3, atol=1e-4 * np.abs(want2[fin2]).max())
+
+
 @pytest.mark.parametrize("shapes", [[(4, 4), (8, 8), (16, 16)], [(6, 10), (12, 20), (24, 40)], [(5, 7), (10, 13)]])
 def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
     """MSDeformAttn with the fused front end == the reference-structured path (Linear -> softmax -> loc ->
