@@ -621,6 +621,10 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       const f4 g = *reinterpret_cast<const f4*>(gsh + qi * D + 4 * j);
       const float* dq = desc + qi * LP * 3;
       float dot = 0.f, myga0 = 0.f, myga1 = 0.f;
+      // the query's out-of-window flags (LP <= 16 bits) from the two words they can straddle, read once
+      const int sid0 = qi * LP, sh = sid0 & 31;
+      const unsigned w0 = oow[sid0 >> 5], w1 = oow[min((sid0 + LP - 1) >> 5, (nsamp_max + 31) / 32 - 1)];
+      const unsigned qfar = (sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0) & ((1u << LP) - 1u);
 #pragma unroll 1
       for (int l = 0; l < LT; ++l) {
         const int H = geo.H[l], W = geo.W[l];
@@ -643,7 +647,8 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             const int y0 = min(max(h0, 0), H - 1), y1 = min(max(h0 + 1, 0), H - 1);
             const int x0 = min(max(w0, 0), W - 1), x1 = min(max(w0 + 1, 0), W - 1);
             // one multiply per sample: corners 2-4 are 0 / 1 pixel right and 0 / 1 row down of corner 1
-            const int o1 = lbase + (y0 * W + x0) * rs, dx = x1 != x0 ? rs : 0, dy = y1 != y0 ? Wrs : 0;
+            const int o1 = lbase + static_cast<int>(__umul24(__umul24(y0, W) + x0, rs));  // 24-bit products
+            const int dx = x1 != x0 ? rs : 0, dy = y1 != y0 ? Wrs : 0;
             vb[pp][0] = ld4(value + o1);
             vb[pp][1] = ld4(value + o1 + dx);
             vb[pp][2] = ld4(value + o1 + dy);
@@ -682,8 +687,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
               if (j == p) st_a = ok ? pa : 0.f;
               if ((j >> 1) == p) st_l = ok ? ((j & 1) ? H * py : W * px) : 0.f;
             }
-            const int sid = qi * LP + k;
-            if (ok && ((oow[sid >> 5] >> (sid & 31)) & 1u)) {
+            if (ok && ((qfar >> k) & 1u)) {
               // outside the window: the 4 corner rows go straight to HBM (fp32 atomics, as the reference)
               const f4 tg = g * a;
               const int o1 = lbase + (min(max(h0, 0), H - 1) * W + min(max(w0, 0), W - 1)) * rs;
