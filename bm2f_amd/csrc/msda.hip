@@ -444,8 +444,15 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     int bmin_y[LT], bmax_y[LT], bmin_x[LT], bmax_x[LT];
 #pragma unroll
     for (int l = 0; l < LT; ++l) { bmin_y[l] = 0x7fffffff; bmax_y[l] = -1; bmin_x[l] = 0x7fffffff; bmax_x[l] = -1; }
-    for (int t = tid; t < Qt * LT; t += blockDim.x) {
-      const int qi = t / LT, l = t - qi * LT;
+    // FUSED: a quad of lanes per query (lane l < LT handles level l), so the softmax over the pair's L*P
+    // logits is shared: each lane exps its level's P logits, the quad max is a DPP reduction (exact), and
+    // the sum is carried from lane to lane in logit order (the sequential sum the forward forms)
+    constexpr int TPQ = FUSED ? 4 : LT;  // tasks per query
+    static_assert(!FUSED || LT <= 4, "one quad lane per level");
+    for (int t = tid; t < Qt * TPQ; t += blockDim.x) {  // whole quads enter and leave together
+      const int qi = t / TPQ, lt = t - qi * TPQ;
+      const bool act = lt < LT;
+      const int l = act ? lt : LT - 1;  // a spare quad lane mirrors the last level (its results are dropped)
       const int q = tile_query(ts, geo, qi);
       const int64_t nq = static_cast<int64_t>(n) * S + q;
       const int H = geo.H[l], W = geo.W[l];
@@ -453,13 +460,38 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       if constexpr (FUSED) {
         const float* prow = fe.proj + nq * fe.ld;
         const float* lg = prow + M * LP * 2 + m * LP;
-        float e[LP];
+        float x[P];
         float mx = -INFINITY;
 #pragma unroll
-        for (int k = 0; k < LP; ++k) { e[k] = lg[k]; mx = fmaxf(mx, e[k]); }
-        float sum = 0.f;
+        for (int p = 0; p < P; ++p) { x[p] = lg[l * P + p]; mx = fmaxf(mx, x[p]); }
+        mx = fmaxf(mx, qperm<0xB1>(mx));  // quad lanes 1 0 3 2
+        mx = fmaxf(mx, qperm<0x4E>(mx));  // quad lanes 2 3 0 1
 #pragma unroll
-        for (int k = 0; k < LP; ++k) sum += expf(e[k] - mx);
+        for (int p = 0; p < P; ++p) x[p] = expf(x[p] - mx);
+        float run = 0.f;
+#pragma unroll
+        for (int ll = 0; ll < LT; ++ll) {
+          float prev = 0.f;
+          if (ll > 0) {
+            switch (ll) {  // broadcast quad lane ll - 1 (the DPP control must be an immediate)
+              case 1: prev = qperm<0x00>(run); break;
+              case 2: prev = qperm<0x55>(run); break;
+              default: prev = qperm<0xAA>(run); break;
+            }
+          }
+          if (lt == ll) {
+            run = prev;
+#pragma unroll
+            for (int p = 0; p < P; ++p) run += x[p];
+          }
+        }
+        float sum;
+        switch (LT) {
+          case 1: sum = qperm<0x00>(run); break;
+          case 2: sum = qperm<0x55>(run); break;
+          case 3: sum = qperm<0xAA>(run); break;
+          default: sum = qperm<0xFF>(run); break;
+        }
         const float inv = 1.f / sum;
         const float2 rf = *reinterpret_cast<const float2*>(fe.ref + n * fe.ref_bs + (static_cast<int64_t>(q) * LT + l) * 2);
         const float* of = prow + (m * LP + l * P) * 2;
@@ -472,7 +504,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             const float2 off = *reinterpret_cast<const float2*>(of + 2 * p);
             lx[p] = rf.x + div_norm(off.x, fW, iW, POW2);
             ly[p] = rf.y + div_norm(off.y, fH, iH, POW2);
-            av[p] = expf(lg[l * P + p] - mx) * inv;
+            av[p] = x[p] * inv;
           }
         };
         if (((W & (W - 1)) | (H & (H - 1))) == 0) points(std::true_type{});
@@ -487,6 +519,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           av[p] = attn[kb + p];
         }
       }
+      if (!act) continue;
       float* dq = desc + (qi * LP + l * P) * 3;
 #pragma unroll
       for (int p = 0; p < P; ++p) {

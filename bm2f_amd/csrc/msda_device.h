@@ -118,6 +118,12 @@ __device__ __forceinline__ float sum8_dpp(float v) {
   return v;
 }
 
+// DPP quad permutation (CTRL = quad_perm selector) of a float
+template <int CTRL>
+__device__ __forceinline__ float qperm(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
 // max over each aligned group of 8 lanes (exact and order-free, unlike a sum)
 __device__ __forceinline__ float max8_dpp(float v) {
   v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false)));
