@@ -799,8 +799,13 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           any |= s1 > s0;
           // two records per step: their LDS reads overlap
           int i = s0;
+          // the next pair's slots are read one step ahead (clamped into the range), so a step waits on one
+          // LDS round trip (descriptors and g rows) instead of two
+          unsigned npa = slots[max(min(i, s1 - 1), 0)], npb = slots[max(min(i + 1, s1 - 1), 0)];
           for (; i + 1 < s1; i += 2) {
-            const unsigned pa = slots[i], pb = slots[i + 1];
+            const unsigned pa = npa, pb = npb;
+            npa = slots[min(i + 2, s1 - 1)];
+            npb = slots[min(i + 3, s1 - 1)];
             const unsigned qa = pa >> 4, qb = pb >> 4;
             const unsigned sa = __umul24(qa, LP) + (pa & 15u), sb = __umul24(qb, LP) + (pb & 15u);
             // descriptors in coefficient form {(1 - ly) a, ly a, lx} (end of phase 2)
@@ -818,7 +823,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             }
           }
           if (i < s1) {
-            const unsigned pa = slots[i], qa = pa >> 4, sa = __umul24(qa, LP) + (pa & 15u);
+            const unsigned pa = npa, qa = pa >> 4, sa = __umul24(qa, LP) + (pa & 15u);
             const float Aa = desc[3 * sa + ((c & 2) ? 1 : 0)], lxa = desc[3 * sa + 2];
             const f4* ga = reinterpret_cast<const f4*>(gsh + qa * D + CPL * jl);
             const float ca = Aa * ((c & 1) ? lxa : 1.f - lxa);
