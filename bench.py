@@ -2,7 +2,7 @@
 """Benchmark: images/sec of the Mask2Former R50 training step (fwd + bwd + AdamW) on synthetic
 1024x1024 batches, 16 images per GPU (BASELINE.json config 2; config 3 at --gpus 8).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 16] [--res 1024] [--amp bf16|fp16|none]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 16] [--res 1024] [--amp fp16|bf16|none]
 
 One process per GPU.  ``--gpus N`` with N > 1 outside torch.distributed.run starts
 ``python -m torch.distributed.run --nproc-per-node N`` itself (before touching the GPU) and exits with its
@@ -15,8 +15,13 @@ Besides the contract fields it reports:
                 launch (profiles/msda_bwd_traffic.json).
   roofline_all  the same for every hand-written kernel family (HBM- or MFMA-bound as DESIGN.md §3 says),
                 from extra instrumented steps after the timed region (the timed steps carry no events).
-  modes         N=1 only: the same step under AMP fp16 (the reference's training dtype, with a GradScaler
-                as detectron2's AMPTrainer) and with no autocast at all (fp32 parity mode), fewer steps.
+  The headline runs under AMP fp16 with a GradScaler, the reference's training precision
+  (Base-COCO-PanopticSegmentation.yaml SOLVER.AMP.ENABLED; detectron2's AMPTrainer).
+  modes         N=1 only: the same step under AMP bf16 (no scaler) and with no autocast at all (fp32 parity
+                mode), fewer steps.
+  achievable    N=1 only: measured ceilings on this box -- a nontemporal float4 stream copy (m2f_stream_copy,
+                2 x 2 GiB per launch) and an 8192^3 bf16 GEMM (hipBLASLt via torch.matmul) -- so each roofline
+                entry carries its fraction of the spec peak (frac) and of the measured one (frac_achievable).
   cpu_baseline  the reference's CPU path (oracle/cpu_path.py) on config 1 (1 x 512^2) and one 1024^2 image,
                 warm-up 1, median of 3, rank 0, N=1; value = the 1024^2 img/s.
   env           every M2F_* variable in the environment.  The bench refuses to run with any set (they select
@@ -49,14 +54,15 @@ def log(msg):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=16, help="images per GPU")
     ap.add_argument("--res", type=int, default=1024)
     ap.add_argument("--queries", type=int, default=100)
-    ap.add_argument("--amp", default="bf16", choices=["bf16", "fp16", "none"])
+    ap.add_argument("--amp", default="fp16", choices=["fp16", "bf16", "none"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-modes", action="store_true", help="skip the fp16 / fp32 mode lines")
+    ap.add_argument("--no-modes", action="store_true", help="skip the bf16 / fp32 mode lines")
+    ap.add_argument("--no-peaks", action="store_true", help="skip the achievable-peak probes")
     ap.add_argument("--mode-steps", type=int, default=4)
     ap.add_argument("--kernel-steps", type=int, default=2, help="instrumented steps for roofline_all")
     ap.add_argument("--allow-knobs", action="store_true")
@@ -231,6 +237,49 @@ def msda_bwd_bytes(n_images, res, M=8, D=32, L=3, P=4):
     return 2 * value + 2 * loc + 2 * attn + value  # reads v,loc,attn,gout; writes gv,gloc,gattn
 
 
+def measure_peaks(device):
+    """Achievable ceilings on this box: HBM by a nontemporal stream copy, MFMA by a large bf16 GEMM."""
+    import torch
+    from bm2f_amd import _native
+    st = torch.cuda.current_stream(device)
+    nbytes = 2 << 30
+    a = torch.empty(nbytes, dtype=torch.uint8, device=device).fill_(1)
+    b = torch.empty_like(a)
+
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(reps):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        return s.elapsed_time(e) / reps * 1e-3
+
+    t_copy = timed(lambda: _native.call("m2f_stream_copy", a.data_ptr(), b.data_ptr(), nbytes, st.cuda_stream), 20)
+    del a, b
+    n = 8192
+    x = torch.randn(n, n, device=device, dtype=torch.bfloat16)
+    y = torch.randn(n, n, device=device, dtype=torch.bfloat16)
+    out = torch.empty(n, n, device=device, dtype=torch.bfloat16)
+    t_mm = timed(lambda: torch.matmul(x, y, out=out), 20)
+    del x, y, out
+    torch.cuda.empty_cache()
+    return {"hbm_gbs": round(2 * nbytes / t_copy / 1e9, 1), "bf16_gemm_tflops": round(2 * n ** 3 / t_mm / 1e12, 1),
+            "hbm_probe": "m2f_stream_copy: nontemporal float4 copy, 2 GiB in + 2 GiB out per launch, mean of 20",
+            "mfma_probe": f"torch.matmul bf16 {n}x{n}x{n} (hipBLASLt), mean of 20"}
+
+
+def add_achievable(ent, peaks):
+    if not peaks or not ent:
+        return ent
+    key = "hbm_gbs" if ent.get("unit") == "GB/s" else "bf16_gemm_tflops"
+    ent["achievable_peak"] = peaks[key]
+    ent["frac_achievable"] = round(ent["achieved"] / peaks[key], 4)
+    return ent
+
+
 def load_traffic():
     path = os.path.join(ROOT, "profiles", "msda_bwd_traffic.json")
     try:
@@ -308,6 +357,10 @@ def main():
         return elapsed
 
     elapsed = run(args.amp, args.steps, args.warmup, "timed")
+    peaks = None
+    if world == 1 and not args.no_peaks:
+        peaks = measure_peaks(device)
+        log(f"achievable peaks: {peaks}")
 
     # instrumented steps (after the timed region): per-kernel-family durations and algorithmic work
     kern = {}
@@ -321,12 +374,12 @@ def main():
     modes = None
     if world == 1 and not args.no_modes:
         modes = {}
-        for name in ("fp16", "none"):
+        for name in ("fp16", "bf16", "none"):
             if name == args.amp:
                 continue
             torch.cuda.empty_cache()
             el = run(name, args.mode_steps, 2, f"mode {name}")
-            key = "amp_fp16" if name == "fp16" else "fp32_parity"
+            key = {"fp16": "amp_fp16", "bf16": "amp_bf16", "none": "fp32_parity"}[name]
             modes[key] = {"value": round(world * args.batch * args.mode_steps / el, 3), "unit": "images/s",
                           "ms_per_step": round(el / args.mode_steps * 1e3, 3), "steps": args.mode_steps, "warmup": 2,
                           "autocast": None if name == "none" else name,
@@ -345,8 +398,10 @@ def main():
                     "traffic": (tr or {}).get("hbm_bytes_per_launch") if tr else None,
                     "kernel": "MSDA backward (m2f_msda_fused_bwd_f32)",
                     "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(bwd["mean_ms"], 4)}
+            add_achievable(roof, peaks)
         bounds = {v[0]: v[1] for v in ENTRIES.values()}
-        roof_all = [roofline_entry(fam, k, bounds[fam]) for fam, k in sorted(kern.items(), key=lambda x: -x[1]["total_ms"])]
+        roof_all = [add_achievable(roofline_entry(fam, k, bounds[fam]), peaks)
+                    for fam, k in sorted(kern.items(), key=lambda x: -x[1]["total_ms"])]
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             from oracle.cpu_path import cpu_model, time_cpu_step
@@ -368,11 +423,12 @@ def main():
             "data": "synthetic (randn images, random-init weights)",
             "config": {"workload": "config 2: Mask2Former R50 COCO-panoptic, 100 queries, 1024x1024, "
                                    f"{args.batch} images/GPU, fwd+bwd+AdamW; pixel decoder + MSDA in fp32 "
-                                   f"(as the reference forces), backbone/decoder under AMP {args.amp}",
+                                   f"(as the reference forces), backbone/decoder under AMP {args.amp}"
+                                   + (" with GradScaler" if args.amp == "fp16" else ""),
                        "model": "maskformer2_R50", "global_batch": world * args.batch,
                        "seq_len": sum((args.res // s) ** 2 for s in (32, 16, 8)), "queries": args.queries,
                        "parallelism": f"dp{world}", "env": knobs},
-            "roofline": roof, "roofline_all": roof_all, "modes": modes, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_all": roof_all, "achievable": peaks, "modes": modes, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -8,6 +8,7 @@ reference's silent pure-PyTorch fallback (ops/modules/ms_deform_attn.py:116-121)
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -59,6 +60,9 @@ _SIGNATURES = {
     "m2f_upsample2x_bwd_f32": [_p, _p, _i, _i, _i, _i, _p],
     "m2f_maxpool3s2_fwd": [_p, _p, _p, _l, _i, _i, _i, _p],
     "m2f_maxpool3s2_bwd": [_p, _p, _p, _l, _i, _i, _i, _p],
+    "m2f_stream_copy": [_p, _p, _l, _p],
+    "m2f_set_option": [ctypes.c_char_p, _l],
+    "m2f_get_option": [ctypes.c_char_p, _p],
     "m2f_transpose_f32": [_p, _l, _l, _p, _l, _l, _i, _i, _i, _p],
     "m2f_group_norm_workspace": [_i, _i, _i, _l, _p],
     "m2f_group_norm_fwd_f32": [_p, _p, _p, _i, _i, _i, _l, _f, _i, _p, _p, _p, _p, _l, _p],
@@ -124,3 +128,27 @@ def call(name: str, *args) -> None:
     if rc != 0:
         msg = lib.m2f_last_error().decode("utf-8", "replace")
         raise NativeError(f"{name} failed (code {rc}): {msg}")
+
+
+def set_option(name: str, value: int) -> None:
+    """m2f_set_option: a geometry / engine override (value < 0 restores the default)."""
+    call("m2f_set_option", name.encode(), int(value))
+
+
+def get_option(name: str) -> int:
+    v = ctypes.c_int64()
+    call("m2f_get_option", name.encode(), ctypes.byref(v))
+    return v.value
+
+
+@contextlib.contextmanager
+def options(**kw):
+    """Set native options for the duration of a with-block (tests sweep geometries this way)."""
+    old = {k: get_option(k) for k in kw}
+    try:
+        for k, v in kw.items():
+            set_option(k, v)
+        yield
+    finally:
+        for k, v in old.items():
+            set_option(k, v)

@@ -25,6 +25,7 @@ from .transformer_decoder import MultiScaleMaskedTransformerDecoder
 
 PIXEL_MEAN = (123.675, 116.280, 103.530)
 PIXEL_STD = (58.395, 57.120, 57.375)
+_CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}   # M2F_F32 / M2F_F16 / M2F_BF16
 
 
 class FrozenBNConv(nn.Module):
@@ -91,7 +92,7 @@ class _BiasAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, r, bias, nout):
         from . import _native
-        code = {torch.bfloat16: 2, torch.float32: 0}[x.dtype]
+        code = _CODE[x.dtype]
         cl = 0 if x.is_contiguous() else 1
         _native.call("m2f_bias_act_nchw", x.data_ptr(), r.data_ptr() if r is not None else None,
                      bias.data_ptr(), x.shape[0], x.shape[1], x.shape[2] * x.shape[3], code, cl,
@@ -110,12 +111,12 @@ class _BiasAct(torch.autograd.Function):
         gs = [g for g in grads if g is not None]
         if len(gs) == 1:
             g = torch.ops.aten.threshold_backward(gs[0], y, 0)  # ReLU's own backward: one pass
-        elif (y.is_contiguous() and len(gs) <= 4 and y.numel() % 8 == 0
-              and all(t.dtype == y.dtype and t.is_contiguous() for t in gs)):
+        elif (y.is_contiguous() and len(gs) <= 4 and y.numel() % 8 == 0 and y.data_ptr() % 16 == 0
+              and all(t.dtype == y.dtype and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in gs)):
             g = torch.empty_like(y, memory_format=torch.contiguous_format)
             ptrs = (ctypes.c_void_p * len(gs))(*[t.data_ptr() for t in gs])
             _native.call("m2f_relu_bwd_sum", ptrs, len(gs), y.data_ptr(), g.data_ptr(), y.numel(),
-                         {torch.bfloat16: 2, torch.float32: 0}[y.dtype], torch.cuda.current_stream(y.device).cuda_stream)
+                         _CODE[y.dtype], torch.cuda.current_stream(y.device).cuda_stream)
         else:
             g = torch.ops.aten.threshold_backward(sum(gs), y, 0)
         return g, (g if ctx.has_r else None), None, None
@@ -129,7 +130,7 @@ def bias_act(x, bias, residual=None, nout=1):
     ok = ((x.is_contiguous() and hw % 8 == 0 and (residual is None or residual.is_contiguous()))
           or (x.is_contiguous(memory_format=cl) and x.shape[1] % 8 == 0
               and (residual is None or residual.is_contiguous(memory_format=cl))))
-    if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and ok
+    if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and ok
             and (residual is None or residual.dtype == x.dtype)):
         return _BiasAct.apply(x, residual, bias.float().contiguous(), nout)
     y = x + bias.view(1, -1, 1, 1).to(x.dtype)
@@ -150,7 +151,7 @@ class _MaxPool3s2(torch.autograd.Function):
         y = torch.empty(N, C, OH, OW, device=x.device, dtype=x.dtype)
         win = torch.empty(N, C, OH, OW, device=x.device, dtype=torch.uint8)
         _native.call("m2f_maxpool3s2_fwd", x.data_ptr(), y.data_ptr(), win.data_ptr(), N * C, H, W,
-                     {torch.bfloat16: 2, torch.float32: 0}[x.dtype], torch.cuda.current_stream(x.device).cuda_stream)
+                     _CODE[x.dtype], torch.cuda.current_stream(x.device).cuda_stream)
         ctx.save_for_backward(win)
         ctx.in_shape = x.shape
         return y
@@ -163,13 +164,13 @@ class _MaxPool3s2(torch.autograd.Function):
         N, C, H, W = ctx.in_shape
         gx = torch.empty(ctx.in_shape, device=g.device, dtype=g.dtype)
         _native.call("m2f_maxpool3s2_bwd", g.data_ptr(), win.data_ptr(), gx.data_ptr(), N * C, H, W,
-                     {torch.bfloat16: 2, torch.float32: 0}[g.dtype], torch.cuda.current_stream(g.device).cuda_stream)
+                     _CODE[g.dtype], torch.cuda.current_stream(g.device).cuda_stream)
         return gx
 
 
 def max_pool_stem(x):
     """detectron2 BasicStem's ``F.max_pool2d(x, kernel_size=3, stride=2, padding=1)``."""
-    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float32) and x.dim() == 4 and x.is_contiguous():
+    if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and x.dim() == 4 and x.is_contiguous():
         return _MaxPool3s2.apply(x)
     return F.max_pool2d(x, kernel_size=3, stride=2, padding=1)
 
@@ -315,7 +316,13 @@ def surrogate_loss(out):
 
 
 def make_optimizer(model):
-    return torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=0.05, foreach=True)
+    """AdamW (lr 1e-4, weight decay 0.05; train_net.py:185-263).  On a GPU the fused single-kernel form: with
+    it GradScaler.step hands found_inf to the kernel instead of reading it on the host (torch's non-fused path
+    syncs on found_inf.item() every fp16 step).  Same update arithmetic."""
+    params = list(model.parameters())
+    if params and params[0].is_cuda:
+        return torch.optim.AdamW(params, lr=1e-4, weight_decay=0.05, fused=True)
+    return torch.optim.AdamW(params, lr=1e-4, weight_decay=0.05, foreach=True)
 
 
 def make_scaler(amp_dtype):

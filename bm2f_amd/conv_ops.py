@@ -11,7 +11,6 @@ else uses ``F.conv2d``.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 import torch.nn.functional as F
@@ -24,7 +23,7 @@ from . import _native
 #   "tn"     nine x3 TN GEMMs over zero-bordered pixel-row copies of dO and I (_wgrad3_tn): ~9.4 ms
 #   "miopen" fp32 igemm_wrw on its own NHWC transposes: ~10.1 ms
 #   "x3"     the implicit-GEMM kernel of csrc/conv_x3.hip on NCHW (channel-strided operands): ~14 ms
-WGRAD3 = os.environ.get("M2F_CONV3_WGRAD", "tn")
+WGRAD3 = "tn"   # 3x3 weight gradient: "tn" (x3 TN GEMMs per tap) or "miopen"; set by tools / tests
 
 
 def _stream(t):
@@ -73,7 +72,7 @@ class Conv2dX3(Function):
             dw = _wgrad3_tn(g, x)
             db = g.sum((0, 2, 3)) if want_b else None
         elif k == 3 and WGRAD3 == "miopen" and (ctx.needs_input_grad[1] or want_b):
-            # 3x3 weight gradient on the library (M2F_CONV3_WGRAD=miopen)
+            # 3x3 weight gradient on the library (WGRAD3 = "miopen")
             _, dw, db = torch.ops.aten.convolution_backward(
                 g, x, weight, [Co] if want_b else None, [1, 1], [1, 1], [1, 1], False, [0, 0], 1,
                 [False, bool(ctx.needs_input_grad[1]), want_b])

@@ -22,14 +22,13 @@ host round trips per step), and reads ``_iter`` / ``num_masks`` back with ``.ite
   intermediates);
 * ``_iter`` is mirrored on the host, ``num_masks`` stays a device scalar under torch.distributed, and
   LSAP failures (NaN / -inf / infeasible costs, which scipy raises for) are checked once per criterion call
-  (``M2F_LSAP_CHECK=0`` skips that one sync).
+  (``check_matching = False`` on the criterion skips that one sync).
 
 Matched indices are returned as int64 tensors on the masks' device (the reference returns CPU tensors;
 both index the same way).
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -243,7 +242,7 @@ class SetCriterionProjPair(nn.Module):
         self.register_buffer("empty_weight", empty_weight)
         self.register_buffer("_iter", torch.zeros([1]))
         self._iter_host = _IterMirror(self)
-        self.check_matching = os.environ.get("M2F_LSAP_CHECK", "1") != "0"
+        self.check_matching = True   # one host sync per call for scipy's ValueErrors; False skips it
         self._tg = self._tg_key = None
         self._status = []
         self._gathered = {}

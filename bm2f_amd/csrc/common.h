@@ -39,4 +39,17 @@ inline bool aligned(const void* p, size_t a) { return (reinterpret_cast<uintptr_
 
 inline unsigned ceil_div(int64_t a, int64_t b) { return static_cast<unsigned>((a + b - 1) / b); }
 
+// Explicit tuning options (m2f_set_option, include/bm2f.h): geometry and engine overrides for tests and
+// tools.  The library never reads the environment; an unset option means the built-in default.  Every
+// option changes the partition or the kernel variant only, never the arithmetic's result.
+enum Option : int {
+  kOptMsdaThreads, kOptMsdaTile, kOptMsdaTileW, kOptMsdaHalo, kOptMsdaWinRows, kOptMsdaBwdTiled, kOptMsdaFwdTiled,
+  kOptMattnDqAtomic, kOptGemmNtCfg, kOptX3TnNw, kOptX3TnBlocks, kOptX3NtCfg, kOptCount
+};
+int64_t option_raw(Option o);  // -1 when unset
+inline int option(Option o, int dflt) {
+  const int64_t v = option_raw(o);
+  return v < 0 ? dflt : static_cast<int>(v);
+}
+
 }  // namespace m2f

@@ -788,10 +788,7 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   const size_t lds = bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T));
   if (lds > 160 * 1024) return m2f::fail(M2F_EUNSUPPORTED, "%s: %zu B of LDS", fn, lds);
   // register dQ accumulation up to 128 queries (the decoders' 100 / 200-frame-shared cases use it)
-  static const bool reg_dq = [] {
-    const char* e = std::getenv("M2F_MATTN_DQ_ATOMIC");
-    return !(e && e[0] == '1');
-  }();
+  const bool reg_dq = m2f::option(m2f::kOptMattnDqAtomic, 0) != 1;
   auto kern = (reg_dq && Lqp <= 128) ? &mattn_bwd_kernel<T, 8> : &mattn_bwd_kernel<T, 0>;
   static bool attr_set[3][2] = {{false, false}, {false, false}, {false, false}};
   const int ai = std::is_same<T, float>::value ? 0 : (std::is_same<T, __bf16>::value ? 1 : 2);

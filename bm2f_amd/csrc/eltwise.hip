@@ -2,12 +2,14 @@
 //     y = max(x + r + bias[c], 0)
 // NCHW or channels_last (NHWC memory).  For the benchmark's R50 backbone (detectron2 FrozenBatchNorm2d folded into the convs: the conv runs
 // without bias and this op applies the BN shift, the residual and the ReLU in one HBM pass instead of
-// the library's broadcast bias add, a residual add and a ReLU).  bf16 or fp32, 16-byte vectors; needs
-// H*W % 8 == 0 (bf16) / % 4 (fp32) so a vector never straddles two channels.
+// the library's broadcast bias add, a residual add and a ReLU).  bf16, fp16 or fp32, 16-byte vectors; needs
+// H*W % 8 == 0 (bf16 / fp16) / % 4 (fp32) so a vector never straddles two channels.
 #include "bm2f.h"
 #include "common.h"
 
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 namespace {
 
@@ -31,7 +33,7 @@ __global__ void __launch_bounds__(256) bias_act_kernel(T* __restrict__ x, const 
   for (int e = 0; e < V; ++e) {
     float v = static_cast<float>(a.v[e]) + bias[NHWC ? c + e : c];
     if (r) v += static_cast<float>(rr.v[e]);
-    a.v[e] = static_cast<T>(fmaxf(v, 0.f));
+    a.v[e] = static_cast<T>(v > 0.f || v != v ? v : 0.f);   // torch's relu: NaN propagates
   }
   reinterpret_cast<VT*>(x)[i] = a;
 }
@@ -42,8 +44,9 @@ extern "C" int m2f_bias_act_nchw(void* x, const void* residual, const float* bia
                                  int dtype, int channels_last, void* stream) {
   const char* fn = "m2f_bias_act_nchw";
   if (!x || !bias || N < 0 || C <= 0 || HW <= 0) return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
-  const int V = dtype == M2F_BF16 ? 8 : 4;
-  if (dtype != M2F_BF16 && dtype != M2F_F32) return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  if (dtype != M2F_BF16 && dtype != M2F_F16 && dtype != M2F_F32)
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  const int V = dtype == M2F_F32 ? 4 : 8;
   if ((channels_last ? C % V : HW % V) || !m2f::aligned(x, 16) || (residual && !m2f::aligned(residual, 16)))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs %s %% %d == 0 and 16-byte aligned tensors", fn,
                      channels_last ? "C" : "H*W", V);
@@ -55,6 +58,8 @@ extern "C" int m2f_bias_act_nchw(void* x, const void* residual, const float* bia
                                                                       bias, nvec, C, static_cast<int>(HW / V))
   if (dtype == M2F_BF16) {
     if (channels_last) M2F_BA(__bf16, 8, true); else M2F_BA(__bf16, 8, false);
+  } else if (dtype == M2F_F16) {
+    if (channels_last) M2F_BA(_Float16, 8, true); else M2F_BA(_Float16, 8, false);
   } else {
     if (channels_last) M2F_BA(float, 4, true); else M2F_BA(float, 4, false);
   }
@@ -65,7 +70,7 @@ extern "C" int m2f_bias_act_nchw(void* x, const void* residual, const float* bia
 // ---------------------------------------------------------------------------------------------------
 // ReLU backward over the gradients of several consumers of one activation (a residual block's output feeds
 // the next block's first conv, its shortcut / identity path and, at a stage end, the pixel decoder):
-//     out = (g_0 + ... + g_{k-1}) * (y > 0)
+//     out = (g_0 + ... + g_{k-1}) masked where y <= 0 (torch's threshold_backward rule: a NaN y passes)
 // one pass (k + 1 reads, one write) instead of the autograd engine's k - 1 accumulating adds and a separate
 // threshold_backward.  The sum is formed in fp32 in consumer order and rounded once.
 // ---------------------------------------------------------------------------------------------------
@@ -95,7 +100,7 @@ __global__ void __launch_bounds__(256) relu_bwd_sum_kernel(ReluGrads gs, int ng,
   const VT yy = reinterpret_cast<const VT*>(y)[i];
   VT o;
 #pragma unroll
-  for (int e = 0; e < V; ++e) o.v[e] = static_cast<T>(static_cast<float>(yy.v[e]) > 0.f ? acc[e] : 0.f);
+  for (int e = 0; e < V; ++e) o.v[e] = static_cast<T>(!(static_cast<float>(yy.v[e]) <= 0.f) ? acc[e] : 0.f);  // threshold_backward: NaN y passes
   reinterpret_cast<VT*>(out)[i] = o;
 }
 
@@ -106,8 +111,9 @@ extern "C" int m2f_relu_bwd_sum(const void* const* grads, int ngrads, const void
   const char* fn = "m2f_relu_bwd_sum";
   if (!grads || ngrads < 1 || ngrads > kMaxReluGrads || !y || !out || n < 0)
     return m2f::fail(M2F_EINVAL, "%s: bad arguments (1 <= grads <= %d)", fn, kMaxReluGrads);
-  if (dtype != M2F_BF16 && dtype != M2F_F32) return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
-  const int V = dtype == M2F_BF16 ? 8 : 4;
+  if (dtype != M2F_BF16 && dtype != M2F_F16 && dtype != M2F_F32)
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  const int V = dtype == M2F_F32 ? 4 : 8;
   ReluGrads gs{};
   bool aligned = m2f::aligned(y, 16) && m2f::aligned(out, 16);
   for (int k = 0; k < ngrads; ++k) {
@@ -123,6 +129,9 @@ extern "C" int m2f_relu_bwd_sum(const void* const* grads, int ngrads, const void
   if (dtype == M2F_BF16)
     relu_bwd_sum_kernel<__bf16, 8><<<grid, 256, 0, st>>>(gs, ngrads, static_cast<const __bf16*>(y),
                                                          static_cast<__bf16*>(out), nvec);
+  else if (dtype == M2F_F16)
+    relu_bwd_sum_kernel<_Float16, 8><<<grid, 256, 0, st>>>(gs, ngrads, static_cast<const _Float16*>(y),
+                                                           static_cast<_Float16*>(out), nvec);
   else
     relu_bwd_sum_kernel<float, 4><<<grid, 256, 0, st>>>(gs, ngrads, static_cast<const float*>(y),
                                                         static_cast<float*>(out), nvec);
@@ -258,6 +267,9 @@ extern "C" int m2f_maxpool3s2_fwd(const void* x, void* y, uint8_t* window, int64
   if (dtype == M2F_BF16)
     maxpool3s2_fwd<__bf16><<<grid, 256, 0, st>>>(static_cast<const __bf16*>(x), static_cast<__bf16*>(y), window, H,
                                                  W, OH, OW, total);
+  else if (dtype == M2F_F16)
+    maxpool3s2_fwd<_Float16><<<grid, 256, 0, st>>>(static_cast<const _Float16*>(x), static_cast<_Float16*>(y), window,
+                                                   H, W, OH, OW, total);
   else if (dtype == M2F_F32)
     maxpool3s2_fwd<float><<<grid, 256, 0, st>>>(static_cast<const float*>(x), static_cast<float*>(y), window, H, W,
                                                 OH, OW, total);
@@ -275,12 +287,15 @@ extern "C" int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, voi
   const int64_t total = planes * H * W;
   if (total == 0) return m2f::ok();
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (W % 8 == 0 && m2f::aligned(grad_x, 16) && (dtype == M2F_BF16 || dtype == M2F_F32)) {
+  if (W % 8 == 0 && m2f::aligned(grad_x, 16) && (dtype == M2F_BF16 || dtype == M2F_F16 || dtype == M2F_F32)) {
     const int64_t total8 = total / 8;
     const unsigned g8 = m2f::ceil_div(total8, 256);
     if (dtype == M2F_BF16)
       maxpool3s2_bwd8<__bf16><<<g8, 256, 0, st>>>(static_cast<const __bf16*>(grad_y), window,
                                                    static_cast<__bf16*>(grad_x), H, W, OH, OW, total8);
+    else if (dtype == M2F_F16)
+      maxpool3s2_bwd8<_Float16><<<g8, 256, 0, st>>>(static_cast<const _Float16*>(grad_y), window,
+                                                     static_cast<_Float16*>(grad_x), H, W, OH, OW, total8);
     else
       maxpool3s2_bwd8<float><<<g8, 256, 0, st>>>(static_cast<const float*>(grad_y), window,
                                                   static_cast<float*>(grad_x), H, W, OH, OW, total8);
@@ -290,6 +305,9 @@ extern "C" int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, voi
   if (dtype == M2F_BF16)
     maxpool3s2_bwd<__bf16><<<grid, 256, 0, st>>>(static_cast<const __bf16*>(grad_y), window,
                                                  static_cast<__bf16*>(grad_x), H, W, OH, OW, total);
+  else if (dtype == M2F_F16)
+    maxpool3s2_bwd<_Float16><<<grid, 256, 0, st>>>(static_cast<const _Float16*>(grad_y), window,
+                                                   static_cast<_Float16*>(grad_x), H, W, OH, OW, total);
   else if (dtype == M2F_F32)
     maxpool3s2_bwd<float><<<grid, 256, 0, st>>>(static_cast<const float*>(grad_y), window,
                                                 static_cast<float*>(grad_x), H, W, OH, OW, total);
@@ -338,5 +356,46 @@ extern "C" int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, 
   if (B > 65535) return m2f::fail(M2F_EUNSUPPORTED, "%s: batch %d > 65535", fn, B);
   const dim3 grid((Q + 63) / 64, (R + 63) / 64, B);
   transpose_f32<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(in, in_bs, in_ld, out, out_bs, out_ld, R, Q);
+  return m2f::check_launch(fn);
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Achievable-HBM probe ("measure achievable peaks with a stream kernel"): out = in over
+// n16 16-byte vectors, grid-stride with a fixed grid of 8 workgroups per CU (256 CUs), nontemporal
+// loads and stores so neither pass is served from the 256 MB MALL.  Bytes moved = 32 * n16.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(256) stream_copy_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                         int64_t n16) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  for (; i + 3 * stride < n16; i += 4 * stride) {  // four independent 16-byte loads in flight per lane
+    const u32x4 a = __builtin_nontemporal_load(in + i);
+    const u32x4 b = __builtin_nontemporal_load(in + i + stride);
+    const u32x4 c = __builtin_nontemporal_load(in + i + 2 * stride);
+    const u32x4 d = __builtin_nontemporal_load(in + i + 3 * stride);
+    __builtin_nontemporal_store(a, out + i);
+    __builtin_nontemporal_store(b, out + i + stride);
+    __builtin_nontemporal_store(c, out + i + 2 * stride);
+    __builtin_nontemporal_store(d, out + i + 3 * stride);
+  }
+  for (; i < n16; i += stride) __builtin_nontemporal_store(__builtin_nontemporal_load(in + i), out + i);
+}
+
+}  // namespace
+
+extern "C" int m2f_stream_copy(const void* in, void* out, int64_t nbytes, void* stream) {
+  const char* fn = "m2f_stream_copy";
+  if (!in || !out || nbytes < 0) return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  if (nbytes % 16 || !m2f::aligned(in, 16) || !m2f::aligned(out, 16))
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs 16-byte aligned buffers and nbytes %% 16 == 0", fn);
+  const int64_t n16 = nbytes / 16;
+  if (n16 == 0) return m2f::ok();
+  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(2048, m2f::ceil_div(n16, 256)));
+  stream_copy_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(static_cast<const u32x4*>(in),
+                                                                          static_cast<u32x4*>(out), n16);
   return m2f::check_launch(fn);
 }

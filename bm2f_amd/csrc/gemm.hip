@@ -395,7 +395,7 @@ extern "C" int m2f_gemm_f32_nt(const float* A, int64_t lda, const float* B, int6
   const int epi = (bias ? kBias : 0) | (relu ? kRelu : 0) | (mask ? kMask : 0);
   // tile choice: N a multiple of 96 but not 128 (the 288-wide sampling projection) gets 96-wide blocks
   int cfg = (N % 128 != 0 && N % 96 == 0) ? 4 : 0;
-  if (const char* e = std::getenv("M2F_GEMM_NT_CFG")) cfg = std::atoi(e);
+  cfg = m2f::option(m2f::kOptGemmNtCfg, cfg);
   switch (cfg) {
     case 0: return launch_nt<128, 128, 2, 2>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);
     case 4: return launch_nt<128, 96, 4, 1>(epi, A, lda, B, ldb, bias, mask, ldm, C, ldc, M, N, K, st);

@@ -563,15 +563,12 @@ TnPlan tn_plan(int M, int N1, int N2) {
   // -9 % at 1024 x 256 (tools/gemm_x3_bench.py, r2ah); else 4 (8 waves lose at 288 rows: 0.60 vs 0.49 ms);
   // 3 (96-row tiles, exact for 288) measured slower: fewer threads share the B staging
   p.nw = p.n1 % 256 == 0 ? 8 : 4;
-  if (const char* e = std::getenv("M2F_GEMM_X3_TN_NW")) {
-    const int v = std::atoi(e);
-    p.nw = v == 3 ? 3 : v == 8 ? 8 : 4;
-  }
+  if (const int v = m2f::option(m2f::kOptX3TnNw, 0)) p.nw = v == 3 ? 3 : v == 8 ? 8 : 4;
   p.tiles = ((p.n1 + 32 * p.nw - 1) / (32 * p.nw)) * ((p.n2 + 255) / 256);
   // ~512 blocks (2 per CU); 768 when the last row tile is partial (the 288-wide sampling projection:
   // 0.52 vs 0.65 ms at M = 344064; full tiles measured best at 512, tools/gemm_x3_bench.py)
   int target = (p.n1 % (32 * p.nw) ? 768 : 512) / (p.nw >= 8 ? 2 : 1);   // 8 waves: one block per CU
-  if (const char* e = std::getenv("M2F_GEMM_X3_TN_BLOCKS")) target = std::max(1, std::atoi(e));
+  target = std::max(1, m2f::option(m2f::kOptX3TnBlocks, target));
   int splits = (target + p.tiles - 1) / p.tiles;
   const int max_splits = (M + 8 * kBK - 1) / (8 * kBK);       // >= 8 chunks per block
   if (splits > max_splits) splits = max_splits;
@@ -626,7 +623,7 @@ extern "C" int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B
   // of 8 waves (256 rows share one B chunk: 0.285 vs 0.321 ms at K = N = 256, 0.913 vs 0.949 at K = 1024,
   // equal at N = 1024; tools/gemm_x3_bench.py, r2af)
   int cfg = (N % 128 != 0 && N % 96 == 0) ? 1 : 3;
-  if (const char* e = std::getenv("M2F_GEMM_X3_NT_CFG")) cfg = std::atoi(e);
+  cfg = m2f::option(m2f::kOptX3NtCfg, cfg);
   switch (cfg) {
     case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
     case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);

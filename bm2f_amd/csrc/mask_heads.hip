@@ -276,29 +276,34 @@ __global__ void __launch_bounds__(256) mask_row_fix_kernel(uint32_t* __restrict_
 
 // ---- backward --------------------------------------------------------------------------------------------
 // d embed = G F^T per head (G = d masks (B, Q, N), F = features (B, C, N), both N-contiguous).  Split over
-// N: grid (splits, B); each block computes the whole (QT*32) x 256 partial of its N range into
-// part[b][split][q][c] (fp32, q < Q), summed in a fixed order by mask_de_reduce_kernel.  4 waves, wave w:
-// channels 64 w .. 64 w + 63 (two 32-tiles) x all query tiles.  Per 32-deep k step the block's G slab
-// (QT*32 rows x 32) is staged once in LDS (rows padded to 80 B: conflict-free 16-byte A reads) and shared
-// by the waves; each wave's F fragments (its own channels) load straight from global memory.  Two steps of
-// global loads in flight in registers, LDS double-buffered, one barrier per step.  HBM-bound.
+// N: grid (splits, B); each block computes the whole (Q padded to 32) x 256 partial of its N range into
+// part[b][split][q][c] (fp32, q < Q), summed in a fixed order by mask_de_reduce_kernel.  QH groups of 4 waves
+// (QH = 2 above 128 queries: config 4's Q = 200, mask2former_transformer_decoder.py:442); wave w: channels
+// 64 (w % 4) .. + 63 (two 32-tiles) x query tiles QT (w / 4) .. + QT - 1, so no wave holds more than four
+// query tiles of accumulators (128 VGPRs).  Per 32-deep k step the block's G slab (QH*QT*32 rows x 32) is
+// staged once in LDS (rows padded to 80 B: conflict-free 16-byte A reads) and shared by the waves; each
+// wave's F fragments (its own channels) load straight from global memory (the second query group's loads
+// of the same F rows hit the CU's L1/L2).  Two steps of global loads in flight in registers, LDS
+// double-buffered, one barrier per step.  HBM-bound.
 constexpr int kDeThreads = 256, kDeK = 32, kDePitch = kDeK + 8;
 
-template <typename T, int QT>
-__global__ void __launch_bounds__(kDeThreads, 2) mask_de_kernel(const T* __restrict__ G, const T* __restrict__ F,
-                                                               int Q, int64_t N, int64_t ks, int splits,
-                                                               float* __restrict__ part) {
+template <typename T, int QT, int QH>
+__global__ void __launch_bounds__(kDeThreads * QH, 2 / QH) mask_de_kernel(const T* __restrict__ G,
+                                                                          const T* __restrict__ F, int Q, int64_t N,
+                                                                          int64_t ks, int splits,
+                                                                          float* __restrict__ part) {
   using E = MhElt<T>;
-  constexpr int C = 256, QP = 32 * QT;
+  constexpr int C = 256, QP = 32 * QT * QH, NT = kDeThreads * QH;
   constexpr int GP = QP * (kDeK / 8);                 // 16-byte G pieces per step
-  constexpr int GPT = (GP + kDeThreads - 1) / kDeThreads;
+  constexpr int GPT = (GP + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) T sg[2][QP * kDePitch];
   const int s = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
+  const int wc = w & 3, q0 = 32 * QT * (w >> 2);      // channel group, first query of this wave's tiles
   const int64_t k0 = s * ks, k1 = min(N, k0 + ks);
   const int nsteps = static_cast<int>((k1 - k0 + kDeK - 1) / kDeK);
   const T* gb = G + static_cast<int64_t>(b) * Q * N;
-  const T* f = F + static_cast<int64_t>(b) * C * N + static_cast<int64_t>(64 * w + li) * N + lh * 8;
+  const T* f = F + static_cast<int64_t>(b) * C * N + static_cast<int64_t>(64 * wc + li) * N + lh * 8;
   struct Stage {
     s8 g[GPT];
     s8 f[2][2];   // [c-tile][k16 half]
@@ -308,9 +313,9 @@ __global__ void __launch_bounds__(kDeThreads, 2) mask_de_kernel(const T* __restr
     const int64_t kb = k0 + static_cast<int64_t>(step) * kDeK;
 #pragma unroll
     for (int u = 0; u < GPT; ++u) {
-      const int p = tid + u * kDeThreads, row = p >> 2, kp = (p & 3) * 8;
+      const int p = tid + u * NT, row = p >> 2, kp = (p & 3) * 8;
       st.g[u] = s8{0, 0, 0, 0, 0, 0, 0, 0};
-      if ((GP % kDeThreads == 0 || p < GP) && row < Q && kb + kp < k1)
+      if ((GP % NT == 0 || p < GP) && row < Q && kb + kp < k1)
         st.g[u] = *reinterpret_cast<const s8*>(gb + static_cast<int64_t>(row) * N + kb + kp);
     }
 #pragma unroll
@@ -324,8 +329,8 @@ __global__ void __launch_bounds__(kDeThreads, 2) mask_de_kernel(const T* __restr
   auto gstore = [&](int buf, const Stage& st) {
 #pragma unroll
     for (int u = 0; u < GPT; ++u) {
-      const int p = tid + u * kDeThreads;
-      if (GP % kDeThreads == 0 || p < GP) *reinterpret_cast<s8*>(&sg[buf][(p >> 2) * kDePitch + (p & 3) * 8]) = st.g[u];
+      const int p = tid + u * NT;
+      if (GP % NT == 0 || p < GP) *reinterpret_cast<s8*>(&sg[buf][(p >> 2) * kDePitch + (p & 3) * 8]) = st.g[u];
     }
   };
   f16v acc[QT][2];
@@ -341,7 +346,7 @@ __global__ void __launch_bounds__(kDeThreads, 2) mask_de_kernel(const T* __restr
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) {
-        const s8 a = *reinterpret_cast<const s8*>(base + (32 * qt + li) * kDePitch + 16 * h + 8 * lh);
+        const s8 a = *reinterpret_cast<const s8*>(base + (q0 + 32 * qt + li) * kDePitch + 16 * h + 8 * lh);
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[qt][j] = E::mma(a, st.f[j][h], acc[qt][j]);
       }
@@ -364,14 +369,14 @@ __global__ void __launch_bounds__(kDeThreads, 2) mask_de_kernel(const T* __restr
     if (t + 1 < nsteps) stepf(t + 1, s1, s0);
   }
   // C map of 32x32x16: lane column li (c), rows (e & 3) + 8 (e >> 2) + 4 lh (q)
-  float* out = part + (static_cast<int64_t>(b) * splits + s) * Q * C + 64 * w + li;
+  float* out = part + (static_cast<int64_t>(b) * splits + s) * Q * C + 64 * wc + li;
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int q = 32 * qt + (e & 3) + 8 * (e >> 2) + 4 * lh;
+        const int q = q0 + 32 * qt + (e & 3) + 8 * (e >> 2) + 4 * lh;
         if (q < Q) out[static_cast<int64_t>(q) * C + 32 * j] = acc[qt][j][e];
       }
 }
@@ -571,11 +576,14 @@ int launch_de(const void* G, const void* F, int B, int Q, int64_t N, float* part
   const dim3 grid(splits, B);
   const T* g = static_cast<const T*>(G);
   const T* f = static_cast<const T*>(F);
+  // up to 128 queries: one group of 4 waves holds every query tile; 129..256: two groups of up to 4 tiles
   switch ((Q + 31) / 32) {
-#define M2F_DE(N_) case N_: mask_de_kernel<T, N_><<<grid, kDeThreads, 0, st>>>(g, f, Q, N, ks, splits, part); break;
-    M2F_DE(1) M2F_DE(2) M2F_DE(3) M2F_DE(4)
+#define M2F_DE(N_, QT, QH) \
+  case N_: mask_de_kernel<T, QT, QH><<<grid, kDeThreads * QH, 0, st>>>(g, f, Q, N, ks, splits, part); break;
+    M2F_DE(1, 1, 1) M2F_DE(2, 2, 1) M2F_DE(3, 3, 1) M2F_DE(4, 4, 1)
+    M2F_DE(5, 3, 2) M2F_DE(6, 3, 2) M2F_DE(7, 4, 2) M2F_DE(8, 4, 2)
 #undef M2F_DE
-    default: return m2f::fail(M2F_EUNSUPPORTED, "m2f_mask_heads_bwd_embed: %d queries (at most 128)", Q);
+    default: return m2f::fail(M2F_EUNSUPPORTED, "m2f_mask_heads_bwd_embed: %d queries (at most 256)", Q);
   }
   const int64_t per_b = static_cast<int64_t>(Q) * 256, total = per_b * B;
   mask_de_reduce_kernel<T><<<m2f::ceil_div(total, 256), 256, 0, st>>>(part, splits, per_b, total, static_cast<T*>(de));
@@ -597,8 +605,8 @@ extern "C" int m2f_mask_heads_bwd_embed(int dtype, const void* grad_masks, const
   const char* fn = "m2f_mask_heads_bwd_embed";
   if (!grad_masks || !feats || !grad_embed || !workspace) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
   if (dtype != M2F_BF16 && dtype != M2F_F16) return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
-  if (channels != 256 || n % 16 || num_queries <= 0 || num_queries > 128 || batch <= 0)
-    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs 256 channels, n %% 16 == 0, 1..128 queries", fn);
+  if (channels != 256 || n % 16 || num_queries <= 0 || num_queries > 256 || batch <= 0)
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs 256 channels, n %% 16 == 0, 1..256 queries", fn);
   if (!m2f::aligned(grad_masks, 16) || !m2f::aligned(feats, 16)) return m2f::fail(M2F_EINVAL, "%s: alignment", fn);
   int64_t need = 0;
   m2f_mask_heads_bwd_workspace(batch, num_queries, n, &need);

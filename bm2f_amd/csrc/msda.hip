@@ -21,8 +21,10 @@
 #include "msda_device.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace m2f {
@@ -34,6 +36,40 @@ std::string& last_error() {
 
 extern "C" const char* m2f_last_error(void) { return m2f::last_error().c_str(); }
 extern "C" int m2f_abi_version(void) { return 1; }
+
+namespace {
+constexpr const char* kOptionNames[m2f::kOptCount] = {
+    "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
+    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg"};
+std::atomic<int64_t> g_options[m2f::kOptCount] = {};
+struct OptionInit {
+  OptionInit() {
+    for (auto& o : g_options) o.store(-1);
+  }
+} g_option_init;
+
+int option_index(const char* name) {
+  for (int i = 0; name && i < m2f::kOptCount; ++i)
+    if (std::strcmp(name, kOptionNames[i]) == 0) return i;
+  return -1;
+}
+}  // namespace
+
+int64_t m2f::option_raw(Option o) { return g_options[o].load(std::memory_order_relaxed); }
+
+extern "C" int m2f_set_option(const char* name, int64_t value) {
+  const int i = option_index(name);
+  if (i < 0) return m2f::fail(M2F_EINVAL, "m2f_set_option: unknown option '%s'", name ? name : "(null)");
+  g_options[i].store(value < 0 ? -1 : value);
+  return m2f::ok();
+}
+
+extern "C" int m2f_get_option(const char* name, int64_t* value) {
+  const int i = option_index(name);
+  if (i < 0 || !value) return m2f::fail(M2F_EINVAL, "m2f_get_option: unknown option '%s'", name ? name : "(null)");
+  *value = g_options[i].load();
+  return m2f::ok();
+}
 
 namespace {
 
@@ -1069,16 +1105,12 @@ int fwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
   return m2f::check_launch(fn);
 }
 
-int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return (v && *v) ? atoi(v) : dflt;
-}
-
 // Tile geometry for the tiled backward; false when the configuration does not qualify (then the
 // caller uses the untiled kernels).  Lq == S: the queries are the flattened pyramid.
-//   M2F_MSDA_THREADS (512): workgroup size, 512 (two workgroups per CU) or 1024 (one);
-//   M2F_MSDA_TILE / M2F_MSDA_TILE_W (12 / 12 at 512 threads, 16 / 16 at 1024): tile on the finest level;
-//   M2F_MSDA_HALO (8): window halo;  M2F_MSDA_WIN_ROWS (cells per workgroup; the halo shrinks until the
+// Options (m2f_set_option):
+//   msda_threads (512): workgroup size, 512 (two workgroups per CU) or 1024 (one);
+//   msda_tile / msda_tile_w (12 / 12 at 512 threads, 16 / 16 at 1024): tile on the finest level;
+//   msda_halo (8): window halo;  msda_win_rows (cells per workgroup; the halo shrinks until the
 //   window fits).  Geometry only: every setting computes the same gradients (tests sweep them).
 bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds, int& threads) {
   if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
@@ -1091,19 +1123,22 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     geo.H[l] = static_cast<int>(host_shapes[2 * l]);
     geo.W[l] = static_cast<int>(host_shapes[2 * l + 1]);
     if (geo.H[l] <= 0 || geo.W[l] <= 0) return false;
+    // phase 2 forms corner offsets (y0 * W + x0) * rs with 24-bit multiplies (__umul24): a level of 2^24 or
+    // more pixels would silently wrap, so such shapes take the untiled kernels
+    if (static_cast<int64_t>(geo.H[l]) * geo.W[l] >= (int64_t{1} << 24)) return false;
     geo.start[l] = static_cast<int>(total);
     total += static_cast<int64_t>(geo.H[l]) * geo.W[l];
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   if (total != d.S) return false;
-  threads = env_int("M2F_MSDA_THREADS", 512) >= 1024 ? 1024 : 512;
+  threads = m2f::option(m2f::kOptMsdaThreads, 512) >= 1024 ? 1024 : 512;
   // 512 threads: 12x12 tiles (78 KB of LDS, two workgroups per CU) measured 2.44 ms at config 2 against 2.45
   // (8x16), 2.52 (16x8) and 2.65 for 1024 threads with 16x16 tiles (tools/msda_bench.py, r2k)
-  const int tile_h = std::max(1, env_int("M2F_MSDA_TILE", threads == 1024 ? 16 : 12));
-  const int tile_w = std::max(1, env_int("M2F_MSDA_TILE_W", tile_h));
+  const int tile_h = std::max(1, m2f::option(m2f::kOptMsdaTile, threads == 1024 ? 16 : 12));
+  const int tile_w = std::max(1, m2f::option(m2f::kOptMsdaTileW, tile_h));
   geo.nty = (geo.H[fi] + tile_h - 1) / tile_h;
   geo.ntx = (geo.W[fi] + tile_w - 1) / tile_w;
-  geo.max_halo = std::max(0, env_int("M2F_MSDA_HALO", 8));
+  geo.max_halo = std::max(0, m2f::option(m2f::kOptMsdaHalo, 8));
   // cells of the largest window any workgroup can choose (tile + 2 halo + 1 per axis, clipped to the level),
   // unless a smaller budget is asked for; it must hold every level's share of one tile at halo 0 (tiles
   // span at most ceil(n / nt) pixels per axis, tile_lo) plus the extra cell row / column
@@ -1114,7 +1149,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     full += (std::min(geo.H[l], th + 2 * geo.max_halo) + 1) * (std::min(geo.W[l], tw + 2 * geo.max_halo) + 1);
     qt += th * tw;
   }
-  geo.max_rows = env_int("M2F_MSDA_WIN_ROWS", full);
+  geo.max_rows = m2f::option(m2f::kOptMsdaWinRows, full);
   geo.max_qt = qt;
   const int lp = d.L * d.P;
   if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff) return false;
@@ -1163,7 +1198,7 @@ void launch_tiled_levels(const float* value, const float* loc, const float* attn
 
 bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,
                       const int64_t* host_shapes, float* gv, float* gl, float* ga, hipStream_t st) {
-  if (env_int("M2F_MSDA_BWD_TILED", 1) == 0) return false;
+  if (m2f::option(m2f::kOptMsdaBwdTiled, 1) == 0) return false;
   TileGeom geo;
   size_t lds;
   int threads;
@@ -1301,11 +1336,7 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
   hipStream_t st = static_cast<hipStream_t>(stream);
   // value and out hold N * Lq(=S) * M * 32 elements; 32-bit offsets when those fit
   const bool off32 = static_cast<int64_t>(d.N) * std::max(d.S, d.Lq) * d.M * d.D < (int64_t{1} << 31);
-  static const bool tiled_env = [] {
-    const char* e = std::getenv("M2F_MSDA_FWD_TILED");
-    return !(e && e[0] == '0');
-  }();
-  if (tiled_env && d.Lq == d.S) {
+  if (m2f::option(m2f::kOptMsdaFwdTiled, 1) != 0 && d.Lq == d.S) {
     int64_t T = 0;
     for (int l = 0; l < d.L; ++l) T += static_cast<int64_t>((geo.H[l] + 3) / 4) * ((geo.W[l] + 7) / 8);
     const int64_t nb = T * d.M * d.N;

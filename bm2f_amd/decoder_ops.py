@@ -221,7 +221,7 @@ def _bwd_fusable(f, g) -> bool:
     """Shapes / dtypes of the mask-head backward kernels (csrc/mask_heads.hip)."""
     B, C, N = f.shape
     return (f.is_cuda and f.dtype in (torch.bfloat16, torch.float16) and g.dtype == f.dtype and C == 256
-            and N % 16 == 0 and g.shape[1] <= 128 and f.is_contiguous() and g.is_contiguous()
+            and N % 16 == 0 and g.shape[1] <= 256 and f.is_contiguous() and g.is_contiguous()
             and f.data_ptr() % 16 == 0 and g.data_ptr() % 16 == 0)
 
 
@@ -363,10 +363,12 @@ class MaskFeatureFold:
     def __call__(self, embed):
         return _FoldedMaskEinsum.apply(embed, self.token, self)
 
-    def fused_ok(self, num_queries, size=None) -> bool:
+    def fused_ok(self, num_queries, size=None, channels=None) -> bool:
         """Shapes / dtypes the mask-heads kernel takes (m2f_mask_heads_fwd's constraints)."""
         f = self.feats_lp
         T, H, W = self.frames_hw
+        if channels is not None and channels != f.shape[1]:
+            return False     # the einsum path raises the reference's shape error
         if not (f.is_cuda and f.dtype in (torch.bfloat16, torch.float16) and f.is_contiguous()
                 and f.shape[1] % 32 == 0 and W % 8 == 0 and num_queries <= 256 and f.data_ptr() % 16 == 0):
             return False
@@ -381,7 +383,10 @@ def mask_heads(fold: MaskFeatureFold, embed: torch.Tensor, size=None):
     """One prediction head's masks and (``size`` given) the next cross-attention's bitmask:
     ``fold(embed)`` + :func:`attn_mask_bits` (reference :442-449 and :400), in one kernel where the shapes
     allow (the pyramid's exact 2/4/8x reductions in bf16 / fp16), else as those two steps."""
-    if fold.fused_ok(embed.shape[1], size):
+    if embed.dim() != 3 or embed.shape[2] != fold.feats_lp.shape[1]:
+        raise RuntimeError(f"einsum bqc,bchw->bqhw: embed {tuple(embed.shape)} does not match "
+                           f"{fold.feats_lp.shape[1]} feature channels")
+    if fold.fused_ok(embed.shape[1], size, embed.shape[2]):
         out, bits = _FoldedMaskHeads.apply(embed, fold.token, fold, size)
         return out, (bits if size is not None else None)
     out = fold(embed)

@@ -22,7 +22,6 @@ every fused-epilogue product and the 256-wide products run on libbm2f.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 import torch.nn.functional as F
@@ -34,7 +33,7 @@ from . import _native
 
 # Which fp32 GEMM engine the encoder linears use: "x3" (bf16 MFMA on exact three-way operand splits,
 # csrc/gemm_x3.hip, fp32-accurate at 2.7x the f32 MFMA rate) or "exact" (f32-input MFMA, csrc/gemm.hip).
-ENGINE = os.environ.get("M2F_F32_GEMM", "x3")
+ENGINE = "x3"   # fp32 GEMM engine: "x3" (split-bf16 MFMA), "exact" (f32 MFMA) or the library; set by tools
 
 
 def _engine(engine):

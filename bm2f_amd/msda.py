@@ -17,7 +17,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 import warnings
 from typing import Optional, Sequence, Tuple
 
@@ -84,9 +83,33 @@ def _check_level_starts(level_start_index: torch.Tensor, shapes) -> None:
     setattr(level_start_index, _LSI_ATTR, want)   # checked once per tensor
 
 
-def _host_shapes(spatial_shapes: torch.Tensor, level_start_index: torch.Tensor = None):
+def _derive_host_shapes(spatial_shapes: torch.Tensor, level_start_index: torch.Tensor):
+    """Host shapes for a device ``spatial_shapes`` that arrived untagged -- the reference's unchanged
+    ``MSDeformAttn.forward`` -> ``MSDeformAttnFunction.apply`` (ops/modules/ms_deform_attn.py:116-117) passes
+    the encoder's device tensor as is.  One device->host copy per tensor object, cached on it (the encoder
+    hands the same tensor to all six layers, msdeformattn.py:75-83, and the backward restores the tag), so
+    the op-level drop-in takes the tiled backward too.  Returns None (untiled kernels, same results) when
+    the tensor cannot be read back here: during graph capture, or when ``level_start_index`` is not the
+    prefix sum the tiled kernels assume."""
+    if (spatial_shapes.dim() != 2 or spatial_shapes.shape[1] != 2 or spatial_shapes.dtype != torch.int64
+            or level_start_index is None or spatial_shapes.device.type != "cuda"
+            or torch.cuda.is_current_stream_capturing()):
+        return None
+    pair = torch.cat((spatial_shapes.reshape(-1), level_start_index.reshape(-1))).cpu().tolist()
+    L = spatial_shapes.shape[0]
+    shapes = tuple((int(pair[2 * i]), int(pair[2 * i + 1])) for i in range(L))
+    if tuple(int(v) for v in pair[2 * L:]) != _prefix_starts(shapes):
+        return None
+    setattr(spatial_shapes, _HOST_ATTR, shapes)
+    setattr(level_start_index, _LSI_ATTR, _prefix_starts(shapes))
+    return shapes
+
+
+def _host_shapes(spatial_shapes: torch.Tensor, level_start_index: torch.Tensor = None, derive: bool = False):
     hs = getattr(spatial_shapes, _HOST_ATTR, None)
-    if hs is not None and level_start_index is not None:
+    if hs is None:
+        return _derive_host_shapes(spatial_shapes, level_start_index) if derive else None
+    if level_start_index is not None:
         _check_level_starts(level_start_index, hs)
     return hs
 
@@ -182,8 +205,9 @@ class MSDeformAttnFunction(Function):
     def forward(ctx, value, value_spatial_shapes, value_level_start_index, sampling_locations, attention_weights,
                 im2col_step):
         ctx.im2col_step = im2col_step
-        ctx.host_shapes = _host_shapes(value_spatial_shapes, value_level_start_index)
-        output =ms_deform_attn_forward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
+        # derive=True: an untagged device spatial_shapes (the reference module's call) is read back once
+        ctx.host_shapes = _host_shapes(value_spatial_shapes, value_level_start_index, derive=True)
+        output = ms_deform_attn_forward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
                                         attention_weights, ctx.im2col_step)
         ctx.save_for_backward(value, value_spatial_shapes, value_level_start_index, sampling_locations,
                               attention_weights)
@@ -245,8 +269,11 @@ class MSDeformAttnFusedFunction(Function):
         return grad_value, grad_proj, None, None, None
 
 
+FUSED = True   # the encoder's fused MSDA front end; False: the reference's op chain (tests, A/B)
+
+
 def _fused_enabled():
-    return os.environ.get("M2F_MSDA_FUSED", "1") != "0"
+    return FUSED
 
 
 def _is_power_of_2(n):

@@ -13,7 +13,6 @@ alter results:
 from __future__ import annotations
 
 import copy
-import os
 from typing import Callable, Dict, List, Optional, Union
 
 import numpy as np
@@ -30,8 +29,8 @@ from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill,
 
 
 # encoder layers hand their residual inputs through the projection / FFN autograd nodes so gradient sums
-# ride in GEMM epilogues (M2F_RESIDUAL_FUSED=0: plain autograd sums, for A/B measurements)
-RESIDUAL_FUSED = os.environ.get("M2F_RESIDUAL_FUSED", "1") != "0"
+# ride in GEMM epilogues (False: plain autograd sums, for A/B measurements and tests)
+RESIDUAL_FUSED = True
 
 
 def _get_clones(module, N):

@@ -270,28 +270,42 @@ int m2f_conv_f32x3(const float* I, const float* W, const float* bias, float* O, 
 int m2f_conv_f32x3_wgrad(const float* grad_out, const float* I, float* dW_tck, float* dbias, int N, int Ci, int Co,
                          int H, int Wd, int ksize, void* workspace, int64_t workspace_bytes, void* stream);
 
-/* Fused per-channel bias (+ residual) + ReLU in place over an NCHW activation (dtype M2F_BF16 or
- * M2F_F32), memory NCHW or (channels_last != 0) NHWC: x = max(x + residual + bias[c], 0).  The
+/* Fused per-channel bias (+ residual) + ReLU in place over an NCHW activation (dtype M2F_BF16, M2F_F16
+ * or M2F_F32), memory NCHW or (channels_last != 0) NHWC: x = max(x + residual + bias[c], 0).  The
  * benchmark backbone's FrozenBN shift + shortcut + ReLU in one pass (not on the reference's hot path).
- * H*W (NCHW) or C (NHWC) % 8 (bf16) / % 4 (fp32), 16-byte aligned. */
+ * H*W (NCHW) or C (NHWC) % 8 (bf16 / fp16) / % 4 (fp32), 16-byte aligned. */
 int m2f_bias_act_nchw(void* x, const void* residual, const float* bias, int64_t N, int C, int64_t HW, int dtype,
                       int channels_last, void* stream);
 
 /* ReLU backward over the summed gradients of up to 4 consumers of one activation y (the benchmark
- * backbone's block outputs): out = (grads[0] + ... + grads[ngrads-1]) * (y > 0), summed in fp32 in the given
- * order and rounded once; bf16 (M2F_BF16) or fp32, contiguous, n % 8 (bf16) / % 4 (fp32), 16-byte aligned.
+ * backbone's block outputs): out = (grads[0] + ... + grads[ngrads-1]) where !(y <= 0), else 0 (torch's
+ * threshold_backward rule: a NaN y passes the gradient), summed in fp32 in the given order and rounded once;
+ * bf16, fp16 or fp32, contiguous, n % 8 (16-bit) / % 4 (fp32), 16-byte aligned (else M2F_EUNSUPPORTED).
  * Replaces the autograd engine's accumulating adds plus torch's threshold_backward (one pass, k + 1 reads). */
 int m2f_relu_bwd_sum(const void* const* grads, int ngrads, const void* y, void* out, int64_t n, int dtype,
                      void* stream);
 
 /* The benchmark backbone's stem max pool (kernel 3, stride 2, padding 1; detectron2 BasicStem; not on the
- * reference's hot path), NCHW, dtype M2F_BF16 or M2F_F32, planes = N*C, output (H-1)/2+1 x (W-1)/2+1.
+ * reference's hot path), NCHW, dtype M2F_BF16, M2F_F16 or M2F_F32, planes = N*C, output (H-1)/2+1 x (W-1)/2+1.
  * m2f_maxpool3s2_fwd: torch's max_pool2d_with_indices rule (first maximum in window order, NaN wins); the
  *   winner's window position (0..8) goes to window[planes][OH][OW] (1 byte instead of an int64 index).
  * m2f_maxpool3s2_bwd: grad_x = each input pixel's sum over the windows it won (torch's order, fp32). */
 int m2f_maxpool3s2_fwd(const void* x, void* y, uint8_t* window, int64_t planes, int H, int W, int dtype, void* stream);
 int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, int64_t planes, int H, int W, int dtype,
                        void* stream);
+
+/* Explicit tuning options: geometry / engine overrides for tests and tools (the library never reads the
+ * environment).  value < 0 restores the built-in default.  Names: msda_threads, msda_tile, msda_tile_w,
+ * msda_halo, msda_win_rows, msda_bwd_tiled, msda_fwd_tiled (MSDA partitions), mattn_dq_atomic (masked
+ * attention dQ variant), gemm_nt_cfg, x3_tn_nw, x3_tn_blocks, x3_nt_cfg (GEMM tilings).  Every option
+ * changes the partition or kernel variant only; results are the same.  Process-wide; not synchronised
+ * with launches in flight on other threads.  Unknown names return M2F_EINVAL. */
+int m2f_set_option(const char* name, int64_t value);
+int m2f_get_option(const char* name, int64_t* value);
+
+/* Achievable-HBM probe (BASELINE.md §4 asks for measured peaks beside the spec sheet's): out = in over
+ * nbytes (16-byte aligned, nbytes % 16 == 0) with nontemporal 16-byte loads and stores; moves 2 * nbytes. */
+int m2f_stream_copy(const void* in, void* out, int64_t nbytes, void* stream);
 
 /* Batched fp32 transpose out[b][q][r] = in[b][r][q] (row strides in_ld / out_ld, batch strides in_bs /
  * out_bs, in elements; B <= 65535): the pixel decoder's level flatten, cat([x_l.flatten(2).transpose(1, 2)],

@@ -8,7 +8,7 @@ from bm2f_amd.bench_model import bias_act
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("residual", [False, True])
 def test_bias_act_matches_unfused(device, dtype, residual):
     torch.manual_seed(0)
@@ -29,7 +29,7 @@ def test_bias_act_matches_unfused(device, dtype, residual):
         torch.testing.assert_close(ra.grad, torch.where(mask, g, torch.zeros_like(g)))
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("nout,unused", [(2, None), (3, None), (3, 1)])
 def test_bias_act_fork_sums_consumer_grads(device, dtype, nout, unused):
     """bias_act(..., nout): one handle per consumer; the backward (m2f_relu_bwd_sum) gives sum_k g_k * (y > 0)
@@ -55,7 +55,7 @@ def test_bias_act_fork_sums_consumer_grads(device, dtype, nout, unused):
     torch.testing.assert_close(ra.grad, want, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 @pytest.mark.parametrize("H,W", [(16, 24), (7, 9), (1, 1), (2, 3), (5, 16), (1, 8)])
 def test_stem_maxpool_matches_torch(device, dtype, H, W):
     """The stem max pool (csrc/eltwise.hip, 1-byte winners) against F.max_pool2d(3, 2, 1): forward and
@@ -76,3 +76,23 @@ def test_stem_maxpool_matches_torch(device, dtype, H, W):
     ya.backward(g)
     yb.backward(g)
     assert torch.equal(xa.grad, xb.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
+def test_bias_act_nan_follows_torch(device, dtype):
+    """NaN activations: the forward propagates them as torch's relu does, and the multi-consumer backward
+    (m2f_relu_bwd_sum) passes the gradient where y is NaN, as torch's threshold_backward (y <= 0 -> 0)."""
+    torch.manual_seed(1)
+    x = torch.randn(2, 64, 16, 24, device=device, dtype=dtype)
+    x.view(-1)[::97] = float("nan")
+    b = torch.randn(64, device=device)
+    xa = x.clone().requires_grad_()
+    hs = bias_act(xa.clone(), b, None, 2)
+    want_y = F.relu(x.float() + b.view(1, -1, 1, 1)).to(dtype)
+    assert torch.equal(hs[0].isnan(), want_y.isnan())
+    torch.testing.assert_close(hs[0].nan_to_num(), want_y.nan_to_num(), rtol=0, atol=0)
+    gs = [torch.randn_like(hs[0]) for _ in range(2)]
+    sum((h.float() * g.float()).sum() for h, g in zip(hs, gs)).backward()
+    tot = gs[0].float() + gs[1].float()
+    want = torch.ops.aten.threshold_backward(tot, want_y.float(), 0).to(dtype)
+    torch.testing.assert_close(xa.grad, want, rtol=0, atol=0)

@@ -111,7 +111,8 @@ def test_mask_heads_fallback_shapes(device):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
-@pytest.mark.parametrize("B,Q,N", [(2, 100, 4096), (1, 7, 1040), (2, 37, 65536), (1, 128, 2064), (3, 65, 512)])
+@pytest.mark.parametrize("B,Q,N", [(2, 100, 4096), (1, 7, 1040), (2, 37, 65536), (1, 128, 2064), (3, 65, 512),
+                                   (2, 200, 16384), (1, 129, 1040), (2, 256, 4096), (1, 161, 528), (2, 224, 2064)])
 def test_mask_heads_bwd_embed(device, dt, B, Q, N):
     """d embed = G F^T (split over N, fp32 partials summed in a fixed order): within one dtype ulp of the
     exact product rounded once, plus the fp32 accumulation error sqrt(N) 2^-24 sum|g f| that any fp32 GEMM
@@ -127,7 +128,7 @@ def test_mask_heads_bwd_embed(device, dt, B, Q, N):
     bound = ref.float().abs() * ULP[dt] + mag * (N ** 0.5 * 2.0 ** -24) + 1e-6
     assert bool((d <= bound).all()), f"max {d.max().item():.3g}"
     assert decoder_ops._bwd_fusable(f, g)
-    assert not decoder_ops._bwd_fusable(f, torch.empty(B, 129, N, device=device, dtype=DT[dt]))  # -> torch.bmm
+    assert not decoder_ops._bwd_fusable(f, torch.empty(B, 257, N, device=device, dtype=DT[dt]))  # -> torch.bmm
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])

@@ -186,13 +186,16 @@ def _pyramid_case(shapes, N, M, far_frac, seed):
 @pytest.mark.parametrize("tile,rows,halo", [(16, 2304, 8), (12, 2304, 8), (8, 480, 8), (4, 64, 2), (8, 200, 0),
                                            (6, 2304, 12), (16, 700, 8)])
 def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo):
-    """The tiled backward over tile / cell-budget / halo geometries (M2F_MSDA_*: geometry only), on a
+    """The tiled backward over tile / cell-budget / halo geometries (m2f_set_option msda_*: geometry only), on a
     non-square pyramid whose tiles do not divide every level evenly, 5 % of the samples thrown far (the
     direct-atomic path), against the C oracle and the untiled kernel."""
-    from bm2f_amd import msda
-    monkeypatch.setenv("M2F_MSDA_TILE", str(tile))
-    monkeypatch.setenv("M2F_MSDA_WIN_ROWS", str(rows))
-    monkeypatch.setenv("M2F_MSDA_HALO", str(halo))
+    from bm2f_amd import _native, msda
+    with _native.options(msda_tile=tile, msda_win_rows=rows, msda_halo=halo):
+        _tiled_backward_case(device, tile, rows)
+
+
+def _tiled_backward_case(device, tile, rows):
+    from bm2f_amd import _native, msda
     shapes = [(6, 10), (12, 20), (24, 40)]   # non-square, tiles not dividing every level evenly
     value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 2, 8, 0.05, tile + rows)
     dst = msda.attach_host_shapes(st.to(device), shapes)
@@ -205,9 +208,9 @@ def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo):
     assert amb.mean() < 2e-3
     _close(np.where(amb, 0.0, gl.cpu().numpy()), np.where(amb, 0.0, wl), atol_frac=1e-4)
     # identical to the untiled kernel up to summation order
-    monkeypatch.setenv("M2F_MSDA_BWD_TILED", "0")
-    gv2, gl2, ga2 = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
-                                                attn.to(device), gout.to(device), 64)
+    with _native.options(msda_bwd_tiled=0):
+        gv2, gl2, ga2 = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
+                                                    attn.to(device), gout.to(device), 64)
     torch.testing.assert_close(gv, gv2, rtol=1e-5, atol=1e-5)
     # channel sums in another order (DPP tree vs shuffle tree)
     torch.testing.assert_close(ga, ga2, rtol=1e-4, atol=1e-6 * ga2.abs().max().item())
@@ -278,6 +281,7 @@ def test_forward_nonfinite_values_like_oracle(device):
 def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
     """MSDeformAttn with the fused front end == the reference-structured path (Linear -> softmax -> loc ->
     MSDA), outputs and every gradient, on an encoder-shaped call."""
+    from bm2f_amd import msda
     from bm2f_amd.msda import MSDeformAttn, attach_host_shapes
     torch.manual_seed(0)
     L = len(shapes)
@@ -298,8 +302,8 @@ def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
     src = torch.randn(N, S, 256, device=device)
     pos = torch.randn(N, S, 256, device=device)
     outs, grads = [], []
-    for fused in ("1", "0"):
-        monkeypatch.setenv("M2F_MSDA_FUSED", fused)
+    for fused in (True, False):
+        monkeypatch.setattr(msda, "FUSED", fused)
         m.zero_grad()
         x = src.clone().requires_grad_()
         out = m(x + pos, ref, x, st, lsi)

@@ -7,7 +7,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from bm2f_amd import linear_ops  # noqa: E402
+from bm2f_amd import _native, linear_ops  # noqa: E402
 
 
 def timeit(fn, iters=10):
@@ -29,7 +29,7 @@ def rel(a, b):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=16 * 21504)
-    ap.add_argument("--sweep", default="", help="comma list of M2F_GEMM_NT_CFG values to time for fwd/dgrad")
+    ap.add_argument("--sweep", default="", help="comma list of gemm_nt_cfg option values to time for fwd/dgrad")
     a = ap.parse_args()
     M = a.rows
     dev = torch.device("cuda")
@@ -72,13 +72,13 @@ def main():
         eb = rel(db, g.double().sum(0))
         print(" " * 28, "wgrad".ljust(6), f"{t0:9.3f} {flops / t0 / 1e9:6.1f} {t1:9.3f} {flops / t1 / 1e9:6.1f} {e0:10.2e} {e1:10.2e} bias {eb:.1e}")
         for cfg in [c for c in a.sweep.split(",") if c]:
-            os.environ["M2F_GEMM_NT_CFG"] = cfg
+            _native.set_option("gemm_nt_cfg", int(cfg))
             tf = timeit(lambda: linear_ops.gemm_nt(x, w, b))
             td = timeit(lambda: linear_ops.gemm_nt(g, wt))
             ef = rel(linear_ops.gemm_nt(x, w, b)[sub], x[sub].double() @ w.double().t() + b.double())
             print(" " * 28, f"cfg{cfg}".ljust(6), f"fwd {tf:7.3f} ms {flops / tf / 1e9:6.1f} TF  dgrad {td:7.3f} ms "
                   f"{flops / td / 1e9:6.1f} TF  err {ef:.1e}")
-            del os.environ["M2F_GEMM_NT_CFG"]
+            _native.set_option("gemm_nt_cfg", -1)
         del x, w, g
 
 

@@ -7,7 +7,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
 
-from bm2f_amd import linear_ops  # noqa: E402
+from bm2f_amd import _native, linear_ops  # noqa: E402
 
 
 def timeit(fn, iters=10):
@@ -29,7 +29,7 @@ def rel(a, b):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=16 * 21504)
-    ap.add_argument("--cfgs", default="0,2,3", help="M2F_GEMM_X3_NT_CFG values to time")
+    ap.add_argument("--cfgs", default="0,2,3", help="x3_nt_cfg option values to time")
     ap.add_argument("--x3-only", action="store_true", help="time only the x3 engine (A/B runs)")
     a = ap.parse_args()
     M = a.rows
@@ -52,12 +52,12 @@ def main():
         res["x3"] = (timeit(lambda: linear_ops.gemm_nt(x, w, b, engine="x3")),
                      rel(linear_ops.gemm_nt(x, w, b, engine="x3")[sub], ref))
         for c in [c for c in a.cfgs.split(",") if c]:
-            os.environ["M2F_GEMM_X3_NT_CFG"] = c
+            _native.set_option("x3_nt_cfg", int(c))
             try:
                 res[f"x3c{c}"] = (timeit(lambda: linear_ops.gemm_nt(x, w, b, engine="x3")),
                                   rel(linear_ops.gemm_nt(x, w, b, engine="x3")[sub], ref))
             finally:
-                del os.environ["M2F_GEMM_X3_NT_CFG"]
+                _native.set_option("x3_nt_cfg", -1)
         print(f"fwd   M={M} K={K} N={N}: " + "  ".join(f"{k} {t:.3f}ms {fl / t / 1e9:.0f}TF err {e:.1e}" for k, (t, e) in res.items()), flush=True)
         wt = w.t().contiguous()
         ref = g[sub].double() @ w.double()

@@ -129,7 +129,7 @@ def main():
     tf = 0.0 if a.bwd_only else timeit(fwd, a.iters)
     tb = timeit(bwd, a.iters)
     tf = tf or float("nan")
-    print(f"N={a.n} res={r} fused={a.fused} stress={a.stress} noise={a.noise} env={ {k: v for k, v in os.environ.items() if k.startswith('M2F_')} }: fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
+    print(f"N={a.n} res={r} fused={a.fused} stress={a.stress} noise={a.noise} : fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
           f"bwd {tb:.3f} ms ({bwd_bytes / tb / 1e6:.0f} GB/s alg)")
 
 

@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--n", type=int, default=16)
     ap.add_argument("--lib", default=LIB, help="diagnostic library to load (default: the --build output)")
     ap.add_argument("--noise", type=float, default=1.0)
+    ap.add_argument("--threads", type=int, default=512)
+    ap.add_argument("--tile", type=int, default=0, help="tile edge on the finest level (0: the default)")
     a = ap.parse_args()
     if a.build:
         build()
@@ -51,9 +53,12 @@ def main():
     gl = torch.empty_like(loc)
     ga = torch.empty_like(attn)
     import math as _m
-    thr = int(os.environ.get('M2F_MSDA_THREADS', '512'))
-    th = int(os.environ.get('M2F_MSDA_TILE', '16' if thr >= 1024 else '12'))
-    tw = int(os.environ.get('M2F_MSDA_TILE_W', str(th)))
+    thr = a.threads
+    th = a.tile or (16 if thr >= 1024 else 12)
+    tw = th
+    lib.m2f_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
+    lib.m2f_set_option(b"msda_threads", thr)
+    lib.m2f_set_option(b"msda_tile", th)
     nwg = _m.ceil(128 / th) * _m.ceil(128 / tw) * M * N
     stamps = torch.zeros(nwg * 8, dtype=torch.int64, device=v.device)
     hs = (ctypes.c_int64 * 6)(*[x for hw in shapes for x in hw])
