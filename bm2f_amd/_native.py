@@ -49,6 +49,7 @@ _SIGNATURES = {
     "m2f_gemm_f32x3_nt_workspace": [_i, _i, _p],
     "m2f_gemm_f32x3_nt": [_p, _l, _p, _l, _i, _p, _i, _p, _l, _p, _l, _i, _i, _i, _p, _l, _p],
     "m2f_gemm_f32x3_nt_add": [_p, _l, _p, _l, _i, _p, _i, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _p, _l, _p],
+    "m2f_gemm_f32x3_nt_bits": [_p, _l, _p, _l, _i, _p, _i, _p, _p, _l, _p, _l, _i, _i, _i, _p, _l, _p],
     "m2f_gemm_f32x3_tn_workspace": [_i, _i, _i, _p],
     "m2f_gemm_f32x3_tn": [_p, _l, _p, _l, _p, _l, _p, _i, _i, _i, _p, _l, _p],
     "m2f_conv_f32x3_workspace": [_i, _i, _i, _i, _i, _i, _p],

@@ -41,7 +41,19 @@ namespace {
 
 using namespace m2f_x3;
 
-enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4, kAdd = 8 };  // kAdd: C = A.B (+bias) + D1 (+ D2)
+// kAdd: C = A.B (+bias) + D1 (+ D2);  kBitsOut: with kRelu, also bits[m][n / 32] bit n % 32 = (C > 0) (the FFN's
+// ReLU mask, 1 bit per element);  kBitsIn: C = A.B masked by those bits (the FFN input gradient's ReLU backward)
+enum Epi { kNone = 0, kBias = 1, kRelu = 2, kMask = 4, kAdd = 8, kBitsOut = 16, kBitsIn = 32 };
+
+// bit t of each of the four bytes -> bits 4 j + t of a word (j = byte index): the 8 lanes x 4 columns of one
+// epilogue row, ballot-gathered per column offset t, become that row's 32-column mask word
+__device__ __forceinline__ unsigned spread4(unsigned byte) {
+  unsigned x = byte & 0xffu;
+  x = (x | (x << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  x = (x | (x << 3)) & 0x11111111u;
+  return x;
+}
 
 // ---------------------------------------------------------------------------------------------------
 // NT: C[M,N] = A[M,K] . B[N,K]^T.
@@ -94,7 +106,7 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
                                                        const float* __restrict__ bias,
                                                        const float* __restrict__ mask, int64_t ldm,
                                                        const float* D1, const float* D2, int64_t ldd,
-                                                       float* C, int64_t ldc, int M, int N, int K) {
+                                                       uint32_t* bits, float* C, int64_t ldc, int M, int N, int K) {
   constexpr int NT = 64 * NW, BM = 32 * NW, TJ = BN / 32;
   constexpr int PIECES = 3 * BN * 2;             // 16-byte pieces of one B chunk
   constexpr int NBL = (PIECES + NT - 1) / NT;    // per thread
@@ -225,9 +237,25 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
     for (int rr = 0; rr < 4; ++rr) {
       const int lr = rr * 8 + er, row = m0 + w * 32 + lr;
       f4 v = *reinterpret_cast<const f4*>(&img[lr * EP + ec]) + bv;
-      if (row >= M || col >= N) continue;
       if constexpr ((EPI & kRelu) != 0) {
         v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      }
+      if constexpr ((EPI & kBitsOut) != 0) {  // N % 32 == 0: a tile is in range or out as a whole
+        const bool in = row < M && col < N;
+        const unsigned long long b0 = __ballot(in && v.x > 0.f), b1 = __ballot(in && v.y > 0.f);
+        const unsigned long long b2 = __ballot(in && v.z > 0.f), b3 = __ballot(in && v.w > 0.f);
+        if ((lane & 7) == 0 && in) {
+          const int sh = 8 * er;
+          bits[static_cast<int64_t>(row) * ldm + ((n0 + j * 32) >> 5)] =
+              spread4(static_cast<unsigned>(b0 >> sh)) | (spread4(static_cast<unsigned>(b1 >> sh)) << 1) |
+              (spread4(static_cast<unsigned>(b2 >> sh)) << 2) | (spread4(static_cast<unsigned>(b3 >> sh)) << 3);
+        }
+      }
+      if (row >= M || col >= N) continue;
+      if constexpr ((EPI & kBitsIn) != 0) {
+        const unsigned nib = bits[static_cast<int64_t>(row) * ldm + ((n0 + j * 32) >> 5)] >> ec;
+        v.x = (nib & 1u) ? v.x : 0.f; v.y = (nib & 2u) ? v.y : 0.f;
+        v.z = (nib & 4u) ? v.z : 0.f; v.w = (nib & 8u) ? v.w : 0.f;
       }
       const bool vec = col + 3 < N && ((ldc & 3) == 0) && (!(EPI & kMask) || (ldm & 3) == 0);
       if (vec) {
@@ -262,17 +290,17 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
 
 template <int BN, int NW>
 int launch_nt(int epi, const float* A, int64_t lda, const __bf16* Bs, int NP, const float* bias, const float* mask,
-              int64_t ldm, const float* D1, const float* D2, int64_t ldd, float* C, int64_t ldc, int M, int N, int K,
-              hipStream_t st) {
+              int64_t ldm, const float* D1, const float* D2, int64_t ldd, uint32_t* bits, float* C, int64_t ldc, int M,
+              int N, int K, hipStream_t st) {
   constexpr int BM = 32 * NW;
   const int64_t nwg = static_cast<int64_t>((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (nwg > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "m2f_gemm_f32x3_nt: too many tiles");
   const dim3 grid(static_cast<unsigned>(nwg)), block(64 * NW);
 #define M2F_X3NT(E)                                                                                            \
   (K % kBK == 0 ? x3_nt_kernel<BN, NW, E, true><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, \
-                                                                       C, ldc, M, N, K)                           \
+                                                                       bits, C, ldc, M, N, K)                     \
                 : x3_nt_kernel<BN, NW, E, false><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, D1, D2,     \
-                                                                        ldd, C, ldc, M, N, K))
+                                                                        ldd, bits, C, ldc, M, N, K))
   switch (epi) {
     case kNone: M2F_X3NT(kNone); break;
     case kBias: M2F_X3NT(kBias); break;
@@ -282,6 +310,10 @@ int launch_nt(int epi, const float* A, int64_t lda, const __bf16* Bs, int NP, co
     case kBias | kMask: M2F_X3NT(kBias | kMask); break;
     case kAdd: M2F_X3NT(kAdd); break;
     case kBias | kAdd: M2F_X3NT(kBias | kAdd); break;
+    case kRelu | kBitsOut: M2F_X3NT(kRelu | kBitsOut); break;
+    case kBias | kRelu | kBitsOut: M2F_X3NT(kBias | kRelu | kBitsOut); break;
+    case kBitsIn: M2F_X3NT(kBitsIn); break;
+    case kBias | kBitsIn: M2F_X3NT(kBias | kBitsIn); break;
     default: return m2f::fail(M2F_EINVAL, "m2f_gemm_f32x3_nt: epilogue %d", epi);
   }
 #undef M2F_X3NT
@@ -586,18 +618,12 @@ extern "C" int m2f_gemm_f32x3_nt_workspace(int N, int K, int64_t* workspace_byte
   return m2f::ok();
 }
 
-extern "C" int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
-                                 int relu, const float* mask, int64_t ldm, float* C, int64_t ldc, int M, int N, int K,
-                                 void* workspace, int64_t workspace_bytes, void* stream) {
-  return m2f_gemm_f32x3_nt_add(A, lda, B, ldb, b_kn, bias, relu, mask, ldm, nullptr, nullptr, 0, C, ldc, M, N, K,
-                               workspace, workspace_bytes, stream);
-}
+namespace {
 
-extern "C" int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn,
-                                     const float* bias, int relu, const float* mask, int64_t ldm, const float* D1,
-                                     const float* D2, int64_t ldd, float* C, int64_t ldc, int M, int N, int K,
-                                     void* workspace, int64_t workspace_bytes, void* stream) {
-  const char* fn = "m2f_gemm_f32x3_nt";
+int nt_impl(const char* fn, const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
+            int relu, const float* mask, int64_t ldm, const float* D1, const float* D2, int64_t ldd, uint32_t* bits_out,
+            const uint32_t* bits_in, int64_t ldbits, float* C, int64_t ldc, int M, int N, int K, void* workspace,
+            int64_t workspace_bytes, void* stream) {
   if (M < 0 || N <= 0 || K <= 0) return m2f::fail(M2F_EINVAL, "%s: M %d N %d K %d", fn, M, N, K);
   if (!A || !B || !C) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
   if (K % 4 || lda % 4 || lda < K || ldb < (b_kn ? N : K) || ldc < N || !m2f::aligned(A, 16))
@@ -609,6 +635,12 @@ extern "C" int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B
   if (D1 && (ldd < N || (ldd & 3) || (ldc & 3) || ((N & 3) != 0) || !m2f::aligned(D1, 16) ||
              (D2 && !m2f::aligned(D2, 16)) || !m2f::aligned(C, 16)))
     return m2f::fail(M2F_EINVAL, "%s: addends need ldd >= N, N/ldd/ldc multiples of 4, 16-byte alignment", fn);
+  if (bits_out || bits_in) {
+    if ((bits_out && bits_in) || (bits_out && !relu) || (bits_in && relu) || mask || D1)
+      return m2f::fail(M2F_EINVAL, "%s: bits_out needs relu, bits_in excludes relu; neither with mask or addends", fn);
+    if (N % 32 || ldbits < N / 32 || (ldc & 3) || !m2f::aligned(C, 16))
+      return m2f::fail(M2F_EINVAL, "%s: mask bits need N %% 32 == 0, ldbits >= N / 32, ldc %% 4 == 0", fn);
+  }
   if (!workspace || workspace_bytes < nt_workspace(N, K) || !m2f::aligned(workspace, 16))
     return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld (16-byte aligned)", fn,
                      static_cast<long long>(workspace_bytes), static_cast<long long>(nt_workspace(N, K)));
@@ -618,19 +650,48 @@ extern "C" int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B
   __bf16* Bs = static_cast<__bf16*>(workspace);
   x3_presplit<<<m2f::ceil_div(static_cast<int64_t>(nchunks) * NP, 256), 256, 0, st>>>(B, ldb, b_kn, N, K, NP, nchunks, Bs);
   if (int rc = m2f::check_launch(fn)) return rc;
-  const int epi = (bias ? kBias : 0) | (relu ? kRelu : 0) | (mask ? kMask : 0) | (D1 ? kAdd : 0);
+  const int epi = (bias ? kBias : 0) | (relu ? kRelu : 0) | (mask ? kMask : 0) | (D1 ? kAdd : 0) |
+                  (bits_out ? kBitsOut : 0) | (bits_in ? kBitsIn : 0);
+  uint32_t* bits = bits_out ? bits_out : const_cast<uint32_t*>(bits_in);
+  if (bits) ldm = ldbits;
   // 96-wide columns of 4 waves for N = 3 * 96 k (the 288-wide sampling projection), else 128-wide columns
   // of 8 waves (256 rows share one B chunk: 0.285 vs 0.321 ms at K = N = 256, 0.913 vs 0.949 at K = 1024,
   // equal at N = 1024; tools/gemm_x3_bench.py, r2af)
   int cfg = (N % 128 != 0 && N % 96 == 0) ? 1 : 3;
   cfg = m2f::option(m2f::kOptX3NtCfg, cfg);
   switch (cfg) {
-    case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
-    case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
-    case 2: return launch_nt<256, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
-    case 3: return launch_nt<128, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, C, ldc, M, N, K, st);
+    case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, bits, C, ldc, M, N, K, st);
+    case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, bits, C, ldc, M, N, K, st);
+    case 2: return launch_nt<256, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, bits, C, ldc, M, N, K, st);
+    case 3: return launch_nt<128, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, bits, C, ldc, M, N, K, st);
     default: return m2f::fail(M2F_EINVAL, "%s: config %d", fn, cfg);
   }
+}
+
+}  // namespace
+
+extern "C" int m2f_gemm_f32x3_nt(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
+                                 int relu, const float* mask, int64_t ldm, float* C, int64_t ldc, int M, int N, int K,
+                                 void* workspace, int64_t workspace_bytes, void* stream) {
+  return nt_impl("m2f_gemm_f32x3_nt", A, lda, B, ldb, b_kn, bias, relu, mask, ldm, nullptr, nullptr, 0, nullptr,
+                 nullptr, 0, C, ldc, M, N, K, workspace, workspace_bytes, stream);
+}
+
+extern "C" int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn,
+                                     const float* bias, int relu, const float* mask, int64_t ldm, const float* D1,
+                                     const float* D2, int64_t ldd, float* C, int64_t ldc, int M, int N, int K,
+                                     void* workspace, int64_t workspace_bytes, void* stream) {
+  return nt_impl("m2f_gemm_f32x3_nt_add", A, lda, B, ldb, b_kn, bias, relu, mask, ldm, D1, D2, ldd, nullptr, nullptr,
+                 0, C, ldc, M, N, K, workspace, workspace_bytes, stream);
+}
+
+extern "C" int m2f_gemm_f32x3_nt_bits(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn,
+                                      const float* bias, int relu, uint32_t* bits_out, const uint32_t* bits_in,
+                                      int64_t ldbits, float* C, int64_t ldc, int M, int N, int K, void* workspace,
+                                      int64_t workspace_bytes, void* stream) {
+  if (!bits_out && !bits_in) return m2f::fail(M2F_EINVAL, "m2f_gemm_f32x3_nt_bits: no mask bits");
+  return nt_impl("m2f_gemm_f32x3_nt_bits", A, lda, B, ldb, b_kn, bias, relu, nullptr, 0, nullptr, nullptr, 0,
+                 bits_out, bits_in, ldbits, C, ldc, M, N, K, workspace, workspace_bytes, stream);
 }
 
 extern "C" int m2f_gemm_f32x3_tn_workspace(int M, int N1, int N2, int64_t* workspace_bytes) {

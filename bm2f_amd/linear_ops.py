@@ -89,6 +89,40 @@ def gemm_nt(a, b, bias=None, relu=False, mask=None, out=None, engine=None, b_kn=
     return out
 
 
+def gemm_nt_bits(a, b, bias=None, bits_out=None, bits_in=None, b_kn=False):
+    """x3 NT GEMM with the ReLU as a 1-bit mask: ``bits_out`` (M, N/32) int32 -> C = relu(a b^T + bias) and the
+    mask of C > 0 written there; ``bits_in`` -> C = (a b^T + bias) where the mask bit is set, else 0."""
+    M, K = a.shape
+    N = b.shape[1] if b_kn else b.shape[0]
+    out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    bits = bits_out if bits_out is not None else bits_in
+    wsb = ctypes.c_int64(0)
+    _native.call("m2f_gemm_f32x3_nt_workspace", N, K, ctypes.byref(wsb))
+    ws = torch.empty(max(wsb.value, 16), device=a.device, dtype=torch.uint8)
+    _native.call("m2f_gemm_f32x3_nt_bits", a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)),
+                 1 if b_kn else 0, bias.data_ptr() if bias is not None else None, 1 if bits_out is not None else 0,
+                 bits_out.data_ptr() if bits_out is not None else None,
+                 bits_in.data_ptr() if bits_in is not None else None, _c64(bits.stride(0)),
+                 out.data_ptr(), _c64(out.stride(0)), M, N, K, ws.data_ptr(), _c64(ws.numel()), _stream(a))
+    return out
+
+
+def _relu_bits(x2, w1, b1):
+    """h = relu(x2 w1^T + b1) and its 1-bit mask (rows, N/32) when the x3 engine takes it, else (h, None)."""
+    N = w1.shape[0]
+    if ENGINE == "x3" and N % 32 == 0:
+        bits = torch.empty(x2.shape[0], N // 32, device=x2.device, dtype=torch.int32)
+        return gemm_nt_bits(x2, w1, b1, bits_out=bits), bits
+    return gemm_nt(x2, w1, b1, relu=True), None
+
+
+def _masked_dgrad(g, w2, h, bits):
+    """grad_h = (g . w2) * (h > 0): from the 1-bit mask when there is one, else from h itself."""
+    if bits is not None:
+        return gemm_nt_bits(g, w2, bits_in=bits, b_kn=True)
+    return gemm_nt(g, w2, mask=h, b_kn=True)
+
+
 def gemm_tn(a, b, colsum=False, engine=None):
     """(a.T @ b, a.sum(0) if colsum) for a (M, N1), b (M, N2) fp32 row-major."""
     M, N1 = a.shape
@@ -169,22 +203,22 @@ class FFNF32(Function):
         x2 = _rows(x)
         if x2.stride(-1) != 1 or x2.stride(0) % 4:
             x2 = x2.contiguous()
-        h = gemm_nt(x2, w1, b1, relu=True)
+        h, bits = _relu_bits(x2, w1, b1)
         y = _mm_nt(h, w2, b2)
-        ctx.save_for_backward(x2, w1, w2, h)
+        ctx.save_for_backward(x2, w1, w2, h, bits)
         ctx.in_shape = x.shape
         ctx.biases = (b1 is not None, b2 is not None)
         return y.view(*x.shape[:-1], w2.shape[0])
 
     @staticmethod
     def backward(ctx, grad):
-        x2, w1, w2, h = ctx.saved_tensors
+        x2, w1, w2, h, bits = ctx.saved_tensors
         g = _rows(grad)
         if g.stride(-1) != 1 or g.stride(0) % 4:
             g = g.contiguous()
         nig = ctx.needs_input_grad
         dw2, db2 = gemm_tn(g, h, colsum=ctx.biases[1] and nig[4]) if (nig[3] or nig[4]) else (None, None)
-        gh = gemm_nt(g, w2, mask=h, b_kn=True)                  # grad_h with the ReLU mask (h > 0)
+        gh = _masked_dgrad(g, w2, h, bits)                      # grad_h with the ReLU mask (h > 0)
         del h
         dw1, db1 = gemm_tn(gh, x2, colsum=ctx.biases[0] and nig[2]) if (nig[1] or nig[2]) else (None, None)
         dx = _mm_nn(gh, w1).view(ctx.in_shape) if nig[0] else None
@@ -209,20 +243,20 @@ class FFNResidualF32(Function):
         x2 = _rows(x)
         if not x2.is_contiguous():
             x2 = x2.contiguous()
-        h = gemm_nt(x2, w1, b1, relu=True)
+        h, bits = _relu_bits(x2, w1, b1)
         y = gemm_nt(h, w2, b2)
-        ctx.save_for_backward(x2, w1, w2, h)
+        ctx.save_for_backward(x2, w1, w2, h, bits)
         ctx.in_shape = x.shape
         ctx.biases = (b1 is not None, b2 is not None)
         return y.view(*x.shape[:-1], w2.shape[0]), x2.view(x.shape)
 
     @staticmethod
     def backward(ctx, grad, grad_pass):
-        x2, w1, w2, h = ctx.saved_tensors
+        x2, w1, w2, h, bits = ctx.saved_tensors
         g = _grad_rows(grad, x2)
         nig = ctx.needs_input_grad
         dw2, db2 = gemm_tn(g, h, colsum=ctx.biases[1] and nig[4]) if (nig[3] or nig[4]) else (None, None)
-        gh = gemm_nt(g, w2, mask=h, b_kn=True)
+        gh = _masked_dgrad(g, w2, h, bits)
         del h
         dw1, db1 = gemm_tn(gh, x2, colsum=ctx.biases[0] and nig[2]) if (nig[1] or nig[2]) else (None, None)
         dx = None

@@ -250,6 +250,14 @@ int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B, int64_t l
                           int relu, const float* mask, int64_t ldm, const float* D1, const float* D2, int64_t ldd,
                           float* C, int64_t ldc, int M, int N, int K, void* workspace, int64_t workspace_bytes,
                           void* stream);
+/* m2f_gemm_f32x3_nt_bits: the FFN's ReLU as a 1-bit mask (msdeformattn.py:101-106).  With bits_out (relu != 0):
+ *   C = relu(A.B^T + bias) and bits_out[m][n / 32] bit n % 32 = (C[m][n] > 0).  With bits_in (relu == 0):
+ *   C = (A.B^T + bias) where the bit is set, else 0 -- the ReLU backward of grad_h = grad_y . W2 read from
+ *   M*N/8 bytes instead of the (M, N) fp32 activation.  Exactly one of bits_out / bits_in; N % 32 == 0,
+ *   ldbits (in 32-bit words) >= N / 32, ldc % 4 == 0, C 16-byte aligned. */
+int m2f_gemm_f32x3_nt_bits(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
+                           int relu, uint32_t* bits_out, const uint32_t* bits_in, int64_t ldbits, float* C,
+                           int64_t ldc, int M, int N, int K, void* workspace, int64_t workspace_bytes, void* stream);
 int m2f_gemm_f32x3_tn_workspace(int M, int N1, int N2, int64_t* workspace_bytes);
 int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, int64_t ldb, float* C, int64_t ldc,
                       float* colsum, int M, int N1, int N2, void* workspace, int64_t workspace_bytes,

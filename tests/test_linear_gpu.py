@@ -194,3 +194,29 @@ def test_encoder_layer_residual_fused_matches_autograd_sums(device, pos_batch):
     assert torch.equal(res[True][0], res[False][0])
     for a, b in zip(res[True][1:], res[False][1:]):
         assert _rel(a, b) < 1e-6
+
+
+@pytest.mark.parametrize("M,N,K,b_kn", [(1000, 1024, 256, False), (777, 64, 96, False), (513, 256, 1024, True)])
+def test_gemm_nt_relu_bits(device, M, N, K, b_kn):
+    """The FFN's 1-bit ReLU mask (m2f_gemm_f32x3_nt_bits): the forward writes bit (m, n) = relu(.)[m, n] > 0 and
+    the same relu output as the float path; the masked input gradient from the bits equals the one masked by
+    the fp32 activation, bit for bit."""
+    torch.manual_seed(M + N)
+    a = torch.randn(M, K, device=device)
+    w = torch.randn(N, K, device=device) / K ** 0.5
+    b = torch.randn(N, device=device)
+    bits = torch.empty(M, N // 32, device=device, dtype=torch.int32)
+    h = linear_ops.gemm_nt_bits(a, w, b, bits_out=bits)
+    assert torch.equal(h, linear_ops.gemm_nt(a, w, b, relu=True))
+    shifts = torch.arange(32, device=device, dtype=torch.int64)
+    unpacked = ((bits.to(torch.int64).unsqueeze(-1) >> shifts) & 1).reshape(M, N).bool()
+    assert torch.equal(unpacked, h > 0)
+    g = torch.randn(M, K if not b_kn else K, device=device)
+    w2 = torch.randn(N, K, device=device) / K ** 0.5 if not b_kn else torch.randn(K, N, device=device) / K ** 0.5
+    if b_kn:   # grad_h = g . W2 with W2 (K, N) read in place, as the FFN's backward
+        got = linear_ops.gemm_nt_bits(g, w2, bits_in=bits, b_kn=True)
+        want = linear_ops.gemm_nt(g, w2, mask=h, b_kn=True)
+    else:
+        got = linear_ops.gemm_nt_bits(g, w2, bits_in=bits)
+        want = linear_ops.gemm_nt(g, w2, mask=h)
+    assert torch.equal(got, want)
