@@ -19,7 +19,7 @@ Besides the contract fields it reports:
   (Base-COCO-PanopticSegmentation.yaml SOLVER.AMP.ENABLED; detectron2's AMPTrainer).
   modes         N=1 only: the same step under AMP bf16 (no scaler) and with no autocast at all (fp32 parity
                 mode), fewer steps.
-  achievable    N=1 only: measured ceilings on this box -- a nontemporal float4 stream copy (m2f_stream_copy,
+  achievable    N=1 only: measured ceilings on this box -- a float4 stream copy (m2f_stream_copy,
                 2 x 2 GiB per launch) and an 8192^3 bf16 GEMM (hipBLASLt via torch.matmul) -- so each roofline
                 entry carries its fraction of the spec peak (frac) and of the measured one (frac_achievable).
   cpu_baseline  the reference's CPU path (oracle/cpu_path.py) on config 1 (1 x 512^2) and one 1024^2 image,
@@ -54,20 +54,30 @@ def log(msg):
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", type=int, default=2, choices=[2, 4, 5],
+                    help="BASELINE.json config: 2/3 = the R50 step (default; 3 is --gpus 8), 4 / 5 = the per-rank "
+                         "pixel-decoder + decoder slice of the Swin-L Q=200 / video T=5 configs (backbone excluded)")
+    ap.add_argument("--frames", type=int, default=5, help="config 5: frames per clip")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--batch", type=int, default=None, help="images (config 5: clips) per GPU; default 16 / 2 / 2")
     ap.add_argument("--res", type=int, default=1024)
-    ap.add_argument("--queries", type=int, default=100)
+    ap.add_argument("--queries", type=int, default=None, help="default 100 (configs 2, 5) / 200 (config 4)")
     ap.add_argument("--amp", default="fp16", choices=["fp16", "bf16", "none"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-modes", action="store_true", help="skip the bf16 / fp32 mode lines")
     ap.add_argument("--no-peaks", action="store_true", help="skip the achievable-peak probes")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the op-level MSDeformAttnFunction timing")
     ap.add_argument("--mode-steps", type=int, default=4)
     ap.add_argument("--kernel-steps", type=int, default=2, help="instrumented steps for roofline_all")
     ap.add_argument("--allow-knobs", action="store_true")
     ap.add_argument("--master-port", type=int, default=29531)
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.batch is None:
+        a.batch = 16 if a.config == 2 else 2
+    if a.queries is None:
+        a.queries = 200 if a.config == 4 else 100
+    return a
 
 
 def knob_env():
@@ -228,15 +238,6 @@ def roofline_entry(fam, k, bound):
             "ms_per_step": round(k["ms_per_step"], 3), "note": MFMA_NOTE.get(fam)}
 
 
-def msda_bwd_bytes(n_images, res, M=8, D=32, L=3, P=4):
-    S = sum((res // s) ** 2 for s in (32, 16, 8))
-    f = 4
-    value = n_images * S * M * D * f
-    loc = n_images * S * M * L * P * 2 * f
-    attn = n_images * S * M * L * P * f
-    return 2 * value + 2 * loc + 2 * attn + value  # reads v,loc,attn,gout; writes gv,gloc,gattn
-
-
 def measure_peaks(device):
     """Achievable ceilings on this box: HBM by a nontemporal stream copy, MFMA by a large bf16 GEMM."""
     import torch
@@ -257,7 +258,8 @@ def measure_peaks(device):
         torch.cuda.synchronize()
         return s.elapsed_time(e) / reps * 1e-3
 
-    t_copy = timed(lambda: _native.call("m2f_stream_copy", a.data_ptr(), b.data_ptr(), nbytes, st.cuda_stream), 20)
+    t_copy = {mode: timed(lambda: _native.call("m2f_stream_copy", a.data_ptr(), b.data_ptr(), nbytes, mode,
+                                               st.cuda_stream), 20) for mode in (0, 1)}
     del a, b
     n = 8192
     x = torch.randn(n, n, device=device, dtype=torch.bfloat16)
@@ -266,8 +268,10 @@ def measure_peaks(device):
     t_mm = timed(lambda: torch.matmul(x, y, out=out), 20)
     del x, y, out
     torch.cuda.empty_cache()
-    return {"hbm_gbs": round(2 * nbytes / t_copy / 1e9, 1), "bf16_gemm_tflops": round(2 * n ** 3 / t_mm / 1e12, 1),
-            "hbm_probe": "m2f_stream_copy: nontemporal float4 copy, 2 GiB in + 2 GiB out per launch, mean of 20",
+    rates = {mode: 2 * nbytes / t / 1e9 for mode, t in t_copy.items()}
+    return {"hbm_gbs": round(max(rates.values()), 1), "bf16_gemm_tflops": round(2 * n ** 3 / t_mm / 1e12, 1),
+            "hbm_probe": "m2f_stream_copy, 2 GiB in + 2 GiB out per launch, mean of 20, the faster of a one-pass "
+                         f"float4 copy ({rates[0]:.0f} GB/s) and a strided nontemporal one ({rates[1]:.0f} GB/s)",
             "mfma_probe": f"torch.matmul bf16 {n}x{n}x{n} (hipBLASLt), mean of 20"}
 
 
@@ -278,6 +282,94 @@ def add_achievable(ent, peaks):
     ent["achievable_peak"] = peaks[key]
     ent["frac_achievable"] = round(ent["achieved"] / peaks[key], 4)
     return ent
+
+
+def head_config_line(args, world, value, knobs):
+    """Metric / config fields of the per-rank config 4 / 5 lines (the backbone is excluded: not on the path)."""
+    amp = args.amp + (" with GradScaler" if args.amp == "fp16" else "")
+    if args.config == 4:
+        return {"metric": "images/sec fwd+bwd per rank, Swin-L COCO-instance 200-query 1024^2, pixel decoder + "
+                          "decoder (BASELINE config 4 slice, backbone excluded)",
+                "unit": "images/s", "cpu_baseline": None,
+                "data": "synthetic (Swin-L-shaped randn features, random-init weights)",
+                "config": {"workload": f"config 4 per rank: {args.batch} images/GPU at {args.res}^2, Swin-L feature "
+                                       f"channels 192/384/768/1536, MSDA pixel decoder (fp32) + {args.queries}-query "
+                                       f"decoder, K=80, fwd+bwd+AdamW under AMP {amp}; the Swin-L backbone is not "
+                                       "on the hot path and not timed",
+                           "model": "maskformer2_swin_large head", "global_batch": world * args.batch,
+                           "seq_len": sum((args.res // s) ** 2 for s in (32, 16, 8)), "queries": args.queries,
+                           "parallelism": f"dp{world}", "env": knobs}}
+    frames = args.frames
+    return {"metric": "clips/sec fwd+bwd per rank, Video Mask2Former T=5 384x640, pixel decoder + video decoder "
+                      "(BASELINE config 5 slice, backbone excluded)",
+            "unit": "clips/s", "frames_per_s": round(value * frames, 3), "cpu_baseline": None,
+            "data": "synthetic (Swin-T-shaped randn features, random-init weights)",
+            "config": {"workload": f"config 5 per rank: {args.batch} clips x T={frames} frames at 360x640 padded to "
+                                   f"384x640, Swin-T feature channels 96/192/384/768, MSDA pixel decoder per frame "
+                                   f"(N={args.batch * frames}, S=5040, fp32) + video decoder ({args.queries} queries, "
+                                   f"K=40, memory T*HW tokens, einsum bqc,btchw), fwd+bwd+AdamW under AMP {amp}; "
+                                   "the backbone is not on the hot path and not timed",
+                       "model": "video_maskformer2_swin_tiny head", "global_batch": world * args.batch,
+                       "frames": frames, "seq_len": 5040, "queries": args.queries, "parallelism": f"dp{world}",
+                       "env": knobs}}
+
+
+def measure_dropin(device, n, res, timer, kern, iters=5):
+    """The reference's unchanged op-level call (ops/modules/ms_deform_attn.py:116-117 ->
+    MSDeformAttnFunction.apply, ops/functions/ms_deform_attn_func.py:32-49): a device spatial_shapes with no host
+    tag, materialised sampling_locations / attention_weights, at the config-2 layer shape (reference-init rays
+    + N(0, 1 px) noise).  Kernel time per launch (HIP events) against the fused kernels the step
+    runs."""
+    import math
+    import torch
+    from bm2f_amd.msda import MSDeformAttnFunction
+    shapes = [(res // s, res // s) for s in (32, 16, 8)]
+    M, D, L, P = 8, 32, 3, 4
+    S = sum(h * w for h, w in shapes)
+    g = torch.Generator(device=device).manual_seed(7)
+    refs = []
+    for h, w in shapes:
+        ys, xs = torch.meshgrid(torch.linspace(0.5, h - 0.5, h, device=device),
+                                torch.linspace(0.5, w - 0.5, w, device=device), indexing="ij")
+        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
+    ref = torch.cat(refs, 0)
+    th = torch.arange(M, device=device) * (2 * math.pi / M)
+    grid = torch.stack([th.cos(), th.sin()], -1)
+    grid = grid / grid.abs().max(-1, keepdim=True)[0]
+    off = (grid.view(M, 1, 1, 2) * torch.arange(1, P + 1, device=device).view(1, 1, P, 1)).expand(M, L, P, 2)
+    off = off[None, None] + torch.randn(n, S, M, L, P, 2, device=device, generator=g)
+    norm = torch.tensor([[w, h] for h, w in shapes], dtype=torch.float32, device=device)
+    loc = (ref[None, :, None, None, None, :] + off / norm[None, None, None, :, None, :]).contiguous()
+    attn = torch.randn(n, S, M, L * P, device=device, generator=g).softmax(-1).view(n, S, M, L, P).contiguous()
+    value = torch.randn(n, S, M, D, device=device, generator=g)
+    gout = torch.randn(n, S, M * D, device=device, generator=g)
+    lsi = torch.tensor([0, shapes[0][0] * shapes[0][1], shapes[0][0] * shapes[0][1] + shapes[1][0] * shapes[1][1]],
+                       device=device)
+    v, lc, a = (t.requires_grad_() for t in (value, loc, attn))
+
+    def step():
+        st = torch.tensor(shapes, dtype=torch.int64, device=device)   # fresh and untagged, as the encoder's
+        MSDeformAttnFunction.apply(v, st, lsi, lc, a, 64).backward(gout)
+    step()
+    torch.cuda.synchronize()
+    saved, timer.events, timer.enabled = timer.events, {}, True
+    for _ in range(iters):
+        step()
+    res_k = timer.summary(iters)
+    timer.events, timer.enabled = saved, False
+    out = {}
+    for fam in ("msda_fwd", "msda_bwd"):
+        k = res_k.get(fam)
+        if not k:
+            continue
+        ent = roofline_entry(fam, k, "hbm")
+        ent["kernel"] = f"{fam} via MSDeformAttnFunction (m2f_msda_{fam[5:]}_f32, untagged device spatial_shapes)"
+        if kern.get(fam):
+            ent["vs_fused_step_kernel"] = round(k["mean_ms"] / kern[fam]["mean_ms"], 3)
+        out[fam] = ent
+    del v, lc, a, value, loc, attn, gout
+    torch.cuda.empty_cache()
+    return out
 
 
 def load_traffic():
@@ -312,18 +404,26 @@ def main():
     device = torch.device("cuda", local)
 
     from bm2f_amd import _native
-    from bm2f_amd.bench_model import MaskFormerR50, default_cfg, make_optimizer, make_scaler, train_step, wrap_ddp
+    from bm2f_amd.bench_model import (HeadBench, MaskFormerR50, default_cfg, head_features, make_optimizer, make_scaler,
+                                      train_step, wrap_ddp)
 
     timer = KernelTimer()
     timer.install(_native)
 
     torch.manual_seed(0)
-    model = MaskFormerR50(default_cfg(num_queries=args.queries)).to(device)
+    if args.config == 2:
+        model = MaskFormerR50(default_cfg(num_queries=args.queries)).to(device)
+        g = torch.Generator(device=device).manual_seed(1000 + rank)
+        images = torch.randn(args.batch, 3, args.res, args.res, device=device, generator=g) * 57.0 + 117.0
+    elif args.config == 4:   # 2 images per GPU at 1024^2, Swin-L features
+        model = HeadBench("swin_l", args.queries, 80).to(device)
+        images = head_features("swin_l", args.batch, args.res, args.res, device, seed=1000 + rank)
+    else:                    # 2 clips x T frames at 360x640 padded to 384x640, Swin-T features
+        model = HeadBench("swin_t", args.queries, 40, frames=args.frames).to(device)
+        images = head_features("swin_t", args.batch * args.frames, 384, 640, device, seed=1000 + rank)
     if world > 1:
         model = wrap_ddp(model, device)
     opt = make_optimizer(model)
-    g = torch.Generator(device=device).manual_seed(1000 + rank)
-    images = torch.randn(args.batch, 3, args.res, args.res, device=device, generator=g) * 57.0 + 117.0
     dtypes = {"bf16": torch.bfloat16, "fp16": torch.float16, "none": None}
 
     def barrier():
@@ -371,8 +471,11 @@ def main():
         kern = timer.summary(args.kernel_steps)
         timer.enabled = False
 
+    dropin = None
+    if world == 1 and args.config == 2 and not args.no_dropin:
+        dropin = measure_dropin(device, args.batch, args.res, timer, kern)
     modes = None
-    if world == 1 and not args.no_modes:
+    if world == 1 and args.config == 2 and not args.no_modes:
         modes = {}
         for name in ("fp16", "bf16", "none"):
             if name == args.amp:
@@ -390,7 +493,7 @@ def main():
         roof = None
         bwd = kern.get("msda_bwd")
         if bwd:
-            nbytes = msda_bwd_bytes(args.batch, args.res)
+            nbytes = bwd["bytes"] // int(round(bwd["calls_per_step"] * args.kernel_steps))   # per launch
             achieved = nbytes / (bwd["mean_ms"] * 1e-3) / 1e9
             tr = load_traffic()
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -403,7 +506,7 @@ def main():
         roof_all = [add_achievable(roofline_entry(fam, k, bounds[fam]), peaks)
                     for fam, k in sorted(kern.items(), key=lambda x: -x[1]["total_ms"])]
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and args.config == 2 and not args.no_cpu_baseline:
             from oracle.cpu_path import cpu_model, time_cpu_step
             log("cpu baseline ...")
             s512, threads, t512 = time_cpu_step(res=512, images=1, steps=3, warmup=1)
@@ -429,7 +532,10 @@ def main():
                        "seq_len": sum((args.res // s) ** 2 for s in (32, 16, 8)), "queries": args.queries,
                        "parallelism": f"dp{world}", "env": knobs},
             "roofline": roof, "roofline_all": roof_all, "achievable": peaks, "modes": modes, "cpu_baseline": cpu,
+            "msda_op_dropin": dropin,
         }
+        if args.config in (4, 5):
+            line.update(head_config_line(args, world, value, knobs))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -280,6 +280,47 @@ class MaskFormerR50(nn.Module):
         return self.sem_seg_head(self.backbone(x))
 
 
+# backbone output channels of the Swin variants in BASELINE configs 4 and 5 (EMBED_DIM 192 / 96, x2 per stage)
+SWIN_CHANNELS = {"swin_l": {"res2": 192, "res3": 384, "res4": 768, "res5": 1536},
+                 "swin_t": {"res2": 96, "res3": 192, "res4": 384, "res5": 768}}
+STRIDES = {"res2": 4, "res3": 8, "res4": 16, "res5": 32}
+
+
+class HeadBench(nn.Module):
+    """The per-rank slice of BASELINE configs 4 and 5 without the backbone (the Swin is outside the hot path):
+    backbone-shaped features -> MSDeformAttnPixelDecoder -> (video) masked-attention decoder, as
+    MaskFormerHead.layers (mask_former_head.py:118-121).  Config 4: Swin-L channels, Q = 200, K = 80
+    (configs/coco/instance-segmentation/swin/maskformer2_swin_large_IN21k_384_bs16_100ep.yaml); config 5:
+    Swin-T channels, the video decoder with Q = 100, K = 40 and T frames per clip
+    (configs/youtubevis_2019/video_maskformer2_R50_bs16_8ep.yaml)."""
+
+    def __init__(self, swin, num_queries, num_classes, frames=None):
+        super().__init__()
+        from .video_decoder import VideoMultiScaleMaskedTransformerDecoder
+        shape = {k: ShapeSpec(channels=c, stride=STRIDES[k]) for k, c in SWIN_CHANNELS[swin].items()}
+        self.pixel_decoder = MSDeformAttnPixelDecoder(
+            shape, transformer_dropout=0.0, transformer_nheads=8, transformer_dim_feedforward=1024,
+            transformer_enc_layers=6, conv_dim=256, mask_dim=256, norm="GN",
+            transformer_in_features=["res3", "res4", "res5"], common_stride=4)
+        kw = dict(num_classes=num_classes, hidden_dim=256, num_queries=num_queries, nheads=8, dim_feedforward=2048,
+                  dec_layers=9, pre_norm=False, mask_dim=256, enforce_input_project=False)
+        if frames:
+            self.predictor = VideoMultiScaleMaskedTransformerDecoder(256, True, num_frames=frames, **kw)
+        else:
+            self.predictor = MultiScaleMaskedTransformerDecoder(256, True, **kw)
+
+    def forward(self, features):
+        mask_features, _, multi_scale = self.pixel_decoder.forward_features(features)
+        return self.predictor(multi_scale, mask_features)
+
+
+def head_features(swin, n, h, w, device, seed=0):
+    """Backbone-shaped random features (requires_grad: their gradient is what the backbone would receive)."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    return {k: torch.randn(n, c, h // STRIDES[k], w // STRIDES[k], device=device, generator=g).requires_grad_()
+            for k, c in SWIN_CHANNELS[swin].items()}
+
+
 def wrap_ddp(model, device=None):
     """Data parallel over the image batch: DDP's bucketed gradient all-reduce (RCCL on ROCm, gloo on
     CPU) overlapped with the backward -- the path's only cross-GPU exchange."""
@@ -333,8 +374,14 @@ def make_scaler(amp_dtype):
 
 
 def train_step(model, opt, images, amp_dtype=torch.bfloat16, clip=0.01, scaler=None):
+    """One step: forward under autocast, the surrogate loss, backward (scaled under fp16), full-model grad-norm
+    clipping, AdamW.  ``images``: the image batch, or a feature dict for :class:`HeadBench`."""
     opt.zero_grad(set_to_none=True)
-    with torch.autocast(device_type=images.device.type, dtype=amp_dtype, enabled=amp_dtype is not None):
+    dev = images.device if torch.is_tensor(images) else next(iter(images.values())).device
+    if not torch.is_tensor(images):
+        for t in images.values():
+            t.grad = None
+    with torch.autocast(device_type=dev.type, dtype=amp_dtype, enabled=amp_dtype is not None):
         out = model(images)
         loss = surrogate_loss(out)
     if scaler is not None:

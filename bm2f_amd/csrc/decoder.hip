@@ -490,24 +490,42 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
   f4 dqacc[NTR > 0 ? NTR : 1][2];
 #pragma unroll
   for (int qt = 0; qt < (NTR > 0 ? NTR : 1); ++qt) dqacc[qt][0] = dqacc[qt][1] = f4{0.f, 0.f, 0.f, 0.f};
-  for (int kb0 = key_begin; kb0 < key_end; kb0 += 64) {
-    __syncthreads();  // previous block's images fully consumed (and the prologue staged)
-    f4 kreg[2], vreg[2];
-    stage_load<T>(k, kvrow0 + kb0, key_end - kb0, kvs, h * kD, kreg);
-    stage_load<T>(v, kvrow0 + kb0, key_end - kb0, kvs, h * kD, vreg);
-    stage_store<T>(Ks, kreg);
-    stage_store<T>(Vs, vreg);
-    for (int qi = threadIdx.x; qi < Lqp; qi += 256) {
+  // software pipeline: the next key block's K / V rows and mask words are loaded into registers while the
+  // current block is computed (one LDS image; it is rewritten after the barrier that ends its use)
+  constexpr int kMaxMwPerThread = 2;   // Lqp <= 512
+  f4 kreg[2], vreg[2];
+  uint32_t mreg[kMaxMwPerThread][2];
+  auto prefetch = [&](int kb) {
+    stage_load<T>(k, kvrow0 + kb, key_end - kb, kvs, h * kD, kreg);
+    stage_load<T>(v, kvrow0 + kb, key_end - kb, kvs, h * kD, vreg);
+#pragma unroll
+    for (int u = 0; u < kMaxMwPerThread; ++u) {
+      const int qi = threadIdx.x + 256 * u;
       uint32_t a0 = 0xffffffffu, a1 = 0xffffffffu;
       if (qi < Lq) {
-        const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + qi) * nw + (kb0 >> 5);
+        const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + qi) * nw + (kb >> 5);
         a0 = mr[0];
-        a1 = ((kb0 >> 5) + 1 < nw) ? mr[1] : 0xffffffffu;
+        a1 = ((kb >> 5) + 1 < nw) ? mr[1] : 0xffffffffu;
       }
-      mw[2 * qi] = a0;
-      mw[2 * qi + 1] = a1;
+      mreg[u][0] = a0;
+      mreg[u][1] = a1;
+    }
+  };
+  if (key_begin < key_end) prefetch(key_begin);
+  for (int kb0 = key_begin; kb0 < key_end; kb0 += 64) {
+    __syncthreads();  // previous block's images fully consumed (and the prologue staged)
+    stage_store<T>(Ks, kreg);
+    stage_store<T>(Vs, vreg);
+#pragma unroll
+    for (int u = 0; u < kMaxMwPerThread; ++u) {
+      const int qi = threadIdx.x + 256 * u;
+      if (qi < Lqp) {
+        mw[2 * qi] = mreg[u][0];
+        mw[2 * qi + 1] = mreg[u][1];
+      }
     }
     __syncthreads();
+    if (kb0 + 64 < key_end) prefetch(kb0 + 64);   // in flight during this block's MFMAs
     const int kvalid = key_end - kb0;
     const int koff = 16 * w + r;  // this lane's key (column) within the block
     if (16 * w >= kvalid) continue;  // whole tile beyond the chunk (wave-uniform); barriers are at loop top

@@ -361,8 +361,9 @@ extern "C" int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, 
 
 // ---------------------------------------------------------------------------------------------------
 // Achievable-HBM probe ("measure achievable peaks with a stream kernel"): out = in over
-// n16 16-byte vectors, grid-stride with a fixed grid of 8 workgroups per CU (256 CUs), nontemporal
-// loads and stores so neither pass is served from the 256 MB MALL.  Bytes moved = 32 * n16.
+// n16 16-byte vectors.  mode 0: one pass, each thread copies 4 vectors a block-width apart (plain loads and
+// stores, ~n16 / 1024 workgroups); mode 1: a fixed grid of 8 workgroups per CU striding over the buffer with
+// nontemporal loads and stores.  Bytes moved = 32 * n16.
 // ---------------------------------------------------------------------------------------------------
 namespace {
 
@@ -370,6 +371,20 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 __global__ void __launch_bounds__(256) stream_copy_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
                                                          int64_t n16) {
+  const int64_t i = blockIdx.x * 1024ll + threadIdx.x;
+  if (i + 768 < n16) {
+    const u32x4 a = in[i], b = in[i + 256], c = in[i + 512], d = in[i + 768];
+    out[i] = a;
+    out[i + 256] = b;
+    out[i + 512] = c;
+    out[i + 768] = d;
+  } else {
+    for (int64_t k = i; k < n16 && k < i + 1024; k += 256) out[k] = in[k];
+  }
+}
+
+__global__ void __launch_bounds__(256) stream_copy_nt_kernel(const u32x4* __restrict__ in, u32x4* __restrict__ out,
+                                                            int64_t n16) {
   const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
   int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
   for (; i + 3 * stride < n16; i += 4 * stride) {  // four independent 16-byte loads in flight per lane
@@ -387,15 +402,23 @@ __global__ void __launch_bounds__(256) stream_copy_kernel(const u32x4* __restric
 
 }  // namespace
 
-extern "C" int m2f_stream_copy(const void* in, void* out, int64_t nbytes, void* stream) {
+extern "C" int m2f_stream_copy(const void* in, void* out, int64_t nbytes, int mode, void* stream) {
   const char* fn = "m2f_stream_copy";
-  if (!in || !out || nbytes < 0) return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  if (!in || !out || nbytes < 0 || mode < 0 || mode > 1) return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
   if (nbytes % 16 || !m2f::aligned(in, 16) || !m2f::aligned(out, 16))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs 16-byte aligned buffers and nbytes %% 16 == 0", fn);
   const int64_t n16 = nbytes / 16;
   if (n16 == 0) return m2f::ok();
-  const unsigned grid = static_cast<unsigned>(std::min<int64_t>(2048, m2f::ceil_div(n16, 256)));
-  stream_copy_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(static_cast<const u32x4*>(in),
-                                                                          static_cast<u32x4*>(out), n16);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const u32x4* src = static_cast<const u32x4*>(in);
+  u32x4* dst = static_cast<u32x4*>(out);
+  if (mode == 0) {
+    const int64_t blocks = (n16 + 1023) / 1024;
+    if (blocks > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too large", fn);
+    stream_copy_kernel<<<static_cast<unsigned>(blocks), 256, 0, st>>>(src, dst, n16);
+  } else {
+    const unsigned grid = static_cast<unsigned>(std::min<int64_t>(2048, m2f::ceil_div(n16, 256)));
+    stream_copy_nt_kernel<<<grid, 256, 0, st>>>(src, dst, n16);
+  }
   return m2f::check_launch(fn);
 }

@@ -277,60 +277,62 @@ __global__ void __launch_bounds__(256) mask_row_fix_kernel(uint32_t* __restrict_
 // ---- backward --------------------------------------------------------------------------------------------
 // d embed = G F^T per head (G = d masks (B, Q, N), F = features (B, C, N), both N-contiguous).  Split over
 // N: grid (splits, B); each block computes the whole (Q padded to 32) x 256 partial of its N range into
-// part[b][split][q][c] (fp32, q < Q), summed in a fixed order by mask_de_reduce_kernel.  QH groups of 4 waves
-// (QH = 2 above 128 queries: config 4's Q = 200, mask2former_transformer_decoder.py:442); wave w: channels
-// 64 (w % 4) .. + 63 (two 32-tiles) x query tiles QT (w / 4) .. + QT - 1, so no wave holds more than four
-// query tiles of accumulators (128 VGPRs).  Per 32-deep k step the block's G slab (QH*QT*32 rows x 32) is
-// staged once in LDS (rows padded to 80 B: conflict-free 16-byte A reads) and shared by the waves; each
-// wave's F fragments (its own channels) load straight from global memory (the second query group's loads
-// of the same F rows hit the CU's L1/L2).  Two steps of global loads in flight in registers, LDS
-// double-buffered, one barrier per step.  HBM-bound.
-constexpr int kDeThreads = 256, kDeK = 32, kDePitch = kDeK + 8;
+// part[b][split][q][c] (fp32, q < Q), summed in a fixed order by mask_de_reduce_kernel.  8 waves; wave w:
+// channels 64 (w % 4) .. + 63 (two 32-tiles) x query tiles QT (w / 4) .. + QT - 1 (QT = 2 up to 128
+// queries, 4 up to 256: config 4's Q = 200, mask2former_transformer_decoder.py:442).  Per 64-deep k step both
+// operands are staged in LDS as rows of 64 k (144-B pitch: the 16-byte A and B fragment reads of a 16-lane
+// pass cover the 64 banks once): 8 consecutive lanes load one 128-byte row segment, so every global load
+// instruction reads whole lines (the former per-wave F fragment loads read 32-byte pieces of 32 rows and ran
+// the kernel at 3 TB/s).  One LDS image; the next step's loads are issued right after it is written and land
+// during the step's MFMAs.  HBM-bound: G and F are read once.
+constexpr int kDeThreads = 512, kDeK = 64, kDePitch = kDeK + 8;
 
-template <typename T, int QT, int QH>
-__global__ void __launch_bounds__(kDeThreads * QH, 2 / QH) mask_de_kernel(const T* __restrict__ G,
-                                                                          const T* __restrict__ F, int Q, int64_t N,
-                                                                          int64_t ks, int splits,
-                                                                          float* __restrict__ part) {
+template <typename T, int QT>
+__global__ void __launch_bounds__(kDeThreads, QT <= 2 ? 4 : 2) mask_de_kernel(const T* __restrict__ G,
+                                                                              const T* __restrict__ F, int Q,
+                                                                              int64_t N, int64_t ks, int splits,
+                                                                              float* __restrict__ part) {
   using E = MhElt<T>;
-  constexpr int C = 256, QP = 32 * QT * QH, NT = kDeThreads * QH;
-  constexpr int GP = QP * (kDeK / 8);                 // 16-byte G pieces per step
-  constexpr int GPT = (GP + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) T sg[2][QP * kDePitch];
+  constexpr int C = 256, QP = 64 * QT;                // queries staged (two groups of QT 32-tiles)
+  constexpr int GP = QP * (kDeK / 8), FP = C * (kDeK / 8);   // 16-byte pieces per step
+  constexpr int GPT = GP / kDeThreads, FPT = FP / kDeThreads;
+  __shared__ __attribute__((aligned(16))) T sg[QP * kDePitch];
+  __shared__ __attribute__((aligned(16))) T sf[C * kDePitch];
   const int s = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
   const int wc = w & 3, q0 = 32 * QT * (w >> 2);      // channel group, first query of this wave's tiles
   const int64_t k0 = s * ks, k1 = min(N, k0 + ks);
   const int nsteps = static_cast<int>((k1 - k0 + kDeK - 1) / kDeK);
   const T* gb = G + static_cast<int64_t>(b) * Q * N;
-  const T* f = F + static_cast<int64_t>(b) * C * N + static_cast<int64_t>(64 * wc + li) * N + lh * 8;
-  struct Stage {
-    s8 g[GPT];
-    s8 f[2][2];   // [c-tile][k16 half]
-  };
-  // past the range (the tail of the last split, or the steps past nsteps) pieces are zero: k1 is a multiple of 16
-  auto load = [&](Stage& st, int step) {
+  const T* fb = F + static_cast<int64_t>(b) * C * N;
+  s8 rg[GPT], rf[FPT];
+  // piece p: row p / 8, k 8 (p % 8): 8 consecutive lanes read one row's 128-byte segment.  Past k1 (the
+  // last split's tail; k1 is a multiple of 8) or past Q the pieces are zero
+  auto load = [&](int step) {
     const int64_t kb = k0 + static_cast<int64_t>(step) * kDeK;
 #pragma unroll
     for (int u = 0; u < GPT; ++u) {
-      const int p = tid + u * NT, row = p >> 2, kp = (p & 3) * 8;
-      st.g[u] = s8{0, 0, 0, 0, 0, 0, 0, 0};
-      if ((GP % NT == 0 || p < GP) && row < Q && kb + kp < k1)
-        st.g[u] = *reinterpret_cast<const s8*>(gb + static_cast<int64_t>(row) * N + kb + kp);
+      const int p = tid + u * kDeThreads, row = p >> 3, kp = (p & 7) * 8;
+      rg[u] = s8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (row < Q && kb + kp < k1) rg[u] = *reinterpret_cast<const s8*>(gb + static_cast<int64_t>(row) * N + kb + kp);
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        st.f[j][h] = s8{0, 0, 0, 0, 0, 0, 0, 0};
-        if (kb + 16 * h < k1) st.f[j][h] = *reinterpret_cast<const s8*>(f + static_cast<int64_t>(32 * j) * N + kb + 16 * h);
-      }
+    for (int u = 0; u < FPT; ++u) {
+      const int p = tid + u * kDeThreads, row = p >> 3, kp = (p & 7) * 8;
+      rf[u] = s8{0, 0, 0, 0, 0, 0, 0, 0};
+      if (kb + kp < k1) rf[u] = *reinterpret_cast<const s8*>(fb + static_cast<int64_t>(row) * N + kb + kp);
+    }
   };
-  auto gstore = [&](int buf, const Stage& st) {
+  auto store = [&]() {
 #pragma unroll
     for (int u = 0; u < GPT; ++u) {
-      const int p = tid + u * NT;
-      if (GP % NT == 0 || p < GP) *reinterpret_cast<s8*>(&sg[buf][(p >> 2) * kDePitch + (p & 3) * 8]) = st.g[u];
+      const int p = tid + u * kDeThreads;
+      *reinterpret_cast<s8*>(&sg[(p >> 3) * kDePitch + (p & 7) * 8]) = rg[u];
+    }
+#pragma unroll
+    for (int u = 0; u < FPT; ++u) {
+      const int p = tid + u * kDeThreads;
+      *reinterpret_cast<s8*>(&sf[(p >> 3) * kDePitch + (p & 7) * 8]) = rf[u];
     }
   };
   f16v acc[QT][2];
@@ -340,33 +342,25 @@ __global__ void __launch_bounds__(kDeThreads * QH, 2 / QH) mask_de_kernel(const 
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[qt][j][e] = 0.f;
-  auto compute = [&](int buf, const Stage& st) {
-    const T* base = &sg[buf][0];
+  if (nsteps > 0) load(0);
+  for (int t = 0; t < nsteps; ++t) {
+    __syncthreads();          // the previous step's fragment reads are done
+    store();
+    __syncthreads();
+    if (t + 1 < nsteps) load(t + 1);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int kk = 0; kk < kDeK / 16; ++kk) {
+      s8 bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bf[j] = *reinterpret_cast<const s8*>(&sf[(64 * wc + 32 * j + li) * kDePitch + 16 * kk + 8 * lh]);
 #pragma unroll
       for (int qt = 0; qt < QT; ++qt) {
-        const s8 a = *reinterpret_cast<const s8*>(base + (q0 + 32 * qt + li) * kDePitch + 16 * h + 8 * lh);
+        const s8 a = *reinterpret_cast<const s8*>(&sg[(q0 + 32 * qt + li) * kDePitch + 16 * kk + 8 * lh]);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[qt][j] = E::mma(a, st.f[j][h], acc[qt][j]);
+        for (int j = 0; j < 2; ++j) acc[qt][j] = E::mma(a, bf[j], acc[qt][j]);
       }
-  };
-  Stage s0, s1;
-  load(s0, 0);
-  load(s1, 1);
-  gstore(0, s0);
-  __syncthreads();
-  // step t: compute on buffer t & 1 with F fragments of stage t; stage t + 1 goes to the other buffer,
-  // stage t + 2 is loaded into the set stage t used (unrolled by 2: static sets)
-  auto stepf = [&](int t, Stage& cur, Stage& nxt) {
-    compute(t & 1, cur);
-    gstore((t + 1) & 1, nxt);
-    load(cur, t + 2);
-    __syncthreads();
-  };
-  for (int t = 0; t < nsteps; t += 2) {
-    stepf(t, s0, s1);
-    if (t + 1 < nsteps) stepf(t + 1, s1, s0);
+    }
   }
   // C map of 32x32x16: lane column li (c), rows (e & 3) + 8 (e >> 2) + 4 lh (q)
   float* out = part + (static_cast<int64_t>(b) * splits + s) * Q * C + 64 * wc + li;
@@ -562,11 +556,11 @@ extern "C" int m2f_mask_row_fix(uint32_t* bits, int rows, int nwords, int keys, 
 
 namespace {
 int64_t de_splits(int64_t N) {
-  // ~512 blocks at bs16 (two per CU), k ranges of whole 16-steps
+  // ~512 blocks at bs16 (two per CU), k ranges of whole 64-steps
   const int64_t target = 32;
   int64_t ks = (N + target - 1) / target;
-  ks = (ks + 15) / 16 * 16;
-  return ks < 16 ? 16 : ks;
+  ks = (ks + kDeK - 1) / kDeK * kDeK;
+  return ks < kDeK ? kDeK : ks;
 }
 
 template <typename T>
@@ -576,15 +570,15 @@ int launch_de(const void* G, const void* F, int B, int Q, int64_t N, float* part
   const dim3 grid(splits, B);
   const T* g = static_cast<const T*>(G);
   const T* f = static_cast<const T*>(F);
-  // up to 128 queries: one group of 4 waves holds every query tile; 129..256: two groups of up to 4 tiles
-  switch ((Q + 31) / 32) {
-#define M2F_DE(N_, QT, QH) \
-  case N_: mask_de_kernel<T, QT, QH><<<grid, kDeThreads * QH, 0, st>>>(g, f, Q, N, ks, splits, part); break;
-    M2F_DE(1, 1, 1) M2F_DE(2, 2, 1) M2F_DE(3, 3, 1) M2F_DE(4, 4, 1)
-    M2F_DE(5, 3, 2) M2F_DE(6, 3, 2) M2F_DE(7, 4, 2) M2F_DE(8, 4, 2)
-#undef M2F_DE
-    default: return m2f::fail(M2F_EUNSUPPORTED, "m2f_mask_heads_bwd_embed: %d queries (at most 256)", Q);
-  }
+  // two groups of 4 waves split the query tiles: QT = 1 (<= 64 queries), 2 (<= 128), 4 (<= 256)
+  if (Q <= 64)
+    mask_de_kernel<T, 1><<<grid, kDeThreads, 0, st>>>(g, f, Q, N, ks, splits, part);
+  else if (Q <= 128)
+    mask_de_kernel<T, 2><<<grid, kDeThreads, 0, st>>>(g, f, Q, N, ks, splits, part);
+  else if (Q <= 256)
+    mask_de_kernel<T, 4><<<grid, kDeThreads, 0, st>>>(g, f, Q, N, ks, splits, part);
+  else
+    return m2f::fail(M2F_EUNSUPPORTED, "m2f_mask_heads_bwd_embed: %d queries (at most 256)", Q);
   const int64_t per_b = static_cast<int64_t>(Q) * 256, total = per_b * B;
   mask_de_reduce_kernel<T><<<m2f::ceil_div(total, 256), 256, 0, st>>>(part, splits, per_b, total, static_cast<T*>(de));
   return M2F_OK;

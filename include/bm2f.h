@@ -312,8 +312,9 @@ int m2f_set_option(const char* name, int64_t value);
 int m2f_get_option(const char* name, int64_t* value);
 
 /* Achievable-HBM probe (BASELINE.md §4 asks for measured peaks beside the spec sheet's): out = in over
- * nbytes (16-byte aligned, nbytes % 16 == 0) with nontemporal 16-byte loads and stores; moves 2 * nbytes. */
-int m2f_stream_copy(const void* in, void* out, int64_t nbytes, void* stream);
+ * nbytes (16-byte aligned, nbytes % 16 == 0); moves 2 * nbytes.  mode 0: one pass of plain 16-byte loads and
+ * stores (4 per thread); mode 1: a fixed grid striding with nontemporal loads and stores. */
+int m2f_stream_copy(const void* in, void* out, int64_t nbytes, int mode, void* stream);
 
 /* Batched fp32 transpose out[b][q][r] = in[b][r][q] (row strides in_ld / out_ld, batch strides in_bs /
  * out_bs, in elements; B <= 65535): the pixel decoder's level flatten, cat([x_l.flatten(2).transpose(1, 2)],

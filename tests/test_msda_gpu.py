@@ -8,7 +8,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden, loc_crossing_mask
+from conftest import check_crossing_entries, golden, loc_crossing_mask
 from oracle import msda_ref
 
 pytestmark = pytest.mark.gpu
@@ -207,6 +207,8 @@ def _tiled_backward_case(device, tile, rows):
     amb = loc_crossing_mask(loc, shapes)
     assert amb.mean() < 2e-3
     _close(np.where(amb, 0.0, gl.cpu().numpy()), np.where(amb, 0.0, wl), atol_frac=1e-4)
+    check_crossing_entries(gl.cpu().numpy(), value.double(), shapes, lsi, loc.numpy(), attn.numpy(), gout.numpy(), amb,
+                           scale=np.abs(wl).max())
     # identical to the untiled kernel up to summation order
     with _native.options(msda_bwd_tiled=0):
         gv2, gl2, ga2 = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),

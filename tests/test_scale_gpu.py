@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import loc_crossing_mask
+from conftest import check_crossing_entries, loc_crossing_mask
 from oracle import msda_ref
 from oracle.decoder_ref import ref_masked_attention, unpack_bits
 
@@ -113,11 +113,18 @@ def test_fused_msda_config2_pyramid_vs_oracle(device, variant, far):
     ga = wa.reshape(N, S, M, L * P)
     d_logit = (a * (ga - (a * ga).sum(-1, keepdims=True))).reshape(N, S, M * L * P)
     gp = pj.grad.cpu().double().numpy()
-    # d loc is discontinuous at pixel-centre crossings: those entries are left out (conftest.loc_crossing_mask)
-    amb = loc_crossing_mask(loc.numpy(), shapes).reshape(N, S, -1)
+    # d loc is discontinuous at pixel-centre crossings: those entries are compared with the oracle's one-sided
+    # values on either side of the line (conftest.check_crossing_entries), the rest directly
+    amb_full = loc_crossing_mask(loc.numpy(), shapes)
+    amb = amb_full.reshape(N, S, -1)
     assert amb.mean() < 2e-3
     got_off = np.where(amb, 0.0, gp[..., :M * L * P * 2])
     _close(got_off, np.where(amb, 0.0, d_off), atol_frac=1e-4)
+    n_cross = check_crossing_entries(gp[..., :M * L * P * 2], value.double(), shapes, lsi, loc.numpy(), attn.numpy(),
+                                     gout.numpy(), amb_full,
+                                     to_cmp=lambda a: (a / norm).reshape(a.shape[0], a.shape[1], -1),
+                                     scale=np.abs(d_off).max())
+    assert n_cross == int(amb.sum())
     _close(gp[..., M * L * P * 2:], d_logit, atol_frac=1e-4)
 
 
@@ -298,6 +305,39 @@ def test_config5_video_decoder_full_size_vs_torch_ops(device):
     assert rel(gm0, gm1) < 1e-2
 
 
+def test_config4_decoder_full_size_vs_torch_ops(device):
+    """The image decoder at config 4's full per-rank size (2 images, Q=200, K=80, mask features 256x256, pyramid
+    32^2 / 64^2 / 128^2) in fp32 on the HIP ops against the same module on the torch restatements of the decoder
+    ops (oracle/decoder_ref.py, run on the GPU here): outputs and input gradients."""
+    from bm2f_amd.transformer_decoder import MultiScaleMaskedTransformerDecoder
+    from oracle.decoder_ref import torch_decoder_ops
+    torch.manual_seed(0)
+    dec = MultiScaleMaskedTransformerDecoder(256, True, num_classes=80, hidden_dim=256, num_queries=200, nheads=8,
+                                             dim_feedforward=2048, dec_layers=9, pre_norm=False, mask_dim=256,
+                                             enforce_input_project=False).to(device)
+    g = torch.Generator(device=device).manual_seed(9)
+    x0 = [torch.randn(2, 256, h, h, device=device, generator=g) for h in (32, 64, 128)]
+    mf0 = torch.randn(2, 256, 256, 256, device=device, generator=g)
+    res = []
+    for use_ref in (False, True):
+        x = [t.clone().requires_grad_() for t in x0]
+        mf = mf0.clone().requires_grad_()
+        with (torch_decoder_ops() if use_ref else contextlib.nullcontext()):
+            out = dec(x, mf)
+            heads = [out] + out["aux_outputs"]
+            loss = sum(h["pred_logits"].mean() + 0.5 * (h["pred_masks"] ** 2).mean() for h in heads)
+            loss.backward()
+        res.append((out["pred_masks"].detach(), out["pred_logits"].detach(), [t.grad for t in x], mf.grad))
+    (m0, l0, gx0, gm0), (m1, l1, gx1, gm1) = res
+    assert m0.shape == (2, 200, 256, 256) and l0.shape == (2, 200, 81)
+    rel = lambda a, b: ((a - b).abs().max() / b.abs().max()).item()  # noqa: E731
+    assert rel(m0, m1) < 1e-3 and rel(l0, l1) < 1e-3
+    # as config 5: a logit within fp32 rounding of the sigmoid threshold can flip one mask bit between the paths
+    for a, b in zip(gx0, gx1):
+        assert rel(a, b) < 1e-2
+    assert rel(gm0, gm1) < 1e-2
+
+
 # ------------------------------------------------------------------------------------------------------
 # DDP over RCCL with the custom autograd nodes
 # ------------------------------------------------------------------------------------------------------
@@ -356,3 +396,44 @@ def test_ddp_rccl_world1_matches_unwrapped(device, tmp_path):
         assert torch.equal(t, torch.full_like(t, 3.0))
     finally:
         dist.destroy_process_group()
+
+
+def test_op_level_dropin_untagged_shapes_config2(device):
+    """The reference's unchanged MSDeformAttn -> MSDeformAttnFunction.apply call (ops/modules/ms_deform_attn.py:
+    116-117): a device spatial_shapes without host shapes at the config-2 pyramid (N=2).  The forward reads the
+    shapes back once and tags the tensor, so the backward takes the tiled kernel (the bench's msda_op_dropin
+    times it); results against the C oracle, and against the untiled kernel."""
+    from bm2f_amd import _native, msda
+    shapes = SHAPES_1024
+    N, M, L, P = 2, 8, 3, 4
+    value, proj, ref = _fused_case(shapes, N, 0.0, seed=21)
+    loc, attn = _loc_attn(proj, ref, shapes)
+    S = value.shape[1]
+    gout = torch.randn(N, S, M * 32, generator=torch.Generator().manual_seed(8))
+    st = torch.tensor(shapes, dtype=torch.int64, device=device)       # untagged, as the reference's encoder
+    lsi = torch.tensor([0, 1024, 5120], dtype=torch.int64, device=device)
+    assert getattr(st, "_bm2f_host_shapes", None) is None
+    v = value.to(device).requires_grad_()
+    lc = loc.float().to(device).requires_grad_()
+    a = attn.float().to(device).requires_grad_()
+    out = msda.MSDeformAttnFunction.apply(v, st, lsi, lc, a, 64)
+    assert getattr(st, "_bm2f_host_shapes", None) == tuple(shapes)     # derived once in the forward
+    out.backward(gout.to(device))
+    stc = torch.tensor(shapes, dtype=torch.int64)
+    lsic = torch.tensor([0, 1024, 5120], dtype=torch.int64)
+    want = msda_ref.msda_forward(value.double(), stc, lsic, lc.detach().cpu().double(), a.detach().cpu().double())
+    _close(out.detach().cpu(), want)
+    wv, wl, wa = msda_ref.msda_backward(value.double(), stc, lsic, lc.detach().cpu().double(),
+                                        a.detach().cpu().double(), gout.double())
+    _close(v.grad.cpu(), wv)
+    _close(a.grad.cpu(), wa, atol_frac=1e-4)
+    amb = loc_crossing_mask(lc.detach().cpu().numpy(), shapes)
+    _close(np.where(amb, 0.0, lc.grad.cpu().numpy()), np.where(amb, 0.0, wl), atol_frac=1e-4)
+    check_crossing_entries(lc.grad.cpu().numpy(), value.double(), shapes, lsic, lc.detach().cpu().numpy(),
+                           a.detach().cpu().numpy(), gout.numpy(), amb, scale=np.abs(wl).max())
+    # the untiled kernel (no host shapes) agrees to summation order
+    with _native.options(msda_bwd_tiled=0):
+        gv2, gl2, ga2 = msda.ms_deform_attn_backward(v.detach(), st, lsi, lc.detach(), a.detach(),
+                                                    gout.to(device), 64)
+    torch.testing.assert_close(v.grad, gv2, rtol=1e-4, atol=1e-5 * gv2.abs().max().item())
+    torch.testing.assert_close(a.grad, ga2, rtol=1e-4, atol=1e-6 * ga2.abs().max().item())
