@@ -26,6 +26,7 @@ from .transformer_decoder import MultiScaleMaskedTransformerDecoder
 PIXEL_MEAN = (123.675, 116.280, 103.530)
 PIXEL_STD = (58.395, 57.120, 57.375)
 _CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}   # M2F_F32 / M2F_F16 / M2F_BF16
+CHANNELS_LAST = False   # run the benchmark backbone in channels_last memory (MIOpen's NHWC kernels, no transposes)
 
 
 class FrozenBNConv(nn.Module):
@@ -68,7 +69,8 @@ class _ScaledWeight(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, w, scale, dtype):
-        out = torch.empty(w.shape, dtype=dtype, device=w.device)
+        fmt = torch.channels_last if CHANNELS_LAST else torch.contiguous_format
+        out = torch.empty(w.shape, dtype=dtype, device=w.device, memory_format=fmt)
         torch.mul(w, scale.view(-1, 1, 1, 1), out=out)
         ctx.save_for_backward(scale)
         return out
@@ -76,7 +78,7 @@ class _ScaledWeight(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         (scale,) = ctx.saved_tensors
-        gw = torch.empty(grad.shape, dtype=torch.float32, device=grad.device)
+        gw = torch.empty(grad.shape, dtype=torch.float32, device=grad.device)   # the parameter's own layout
         torch.mul(grad, scale.view(-1, 1, 1, 1), out=gw)
         return gw, None, None
 
@@ -111,15 +113,19 @@ class _BiasAct(torch.autograd.Function):
         gs = [g for g in grads if g is not None]
         if len(gs) == 1:
             g = torch.ops.aten.threshold_backward(gs[0], y, 0)  # ReLU's own backward: one pass
-        elif (y.is_contiguous() and len(gs) <= 4 and y.numel() % 8 == 0 and y.data_ptr() % 16 == 0
-              and all(t.dtype == y.dtype and t.is_contiguous() and t.data_ptr() % 16 == 0 for t in gs)):
-            g = torch.empty_like(y, memory_format=torch.contiguous_format)
+        elif (len(gs) <= 4 and y.numel() % 8 == 0 and y.data_ptr() % 16 == 0 and _dense(y)
+              and all(t.dtype == y.dtype and t.stride() == y.stride() and t.data_ptr() % 16 == 0 for t in gs)):
+            g = torch.empty_like(y, memory_format=torch.preserve_format)   # elementwise: any dense layout
             ptrs = (ctypes.c_void_p * len(gs))(*[t.data_ptr() for t in gs])
             _native.call("m2f_relu_bwd_sum", ptrs, len(gs), y.data_ptr(), g.data_ptr(), y.numel(),
                          _CODE[y.dtype], torch.cuda.current_stream(y.device).cuda_stream)
         else:
             g = torch.ops.aten.threshold_backward(sum(gs), y, 0)
         return g, (g if ctx.has_r else None), None, None
+
+
+def _dense(t):
+    return t.is_contiguous() or t.is_contiguous(memory_format=torch.channels_last)
 
 
 def bias_act(x, bias, residual=None, nout=1):
@@ -277,6 +283,8 @@ class MaskFormerR50(nn.Module):
 
     def forward(self, images):
         x = (images - self.pixel_mean) / self.pixel_std
+        if CHANNELS_LAST:
+            x = x.contiguous(memory_format=torch.channels_last)
         return self.sem_seg_head(self.backbone(x))
 
 

@@ -87,8 +87,8 @@ def _derive_host_shapes(spatial_shapes: torch.Tensor, level_start_index: torch.T
     """Host shapes for a device ``spatial_shapes`` that arrived untagged -- the reference's unchanged
     ``MSDeformAttn.forward`` -> ``MSDeformAttnFunction.apply`` (ops/modules/ms_deform_attn.py:116-117) passes
     the encoder's device tensor as is.  One device->host copy per tensor object, cached on it (the encoder
-    hands the same tensor to all six layers, msdeformattn.py:75-83, and the backward restores the tag), so
-    the op-level drop-in takes the tiled backward too.  Returns None (untiled kernels, same results) when
+    hands the same tensor to all six layers, msdeformattn.py:75-83, and autograd hands the same Python object
+    back to the backward, tag included), so the op-level drop-in takes the tiled backward too.  Returns None (untiled kernels, same results) when
     the tensor cannot be read back here: during graph capture, or when ``level_start_index`` is not the
     prefix sum the tiled kernels assume."""
     if (spatial_shapes.dim() != 2 or spatial_shapes.shape[1] != 2 or spatial_shapes.dtype != torch.int64
@@ -170,7 +170,9 @@ def ms_deform_attn_forward(value, spatial_shapes, level_start_index, sampling_lo
         raise RuntimeError("spatial_shapes and level_start_index must be int64")
     N, S, M, D, L, Lq, P = _dims(value, spatial_shapes, sampling_loc)
     out = torch.empty((N, Lq, M * D), dtype=value.dtype, device=value.device)
-    host = _host_shape_buffer(_host_shapes(spatial_shapes, level_start_index))
+    # an untagged device spatial_shapes is read back once and tagged (the reference's own MSDeformAttnFunction
+    # saves this tensor object for its backward, where the tag then selects the tiled kernel)
+    host = _host_shape_buffer(_host_shapes(spatial_shapes, level_start_index, derive=True))
     _native.call(f"m2f_msda_fwd_{sfx}", _ptr(value), _ptr(spatial_shapes), _ptr(level_start_index),
                  _ptr(sampling_loc), _ptr(attn_weight), N, S, M, D, L, Lq, P, int(im2col_step),
                  ctypes.cast(host, ctypes.c_void_p) if host is not None else None, _ptr(out), _stream(value.device))
@@ -190,7 +192,7 @@ def ms_deform_attn_backward(value, spatial_shapes, level_start_index, sampling_l
     grad_value = torch.empty_like(value)
     grad_loc = torch.empty_like(sampling_loc)
     grad_attn = torch.empty_like(attn_weight)
-    host = _host_shape_buffer(_host_shapes(spatial_shapes, level_start_index))
+    host = _host_shape_buffer(_host_shapes(spatial_shapes, level_start_index, derive=True))
     _native.call(f"m2f_msda_bwd_{sfx}", _ptr(value), _ptr(spatial_shapes), _ptr(level_start_index),
                  _ptr(sampling_loc), _ptr(attn_weight), _ptr(grad_output), N, S, M, D, L, Lq, P, int(im2col_step),
                  ctypes.cast(host, ctypes.c_void_p) if host is not None else None,

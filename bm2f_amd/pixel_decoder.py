@@ -194,6 +194,30 @@ class MSDeformAttnTransformerEncoderOnly(nn.Module):
 
 
 @register(lambda: SEM_SEG_HEADS_REGISTRY)
+class _F32Contiguous(torch.autograd.Function):
+    """``x.float()`` as a contiguous NCHW tensor in one copy (a channels_last backbone output would otherwise be
+    cast, then transposed by the first conv), and the gradient handed back in x's dtype and memory layout in
+    one copy (so the backbone's gradient sums see one layout)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.dtype = x.dtype
+        ctx.cl = (x.dim() == 4 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last))
+        return x.to(dtype=torch.float32, memory_format=torch.contiguous_format)
+
+    @staticmethod
+    def backward(ctx, g):
+        fmt = torch.channels_last if ctx.cl else torch.contiguous_format
+        return g.to(dtype=ctx.dtype, memory_format=fmt)
+
+
+def _as_f32_nchw(x):
+    """The reference's ``features[f].float()`` (msdeformattn.py:320, 336), contiguous NCHW."""
+    if x.dtype == torch.float32 and x.is_contiguous():
+        return x
+    return _F32Contiguous.apply(x)
+
+
 class MSDeformAttnPixelDecoder(nn.Module):
     """Deformable-encoder pixel decoder (msdeformattn.py:164-358)."""
 
@@ -286,7 +310,7 @@ class MSDeformAttnPixelDecoder(nn.Module):
     def _forward_features(self, features):
         srcs, pos = [], []
         for idx, f in enumerate(self.transformer_in_features[::-1]):
-            x = features[f].float()
+            x = _as_f32_nchw(features[f])
             proj = self.input_proj[idx]
             srcs.append(group_norm_act(conv_ops.conv2d(x, proj[0]), proj[1]))   # 1x1 conv (x3) + GroupNorm
             pos.append(self.pe_layer(x))
@@ -298,7 +322,7 @@ class MSDeformAttnPixelDecoder(nn.Module):
         out = [z.transpose(1, 2).view(bs, -1, h, w) for z, (h, w) in zip(torch.split(y, sizes, dim=1), host_shapes)]
 
         for idx, f in enumerate(self.in_features[:self.num_fpn_levels][::-1]):
-            x = features[f].float()
+            x = _as_f32_nchw(features[f])
             cur_fpn = conv_ops.conv_norm_act(x, self.lateral_convs[idx])
             y = conv_ops.upsample_add(out[-1], cur_fpn)   # cur_fpn + bilinear resize of out[-1], one pass
             out.append(conv_ops.conv_norm_act(y, self.output_convs[idx]))
