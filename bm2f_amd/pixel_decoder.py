@@ -193,7 +193,6 @@ class MSDeformAttnTransformerEncoderOnly(nn.Module):
         return memory, spatial_shapes, level_start_index
 
 
-@register(lambda: SEM_SEG_HEADS_REGISTRY)
 class _F32Contiguous(torch.autograd.Function):
     """``x.float()`` as a contiguous NCHW tensor in one copy (a channels_last backbone output would otherwise be
     cast, then transposed by the first conv), and the gradient handed back in x's dtype and memory layout in
@@ -218,6 +217,7 @@ def _as_f32_nchw(x):
     return _F32Contiguous.apply(x)
 
 
+@register(lambda: SEM_SEG_HEADS_REGISTRY)
 class MSDeformAttnPixelDecoder(nn.Module):
     """Deformable-encoder pixel decoder (msdeformattn.py:164-358)."""
 
