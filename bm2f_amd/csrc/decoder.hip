@@ -429,8 +429,10 @@ __global__ void __launch_bounds__(256) mattn_combine_kernel(const float* __restr
 // the B operands of dV^T += dO^T P and dK^T += Q^T dS; dQ^T += K^T dS^T needs dS^T, transposed
 // through a per-wave 16x16 LDS scratch.  With NTR > 0 (Lq <= 16 * NTR) each wave keeps its dQ^T in
 // registers over the whole chunk and the four waves are summed through LDS once at the end; with
+// NTR == -1 (Lq <= 208: config 4's Q = 200) each wave adds its tiles' dQ^T into its own LDS copy with plain
+// read-modify-writes (no two waves touch one copy) and the four copies are summed at the end; with
 // NTR == 0 (more queries) each tile's dQ^T goes to LDS float atomics (~190 cycles per wave-instruction
-// on gfx950, the reason for the register path).  Chunks are summed by a reduce pass (deterministic).
+// on gfx950, the reason for the other two paths).  Chunks are summed by a reduce pass (deterministic).
 template <typename T, int NTR>
 __global__ void __launch_bounds__(256) mattn_bwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
@@ -490,6 +492,10 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
   f4 dqacc[NTR > 0 ? NTR : 1][2];
 #pragma unroll
   for (int qt = 0; qt < (NTR > 0 ? NTR : 1); ++qt) dqacc[qt][0] = dqacc[qt][1] = f4{0.f, 0.f, 0.f, 0.f};
+  float* dqw = dqa + (NTR < 0 ? w * Lqp * kD : 0);   // this wave's dQ copy (NTR == -1)
+  if constexpr (NTR < 0) {
+    for (int idx = threadIdx.x; idx < 3 * Lqp * kD; idx += 256) dqa[Lqp * kD + idx] = 0.f;   // copies 1..3
+  }
   // software pipeline: the next key block's K / V rows and mask words are loaded into registers while the
   // current block is computed (one LDS image; it is rewritten after the barrier that ends its use)
   constexpr int kMaxMwPerThread = 2;   // Lqp <= 512
@@ -634,10 +640,18 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
         f4 dqt[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
         tile(qt, dqt);
         // lane holds dQ^T[d = dt*16 + 4g + i][q = qt*16 + r]
+        if constexpr (NTR < 0) {
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
+          for (int dt = 0; dt < 2; ++dt) {
+            f4* dst = reinterpret_cast<f4*>(&dqw[(qt * 16 + r) * kD + dt * 16 + 4 * g]);
+            *dst = *dst + dqt[dt];
+          }
+        } else {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) atomicAdd(&dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i], dqt[dt][i]);
+          for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) atomicAdd(&dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i], dqt[dt][i]);
+        }
       }
     }
     // write dK, dV for this key tile: lane holds [d = dt*16 + 4g + i][key = koff]
@@ -680,7 +694,9 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
   const int BH = gridDim.x;
   for (int idx = threadIdx.x; idx < Lq * kD; idx += 256) {
     const int qi = idx / kD, d = idx % kD;
-    const float val = dqa[idx] * scale;
+    float sum = dqa[idx];
+    if constexpr (NTR < 0) sum = ((sum + dqa[Lqp * kD + idx]) + dqa[2 * Lqp * kD + idx]) + dqa[3 * Lqp * kD + idx];
+    const float val = sum * scale;
     if (nchunks == 1)
       dq[(static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + d] = Elt<T>::from_f(val);
     else
@@ -718,12 +734,12 @@ int plan_chunks(int B, int H, int Lk, int* chunk_len, int* nchunks) {
   return 0;
 }
 
-size_t bwd_lds_bytes(int Lqp, bool k16, int elt) {
+size_t bwd_lds_bytes(int Lqp, bool k16, int elt, int dq_copies = 1) {
   const int RS = k16 ? kDP : kD + 1;
   size_t bytes = static_cast<size_t>(2 * Lqp + 128) * RS * elt;
   bytes = (bytes + 15) & ~size_t(15);
   bytes += sizeof(float) * (2 * Lqp) + sizeof(uint32_t) * 2 * Lqp + sizeof(float) * 4 * 16 * 17 +
-           sizeof(float) * Lqp * kD;
+           sizeof(float) * Lqp * kD * dq_copies;
   return bytes;
 }
 
@@ -803,14 +819,17 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   const size_t need = nch > 1 ? sizeof(float) * static_cast<size_t>(nch) * B * H * Lq * kD : 0;
   if (ws_bytes < need || (need && !ws)) return m2f::fail(M2F_EINVAL, "%s: workspace %zu < %zu", fn, ws_bytes, need);
   const int Lqp = (Lq + 15) / 16 * 16;
-  const size_t lds = bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T));
-  if (lds > 160 * 1024) return m2f::fail(M2F_EUNSUPPORTED, "%s: %zu B of LDS", fn, lds);
-  // register dQ accumulation up to 128 queries (the decoders' 100 / 200-frame-shared cases use it)
+  // register dQ accumulation up to 128 queries (the decoders' Q = 100 case), per-wave LDS copies while four
+  // of them fit (config 4's Q = 200), else LDS atomics; option mattn_dq_atomic = 1 forces the atomics
   const bool reg_dq = m2f::option(m2f::kOptMattnDqAtomic, 0) != 1;
-  auto kern = (reg_dq && Lqp <= 128) ? &mattn_bwd_kernel<T, 8> : &mattn_bwd_kernel<T, 0>;
-  static bool attr_set[3][2] = {{false, false}, {false, false}, {false, false}};
+  const size_t lds_wave = bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T), 4);
+  const int mode = !reg_dq ? 0 : Lqp <= 128 ? 1 : lds_wave <= 160 * 1024 ? 2 : 0;
+  const size_t lds = mode == 2 ? lds_wave : bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T));
+  if (lds > 160 * 1024) return m2f::fail(M2F_EUNSUPPORTED, "%s: %zu B of LDS", fn, lds);
+  auto kern = mode == 1 ? &mattn_bwd_kernel<T, 8> : mode == 2 ? &mattn_bwd_kernel<T, -1> : &mattn_bwd_kernel<T, 0>;
+  static bool attr_set[3][3] = {{false, false, false}, {false, false, false}, {false, false, false}};
   const int ai = std::is_same<T, float>::value ? 0 : (std::is_same<T, __bf16>::value ? 1 : 2);
-  const int ki = kern == &mattn_bwd_kernel<T, 8> ? 1 : 0;
+  const int ki = mode;
   if (!attr_set[ai][ki]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               160 * 1024);

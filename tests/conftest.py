@@ -46,13 +46,14 @@ def loc_crossing_mask(loc, shapes, eps=1e-4):
 
 
 def check_crossing_entries(got, value, shapes, level_start_index, loc, attn, grad_out, amb, to_cmp=None,
-                           delta_px=3e-4, rtol=1e-3, atol_frac=1e-4, scale=None):
+                           delta_px=3e-4, rtol=1e-3, atol_frac=1e-4, scale=None, eps=1e-4):
     """Check the grad_loc entries ``loc_crossing_mask`` flags (where d loc jumps at a pixel-centre line) against
     the C oracle evaluated just on either side of the line: each such entry must match one side's value.
 
     d f / d x is piecewise constant in x across a bilinear cell and continuous across y lines (and vice
-    versa), so shifting every flagged coordinate by -delta and by +delta px gives the two one-sided
-    gradients of every flagged entry at once.  The oracle runs only on the queries that hold a flagged
+    versa), so shifting every coordinate that lies within ``eps`` of a line by -delta and by +delta px gives
+    the two one-sided gradients of every flagged entry at once (only those coordinates move: d f / d y
+    changes with x inside a cell, so moving a sample's other coordinate would shift its other entry).  The oracle runs only on the queries that hold a flagged
     sample (a sample's grad_loc depends on its own location alone).  ``to_cmp`` maps an oracle grad_loc
     array (n, q, M, L, P, 2) to the layout of ``got`` (e.g. d offsets = d loc / (W, H)); ``got`` is
     (N, Lq, ...) in that layout; ``scale`` (default: the largest one-sided value) is the atol reference, as
@@ -73,9 +74,11 @@ def check_crossing_entries(got, value, shapes, level_start_index, loc, attn, gra
             continue
         sub = loc[n:n + 1, qs]
         a_sub = amb[n:n + 1, qs].astype(np.float64)
+        pix = sub * wh - 0.5
+        near = (np.abs(pix - np.round(pix)) < eps).astype(np.float64)   # per coordinate
         sides = []
         for sign in (-1.0, 1.0):
-            shifted = sub + sign * a_sub * (delta_px / wh)
+            shifted = sub + sign * near * (delta_px / wh)
             _, gl, _ = msda_ref.msda_backward(torch.as_tensor(np.asarray(value[n:n + 1], dtype=np.float64)),
                                               shapes_tensor(shapes), level_start_index,
                                               torch.as_tensor(shifted),
