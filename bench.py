@@ -68,8 +68,6 @@ def parse_args(argv=None):
     ap.add_argument("--no-modes", action="store_true", help="skip the bf16 / fp32 mode lines")
     ap.add_argument("--no-peaks", action="store_true", help="skip the achievable-peak probes")
     ap.add_argument("--no-dropin", action="store_true", help="skip the op-level MSDeformAttnFunction timing")
-    ap.add_argument("--channels-last", type=int, default=None, choices=[0, 1],
-                    help="benchmark backbone memory layout (default: bench_model.CHANNELS_LAST)")
     ap.add_argument("--mode-steps", type=int, default=4)
     ap.add_argument("--kernel-steps", type=int, default=2, help="instrumented steps for roofline_all")
     ap.add_argument("--allow-knobs", action="store_true")
@@ -411,9 +409,6 @@ def main():
 
     timer = KernelTimer()
     timer.install(_native)
-    import bm2f_amd.bench_model as bm
-    if args.channels_last is not None:
-        bm.CHANNELS_LAST = bool(args.channels_last)
 
     torch.manual_seed(0)
     if args.config == 2:
@@ -535,7 +530,7 @@ def main():
                                    + (" with GradScaler" if args.amp == "fp16" else ""),
                        "model": "maskformer2_R50", "global_batch": world * args.batch,
                        "seq_len": sum((args.res // s) ** 2 for s in (32, 16, 8)), "queries": args.queries,
-                       "parallelism": f"dp{world}", "env": knobs, "backbone_channels_last": bm.CHANNELS_LAST},
+                       "parallelism": f"dp{world}", "env": knobs},
             "roofline": roof, "roofline_all": roof_all, "achievable": peaks, "modes": modes, "cpu_baseline": cpu,
             "msda_op_dropin": dropin,
         }

@@ -26,7 +26,6 @@ from .transformer_decoder import MultiScaleMaskedTransformerDecoder
 PIXEL_MEAN = (123.675, 116.280, 103.530)
 PIXEL_STD = (58.395, 57.120, 57.375)
 _CODE = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}   # M2F_F32 / M2F_F16 / M2F_BF16
-CHANNELS_LAST = False   # run the benchmark backbone in channels_last memory (MIOpen's NHWC kernels, no transposes)
 
 
 class FrozenBNConv(nn.Module):
@@ -69,8 +68,7 @@ class _ScaledWeight(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, w, scale, dtype):
-        fmt = torch.channels_last if CHANNELS_LAST else torch.contiguous_format
-        out = torch.empty(w.shape, dtype=dtype, device=w.device, memory_format=fmt)
+        out = torch.empty(w.shape, dtype=dtype, device=w.device)
         torch.mul(w, scale.view(-1, 1, 1, 1), out=out)
         ctx.save_for_backward(scale)
         return out
@@ -283,8 +281,6 @@ class MaskFormerR50(nn.Module):
 
     def forward(self, images):
         x = (images - self.pixel_mean) / self.pixel_std
-        if CHANNELS_LAST:
-            x = x.contiguous(memory_format=torch.channels_last)
         return self.sem_seg_head(self.backbone(x))
 
 
