@@ -397,13 +397,11 @@ __global__ void __launch_bounds__(256) mask_de_reduce_kernel(const float* __rest
 // d features = sum over heads h of E_h^T G_h, one pass over the heads' G (no concatenation):
 // df[b, c, n] = sum_{h, q} Et[b, c, h * QP + q] G_h[b, q, n], Et the embeds transposed and zero-padded to QP
 // (a multiple of 16) queries per head.  Block = (image, 128 columns of n), 4 waves, wave w: channels
-// 64 w .. 64 w + 63 (two 32-tiles) x the four 32-column tiles.  A stage is four 16-query k-steps (each within
-// one head): its 64 G rows x 128 columns (16 KB) are loaded as whole 256-byte row segments (16 consecutive
-// lanes per row) one stage ahead in registers and written to one of two LDS images (rows padded to 320 B: the
-// transposed ds_read_b64_tr_b16 of the B operand is conflict-free); the A fragments (Et rows, L2-resident)
-// load straight from global memory.  One barrier per stage (the former one-k-step stages moved 4 KB per
-// barrier and ran at 2.4 TB/s).  fp32 accumulation, one rounding to O.
-constexpr int kDfCols = 128, kDfPitch = kDfCols + 32, kDfMaxHeads = 16, kDfStage = 4;   // k16 steps per stage
+// 64 w .. 64 w + 63 (two 32-tiles) x the four 32-column tiles.  Per k-step (16 queries of one head) the G
+// rows are staged in LDS (rows padded to 320 B: the transposed ds_read_b64_tr_b16 of the B operand is
+// conflict-free), double-buffered with the next two steps' global loads in registers; the A fragments
+// (Et rows, L2-resident) load straight from global memory.  fp32 accumulation, one rounding to T.
+constexpr int kDfCols = 128, kDfPitch = kDfCols + 32, kDfMaxHeads = 16;
 
 struct DfHeads {
   const void* g[kDfMaxHeads];
@@ -415,37 +413,25 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
   using E = MhElt<T>;
   constexpr int C = 256;
   constexpr int EPP = 16 / static_cast<int>(sizeof(O));       // output elements per 16-byte piece
-  constexpr int ROWS = 16 * kDfStage;                         // G rows per stage
-  constexpr int PPT = ROWS * (kDfCols / 8) / 256;             // 16-byte pieces per thread per stage
-  __shared__ __attribute__((aligned(16))) T sg[2][ROWS * kDfPitch];
+  __shared__ __attribute__((aligned(16))) T sg[2][16 * kDfPitch];
   __shared__ __attribute__((aligned(16))) O so[4][32][32 + EPP];
   const int cc = blockIdx.x % ncol, b = blockIdx.x / ncol;
   const int64_t n0 = static_cast<int64_t>(cc) * kDfCols;
   const int cw = static_cast<int>(min<int64_t>(kDfCols, N - n0));
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
   const int KP = H * QP, nsteps = KP / 16, spq = QP / 16;
-  const int nstages = (nsteps + kDfStage - 1) / kDfStage;
-  // staging: piece p = tid + 256 u -> stage row p >> 4 (k16 step (p >> 4) / 16 of the stage), 8 columns
-  // (p & 15) * 8: 16 consecutive lanes read one row's 256-byte segment
-  auto gload = [&](int stg, s8 (&v)[PPT]) {
-#pragma unroll
-    for (int u = 0; u < PPT; ++u) {
-      const int p = tid + 256 * u, row = p >> 4, col = (p & 15) * 8;
-      const int st = stg * kDfStage + (row >> 4);
-      const int h = st / spq, q = (st - h * spq) * 16 + (row & 15);
-      v[u] = s8{0, 0, 0, 0, 0, 0, 0, 0};
-      if (col < cw && st < nsteps && q < Q)
-        v[u] = *reinterpret_cast<const s8*>(static_cast<const T*>(heads.g[h]) + (static_cast<int64_t>(b) * Q + q) * N +
-                                            n0 + col);
-    }
+  // staging: thread -> (k row tid >> 4, 8 columns (tid & 15) * 8) of the step's 16 x 128 G slab
+  const int sr = tid >> 4, scol = (tid & 15) * 8;
+  const bool cok = scol < cw;
+  auto gload = [&](int st) -> s8 {
+    s8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int h = st / spq, q = (st - h * spq) * 16 + sr;
+    if (cok && q < Q && st < nsteps)
+      v = *reinterpret_cast<const s8*>(static_cast<const T*>(heads.g[h]) + (static_cast<int64_t>(b) * Q + q) * N +
+                                       n0 + scol);
+    return v;
   };
-  auto gstore = [&](int buf, const s8 (&v)[PPT]) {
-#pragma unroll
-    for (int u = 0; u < PPT; ++u) {
-      const int p = tid + 256 * u;
-      *reinterpret_cast<s8*>(&sg[buf][(p >> 4) * kDfPitch + (p & 15) * 8]) = v[u];
-    }
-  };
+  auto gstore = [&](int buf, s8 v) { *reinterpret_cast<s8*>(&sg[buf][sr * kDfPitch + scol]) = v; };
   const T* et = Et + (static_cast<int64_t>(b) * C + 64 * w + li) * KP + lh * 8;
   f16v acc[2][4];
 #pragma unroll
@@ -455,35 +441,27 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][t][e] = 0.f;
   const int gq = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-  s8 rv[PPT];
-  gload(0, rv);
-  gstore(0, rv);
-  if (nstages > 1) gload(1, rv);
+  s8 r0 = gload(0), r1 = gload(1);
+  gstore(0, r0);
   __syncthreads();
-  for (int stg = 0; stg < nstages; ++stg) {
-    const int buf = stg & 1;
+  for (int st = 0; st < nsteps; ++st) {
+    const int buf = st & 1;
+    const s8 r2 = gload(st + 2);  // steps st + 1 (r1) and st + 2 (r2) in flight
+    s8 af[2];
 #pragma unroll
-    for (int ks = 0; ks < kDfStage; ++ks) {
-      const int st = stg * kDfStage + ks;
-      if (st >= nsteps) break;   // block-uniform
-      s8 af[2];
+    for (int j = 0; j < 2; ++j) af[j] = *reinterpret_cast<const s8*>(et + static_cast<int64_t>(32 * j) * KP + st * 16);
+    const T* base = &sg[buf][0];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) af[j] = *reinterpret_cast<const s8*>(et + static_cast<int64_t>(32 * j) * KP + st * 16);
-      const T* base = &sg[buf][16 * ks * kDfPitch];
+    for (int t = 0; t < 4; ++t) {
+      const int col = 32 * t + 16 * (gq & 1) + 4 * pp;
+      const s4 lo = tr_read(base + (8 * lh + qq) * kDfPitch + col);
+      const s4 hi = tr_read(base + (8 * lh + 4 + qq) * kDfPitch + col);
+      const s8 bf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        const int col = 32 * t + 16 * (gq & 1) + 4 * pp;
-        const s4 lo = tr_read(base + (8 * lh + qq) * kDfPitch + col);
-        const s4 hi = tr_read(base + (8 * lh + 4 + qq) * kDfPitch + col);
-        const s8 bf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[j][t] = E::mma(af[j], bf, acc[j][t]);
-      }
+      for (int j = 0; j < 2; ++j) acc[j][t] = E::mma(af[j], bf, acc[j][t]);
     }
-    if (stg + 1 < nstages) {
-      gstore(buf ^ 1, rv);                     // stage stg + 1, loaded during stage stg's MFMAs
-      if (stg + 2 < nstages) gload(stg + 2, rv);
-    }
+    gstore(buf ^ 1, r1);
+    r1 = r2;
     __syncthreads();
   }
   // epilogue: per 32x32 tile through the wave's LDS image, 16-byte stores (one rounding to O)

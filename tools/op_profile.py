@@ -18,7 +18,7 @@ use_shipped_find_db()
 import torch  # noqa: E402
 from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
-from bm2f_amd.bench_model import MaskFormerR50, make_optimizer, train_step  # noqa: E402
+from bm2f_amd.bench_model import MaskFormerR50, make_optimizer, make_scaler, train_step  # noqa: E402
 
 
 def attribute(trace_path, rows):
@@ -73,6 +73,7 @@ def main():
     ap.add_argument("--res", type=int, default=1024)
     ap.add_argument("--rows", type=int, default=45)
     ap.add_argument("--part", default="all")
+    ap.add_argument("--amp", default="fp16", choices=["fp16", "bf16"])
     ap.add_argument("--attribute", action="store_true")
     ap.add_argument("--shapes", default="", help="print input shapes of aten ops whose name contains this")
     a = ap.parse_args()
@@ -89,8 +90,11 @@ def main():
             mf, o0, ms = model.pixel_decoder.forward_features(feats)
             (mf.mean() + sum(t.mean() for t in ms)).backward()
     else:
+        amp = torch.float16 if a.amp == "fp16" else torch.bfloat16
+        scaler = make_scaler(amp)
+
         def step():
-            train_step(model, opt, x, torch.bfloat16)
+            train_step(model, opt, x, amp, scaler=scaler)
     for _ in range(2):
         step()
     torch.cuda.synchronize()
