@@ -129,7 +129,8 @@ def _msda_bytes(a, fused, bwd):
     attn = N * Lq * M * L * P * 4
     out = N * Lq * M * D * 4
     fwd_b = value + loc + attn + out
-    return (fwd_b + value + loc + attn if bwd else fwd_b), 0
+    gather = N * Lq * M * L * P * 4 * D * 4       # four corner rows of D fp32 per sample, through L1 / L2
+    return (fwd_b + value + loc + attn if bwd else fwd_b), 0, gather
 
 
 def _x3(M, N, K):
@@ -195,8 +196,10 @@ class KernelTimer:
             s.record()
             out = fn(name, *args)
             e.record()
-            nbytes, flops = ent[2](args)
-            timer.events.setdefault(ent[0], []).append((s, e, nbytes, flops))
+            work = ent[2](args)
+            nbytes, flops = work[0], work[1]
+            gather = work[2] if len(work) > 2 else 0
+            timer.events.setdefault(ent[0], []).append((s, e, nbytes, flops, gather))
             return out
 
         native.call = wrapped
@@ -206,12 +209,13 @@ class KernelTimer:
         torch.cuda.synchronize()
         res = {}
         for fam, evs in self.events.items():
-            ms = [s.elapsed_time(e) for s, e, _, _ in evs]
-            nb = sum(b for _, _, b, _ in evs)
-            fl = sum(f for _, _, _, f in evs)
+            ms = [ev[0].elapsed_time(ev[1]) for ev in evs]
+            nb = sum(ev[2] for ev in evs)
+            fl = sum(ev[3] for ev in evs)
+            ga = sum(ev[4] for ev in evs)
             tot = sum(ms)
             res[fam] = {"calls_per_step": len(ms) / steps, "mean_ms": tot / len(ms), "ms_per_step": tot / steps,
-                        "bytes": nb, "flops": fl, "total_ms": tot}
+                        "bytes": nb, "flops": fl, "gather_bytes": ga, "total_ms": tot}
         return res
 
 
@@ -225,6 +229,10 @@ def roofline_entry(fam, k, bound):
         if k["flops"] and fam in MFMA_NOTE:
             ent["mfma_tflops"] = round(k["flops"] / t / 1e12, 1)
             ent["note"] = MFMA_NOTE[fam]
+        if k.get("gather_bytes"):
+            ent["gather_gbs"] = round(k["gather_bytes"] / t / 1e9, 1)
+            ent["gather_note"] = ("corner-row gathers (4 x 128 B per sample) through L1 / L2: the bound that binds "
+                                  "(compare achievable.l2_gather_gbs)")
         return ent
     if fam.startswith("x3"):
         ach = 6 * k["flops"] / t / 1e12
@@ -269,7 +277,17 @@ def measure_peaks(device):
     del x, y, out
     torch.cuda.empty_cache()
     rates = {mode: 2 * nbytes / t / 1e9 for mode, t in t_copy.items()}
+    # L2-resident gather of 128-byte rows from one head's value rows of one 1024^2 image (2.75 MB)
+    rows, ng = 21504, 1 << 26
+    table = torch.randn(rows, 32, device=device)
+    sink = torch.empty(2048 * 256, device=device)
+    t_g = timed(lambda: _native.call("m2f_gather_probe", table.data_ptr(), rows, ng, sink.data_ptr(), sink.numel(),
+                                     st.cuda_stream), 10)
+    del table, sink
     return {"hbm_gbs": round(max(rates.values()), 1), "bf16_gemm_tflops": round(2 * n ** 3 / t_mm / 1e12, 1),
+            "l2_gather_gbs": round(128 * ng / t_g / 1e9, 1),
+            "gather_probe": "m2f_gather_probe: 2^26 pseudo-random 128-B rows of a 2.75 MB table (one head's value rows "
+                            "of a 1024^2 image, L2-resident), 8 lanes x float4 per row, 4 rows in flight, mean of 10",
             "hbm_probe": "m2f_stream_copy, 2 GiB in + 2 GiB out per launch, mean of 20, the faster of a one-pass "
                          f"float4 copy ({rates[0]:.0f} GB/s) and a strided nontemporal one ({rates[1]:.0f} GB/s)",
             "mfma_probe": f"torch.matmul bf16 {n}x{n}x{n} (hipBLASLt), mean of 20"}
@@ -281,6 +299,8 @@ def add_achievable(ent, peaks):
     key = "hbm_gbs" if ent.get("unit") == "GB/s" else "bf16_gemm_tflops"
     ent["achievable_peak"] = peaks[key]
     ent["frac_achievable"] = round(ent["achieved"] / peaks[key], 4)
+    if "gather_gbs" in ent and peaks.get("l2_gather_gbs"):
+        ent["frac_gather"] = round(ent["gather_gbs"] / peaks["l2_gather_gbs"], 4)
     return ent
 
 
@@ -501,6 +521,8 @@ def main():
                     "traffic": (tr or {}).get("hbm_bytes_per_launch") if tr else None,
                     "kernel": "MSDA backward (m2f_msda_fused_bwd_f32)",
                     "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(bwd["mean_ms"], 4)}
+            if bwd.get("gather_bytes"):
+                roof["gather_gbs"] = round(bwd["gather_bytes"] / (bwd["total_ms"] * 1e-3) / 1e9, 1)
             add_achievable(roof, peaks)
         bounds = {v[0]: v[1] for v in ENTRIES.values()}
         roof_all = [add_achievable(roofline_entry(fam, k, bounds[fam]), peaks)

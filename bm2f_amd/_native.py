@@ -62,6 +62,7 @@ _SIGNATURES = {
     "m2f_maxpool3s2_fwd": [_p, _p, _p, _l, _i, _i, _i, _p],
     "m2f_maxpool3s2_bwd": [_p, _p, _p, _l, _i, _i, _i, _p],
     "m2f_stream_copy": [_p, _p, _l, _i, _p],
+    "m2f_gather_probe": [_p, _i, _l, _p, _i, _p],
     "m2f_set_option": [ctypes.c_char_p, _l],
     "m2f_get_option": [ctypes.c_char_p, _p],
     "m2f_transpose_f32": [_p, _l, _l, _p, _l, _l, _i, _i, _i, _p],

@@ -249,10 +249,27 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
   }
 
   f4 kreg[2], vreg[2];
+  // this lane's mask words of a 64-key block (query row qi of tile t), loaded one block ahead with K / V
+  uint32_t mw[TPW][2];
+  auto mload = [&](int kb) {
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      uint32_t a0 = 0xffffffffu, a1 = 0xffffffffu;
+      if (mrow_ok[t]) {
+        const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + (w + 4 * t) * 16 + r) * nw + (kb >> 5);
+        a0 = mr[0];
+        a1 = ((kb >> 5) + 1 < nw) ? mr[1] : 0xffffffffu;
+      }
+      mw[t][0] = a0;
+      mw[t][1] = a1;
+    }
+  };
+  uint32_t mcur[TPW][2];
   int buf = 0;
   if (key_begin < key_end) {
     stage_load<T>(k, kvrow0 + key_begin, key_end - key_begin, kvs, h * kD, kreg);
     stage_load<T>(v, kvrow0 + key_begin, key_end - key_begin, kvs, h * kD, vreg);
+    mload(key_begin);
     stage_store<T>(Ks[0], kreg);
     stage_store<T>(Vs[0], vreg);
   }
@@ -260,9 +277,12 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
 
   for (int kb0 = key_begin; kb0 < key_end; kb0 += 64) {
     const int next = kb0 + 64;
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) { mcur[t][0] = mw[t][0]; mcur[t][1] = mw[t][1]; }
     if (next < key_end) {  // prefetch the next block into registers
       stage_load<T>(k, kvrow0 + next, key_end - next, kvs, h * kD, kreg);
       stage_load<T>(v, kvrow0 + next, key_end - next, kvs, h * kD, vreg);
+      mload(next);
     }
     const T* Kc = Ks[buf];
     const T* Vc = Vs[buf];
@@ -270,13 +290,7 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
       if ((w + 4 * t) * 16 >= Lq) continue;  // wave-uniform
-      const int qi = (w + 4 * t) * 16 + r;
-      uint32_t w0 = 0xffffffffu, w1 = 0xffffffffu;
-      if (mrow_ok[t]) {
-        const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + qi) * nw + (kb0 >> 5);
-        w0 = mr[0];
-        w1 = ((kb0 >> 5) + 1 < nw) ? mr[1] : 0xffffffffu;
-      }
+      const uint32_t w0 = mcur[t][0], w1 = mcur[t][1];
       f4 st[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {

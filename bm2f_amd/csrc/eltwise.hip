@@ -422,3 +422,55 @@ extern "C" int m2f_stream_copy(const void* in, void* out, int64_t nbytes, int mo
   }
   return m2f::check_launch(fn);
 }
+
+// ---------------------------------------------------------------------------------------------------
+// Achievable-gather probe: the MSDA kernels' binding path is the L2-resident gather of 128-byte value rows
+// (one head's rows of one image, 2.75 MB at 1024^2, stay in an XCD's 4 MB L2), not HBM.  An 8-lane group
+// reads one pseudo-random 128-byte row of `table` (rows x 32 floats) per step, as the MSDA kernels' groups
+// read a sample's corner rows (a float4 per lane), four rows in flight per lane; n rows in total.  Row ids are
+// hashed from the step index (no index traffic).  Gathered bytes = 128 * n; out gets one float per lane.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+__device__ __forceinline__ uint32_t probe_hash(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  return static_cast<uint32_t>(x);
+}
+
+__global__ void __launch_bounds__(256) gather_probe_kernel(const float4* __restrict__ table, uint32_t rows,
+                                                          int64_t n, float* __restrict__ out) {
+  const int64_t gid = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  const int64_t groups = static_cast<int64_t>(gridDim.x) * blockDim.x / 8;
+  const int j = threadIdx.x & 7;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int64_t i = gid >> 3;
+  for (; i + 3 * groups < n; i += 4 * groups) {
+    const float4 a = table[static_cast<int64_t>(probe_hash(i) % rows) * 8 + j];
+    const float4 b = table[static_cast<int64_t>(probe_hash(i + groups) % rows) * 8 + j];
+    const float4 c = table[static_cast<int64_t>(probe_hash(i + 2 * groups) % rows) * 8 + j];
+    const float4 d = table[static_cast<int64_t>(probe_hash(i + 3 * groups) % rows) * 8 + j];
+    acc.x += (a.x + b.x) + (c.x + d.x);
+    acc.y += (a.y + b.y) + (c.y + d.y);
+    acc.z += (a.z + b.z) + (c.z + d.z);
+    acc.w += (a.w + b.w) + (c.w + d.w);
+  }
+  for (; i < n; i += groups) {
+    const float4 a = table[static_cast<int64_t>(probe_hash(i) % rows) * 8 + j];
+    acc.x += a.x; acc.y += a.y; acc.z += a.z; acc.w += a.w;
+  }
+  out[gid] = (acc.x + acc.y) + (acc.z + acc.w);
+}
+
+}  // namespace
+
+extern "C" int m2f_gather_probe(const float* table, int rows, int64_t n, float* out, int out_len, void* stream) {
+  const char* fn = "m2f_gather_probe";
+  if (!table || !out || rows <= 0 || n < 0 || !m2f::aligned(table, 16)) return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  const int grid = 2048;   // 8 workgroups of 4 waves per CU
+  if (out_len < grid * 256) return m2f::fail(M2F_EINVAL, "%s: out needs %d floats", fn, grid * 256);
+  gather_probe_kernel<<<grid, 256, 0, static_cast<hipStream_t>(stream)>>>(reinterpret_cast<const float4*>(table),
+                                                                          static_cast<uint32_t>(rows), n, out);
+  return m2f::check_launch(fn);
+}

@@ -400,7 +400,8 @@ __global__ void __launch_bounds__(256) mask_de_reduce_kernel(const float* __rest
 // 64 w .. 64 w + 63 (two 32-tiles) x the four 32-column tiles.  Per k-step (16 queries of one head) the G
 // rows are staged in LDS (rows padded to 320 B: the transposed ds_read_b64_tr_b16 of the B operand is
 // conflict-free), double-buffered with the next two steps' global loads in registers; the A fragments
-// (Et rows, L2-resident) load straight from global memory.  fp32 accumulation, one rounding to T.
+// (Et rows, L2-resident) load straight from global memory two steps ahead (loaded at their step they left
+// every step waiting out an L2 round trip: 1.32 -> see DESIGN.md §3).  fp32 accumulation, one rounding to T.
 constexpr int kDfCols = 128, kDfPitch = kDfCols + 32, kDfMaxHeads = 16;
 
 struct DfHeads {
@@ -441,15 +442,25 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][t][e] = 0.f;
   const int gq = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  // A fragments of step st (clamped to the last step past the end: loaded, never used)
+  auto aload = [&](int st, s8 (&af)[2]) {
+    const int sc = min(st, nsteps - 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) af[j] = *reinterpret_cast<const s8*>(et + static_cast<int64_t>(32 * j) * KP + sc * 16);
+  };
   s8 r0 = gload(0), r1 = gload(1);
+  s8 a_cur[2], a_n1[2], a_n2[2];
+  aload(0, a_cur);
+  aload(1, a_n1);
   gstore(0, r0);
   __syncthreads();
   for (int st = 0; st < nsteps; ++st) {
     const int buf = st & 1;
     const s8 r2 = gload(st + 2);  // steps st + 1 (r1) and st + 2 (r2) in flight
-    s8 af[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) af[j] = *reinterpret_cast<const s8*>(et + static_cast<int64_t>(32 * j) * KP + st * 16);
+    aload(st + 2, a_n2);          // A fragments two steps ahead
+    s8 af[2] = {a_cur[0], a_cur[1]};
+    a_cur[0] = a_n1[0]; a_cur[1] = a_n1[1];
+    a_n1[0] = a_n2[0]; a_n1[1] = a_n2[1];
     const T* base = &sg[buf][0];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {

@@ -316,6 +316,11 @@ int m2f_get_option(const char* name, int64_t* value);
  * stores (4 per thread); mode 1: a fixed grid striding with nontemporal loads and stores. */
 int m2f_stream_copy(const void* in, void* out, int64_t nbytes, int mode, void* stream);
 
+/* Achievable L2-gather probe (the MSDA kernels' binding path): n pseudo-random 128-byte rows of `table`
+ * (rows x 32 floats, 16-byte aligned) gathered by 8-lane groups, a float4 per lane, four rows in flight;
+ * out receives 2048 * 256 floats (out_len >= that).  Gathered bytes = 128 * n. */
+int m2f_gather_probe(const float* table, int rows, int64_t n, float* out, int out_len, void* stream);
+
 /* Batched fp32 transpose out[b][q][r] = in[b][r][q] (row strides in_ld / out_ld, batch strides in_bs /
  * out_bs, in elements; B <= 65535): the pixel decoder's level flatten, cat([x_l.flatten(2).transpose(1, 2)],
  * 1) (msdeformattn.py:64-74), and its backward. */
