@@ -18,6 +18,7 @@ import ctypes
 import math
 
 import torch
+from torch import nn
 from torch.autograd import Function
 from torch.nn import functional as F
 
@@ -484,3 +485,73 @@ def token_linear(x, weight, bias=None, x_lp=None):
         return F.linear(x, weight, bias)
     with torch.autocast("cuda", enabled=False):
         return _TokenLinear.apply(x, weight, bias)
+
+
+# ------------------------------------------------------------------------------------------------------
+# the decoder's GEMM weights cast to the autocast dtype once per forward, in a few kernels
+# ------------------------------------------------------------------------------------------------------
+class _FlatCast(Function):
+    """Cast a list of parameters to ``dtype`` as views of one flat buffer (a cat and one cast, instead of one
+    autocast copy kernel per weight and use), and their gradients back to the parameters' dtype the same way
+    (instead of one ToCopyBackward per weight).  The values are those of autocast's per-call ``.to(dtype)``
+    and of its backward cast."""
+
+    @staticmethod
+    def forward(ctx, dtype, *params):
+        ctx.shapes = [p.shape for p in params]
+        ctx.numels = [p.numel() for p in params]
+        ctx.src_dtype = params[0].dtype
+        flat = torch.cat([p.detach().reshape(-1) for p in params]).to(dtype)
+        return tuple(o.view(sh) for o, sh in zip(flat.split(ctx.numels), ctx.shapes))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        ref = next((g for g in grads if g is not None), None)
+        if ref is None:
+            return (None,) * (len(grads) + 1)
+        parts = [(g if g is not None else ref.new_zeros(sh)).reshape(-1) for g, sh in zip(grads, ctx.shapes)]
+        flat = torch.cat(parts).to(ctx.src_dtype)
+        return (None,) + tuple(o.view(sh) for o, sh in zip(flat.split(ctx.numels), ctx.shapes))
+
+
+_LOWP_ACTIVE = "_bm2f_lowp_active"
+
+
+def lowp_params(module):
+    """{name: low-precision view} for the GEMM parameters of ``module`` (nn.Linear weights / biases and
+    nn.MultiheadAttention in-projections) when its forward runs under CUDA autocast in fp16 / bf16, else None.
+    LayerNorm, embedding and other parameters keep their fp32 tensors (autocast runs those ops in fp32)."""
+    if getattr(module, _LOWP_ACTIVE, False) or not torch.is_autocast_enabled("cuda"):
+        return None
+    dt = torch.get_autocast_dtype("cuda")
+    if dt not in (torch.float16, torch.bfloat16):
+        return None
+    names, params = [], []
+    for mname, mod in module.named_modules():
+        pre = f"{mname}." if mname else ""
+        if isinstance(mod, nn.Linear):
+            cand = [("weight", mod.weight), ("bias", mod.bias)]
+        elif isinstance(mod, nn.MultiheadAttention) and mod._qkv_same_embed_dim:
+            cand = [("in_proj_weight", mod.in_proj_weight), ("in_proj_bias", mod.in_proj_bias)]
+        else:
+            continue
+        for pn, p in cand:
+            if p is not None and p.is_cuda and p.dtype == torch.float32:
+                names.append(pre + pn)
+                params.append(p)
+    if not params:
+        return None
+    return dict(zip(names, _FlatCast.apply(dt, *params)))
+
+
+def call_with_lowp_params(module, args):
+    """``module(*args)`` with its GEMM parameters swapped for one batched low-precision cast (see
+    :func:`lowp_params`); None when that does not apply (the caller then runs its plain forward)."""
+    lp = lowp_params(module)
+    if lp is None:
+        return None
+    setattr(module, _LOWP_ACTIVE, True)
+    try:
+        return torch.func.functional_call(module, lp, args, strict=False)
+    finally:
+        setattr(module, _LOWP_ACTIVE, False)

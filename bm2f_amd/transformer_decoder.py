@@ -283,6 +283,10 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         return mask_features
 
     def forward(self, x, mask_features, mask=None):
+        # under autocast the GEMM weights are cast once per forward in a few kernels (decoder_ops.lowp_params)
+        out = decoder_ops.call_with_lowp_params(self, (x, mask_features, mask))
+        if out is not None:
+            return out
         assert len(x) == self.num_feature_levels
         del mask
         src, pos, key, size_list = self._levels(x)

@@ -38,6 +38,9 @@ class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder
         return ret
 
     def forward(self, x, mask_features, mask=None):
+        out = decoder_ops.call_with_lowp_params(self, (x, mask_features, mask))
+        if out is not None:
+            return out
         bt, c_m, h_m, w_m = mask_features.shape
         bs = bt // self.num_frames if self.training else 1
         t = bt // bs
