@@ -14,6 +14,7 @@
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import math
 
@@ -514,44 +515,49 @@ class _FlatCast(Function):
         return (None,) + tuple(o.view(sh) for o, sh in zip(flat.split(ctx.numels), ctx.shapes))
 
 
-_LOWP_ACTIVE = "_bm2f_lowp_active"
+_LOWP = [None]   # {id(param): low-precision view} of the decoder forward in progress (lowp_scope)
 
 
-def lowp_params(module):
-    """{name: low-precision view} for the GEMM parameters of ``module`` (nn.Linear weights / biases and
-    nn.MultiheadAttention in-projections) when its forward runs under CUDA autocast in fp16 / bf16, else None.
-    LayerNorm, embedding and other parameters keep their fp32 tensors (autocast runs those ops in fp32)."""
-    if getattr(module, _LOWP_ACTIVE, False) or not torch.is_autocast_enabled("cuda"):
-        return None
-    dt = torch.get_autocast_dtype("cuda")
-    if dt not in (torch.float16, torch.bfloat16):
-        return None
-    names, params = [], []
-    for mname, mod in module.named_modules():
-        pre = f"{mname}." if mname else ""
+def _gemm_params(module):
+    out = []
+    for mod in module.modules():
         if isinstance(mod, nn.Linear):
-            cand = [("weight", mod.weight), ("bias", mod.bias)]
+            cand = (mod.weight, mod.bias)
         elif isinstance(mod, nn.MultiheadAttention) and mod._qkv_same_embed_dim:
-            cand = [("in_proj_weight", mod.in_proj_weight), ("in_proj_bias", mod.in_proj_bias)]
+            cand = (mod.in_proj_weight, mod.in_proj_bias)
         else:
             continue
-        for pn, p in cand:
-            if p is not None and p.is_cuda and p.dtype == torch.float32:
-                names.append(pre + pn)
-                params.append(p)
-    if not params:
-        return None
-    return dict(zip(names, _FlatCast.apply(dt, *params)))
+        out.extend(p for p in cand if p is not None and p.is_cuda and p.dtype == torch.float32)
+    return out
 
 
-def call_with_lowp_params(module, args):
-    """``module(*args)`` with its GEMM parameters swapped for one batched low-precision cast (see
-    :func:`lowp_params`); None when that does not apply (the caller then runs its plain forward)."""
-    lp = lowp_params(module)
-    if lp is None:
-        return None
-    setattr(module, _LOWP_ACTIVE, True)
+@contextlib.contextmanager
+def lowp_scope(module):
+    """Inside, :func:`lp` maps the GEMM parameters of ``module`` (nn.Linear weights / biases and
+    nn.MultiheadAttention in-projections) to views of one low-precision copy made by :class:`_FlatCast`, when
+    the forward runs under CUDA autocast in fp16 / bf16; elsewhere (or nested) it changes nothing.  LayerNorm,
+    embedding and other parameters keep their fp32 tensors (autocast runs those ops in fp32)."""
+    prev = _LOWP[0]
+    m = None
+    if prev is None and torch.is_autocast_enabled("cuda"):
+        dt = torch.get_autocast_dtype("cuda")
+        if dt in (torch.float16, torch.bfloat16):
+            params = _gemm_params(module)
+            if params:
+                m = {id(p): t for p, t in zip(params, _FlatCast.apply(dt, *params))}
+    _LOWP[0] = m if m is not None else prev
     try:
-        return torch.func.functional_call(module, lp, args, strict=False)
+        yield
     finally:
-        setattr(module, _LOWP_ACTIVE, False)
+        _LOWP[0] = prev
+
+
+def lp(p):
+    """The low-precision view of parameter ``p`` inside :func:`lowp_scope`, else ``p``."""
+    m = _LOWP[0]
+    return m.get(id(p), p) if m is not None and p is not None else p
+
+
+def linear(x, mod):
+    """``mod(x)`` for an nn.Linear, with its parameters through :func:`lp`."""
+    return F.linear(x, lp(mod.weight), lp(mod.bias))

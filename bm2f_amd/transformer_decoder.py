@@ -59,14 +59,14 @@ class SelfAttentionLayer(nn.Module):
         a = self.self_attn
         B, L, C = q_in.shape
         H = a.num_heads
-        w, b = a.in_proj_weight, a.in_proj_bias
+        w, b = decoder_ops.lp(a.in_proj_weight), decoder_ops.lp(a.in_proj_bias)
         qk = F.linear(q_in, w[:2 * C], b[:2 * C])
         v = F.linear(v_in, w[2 * C:], b[2 * C:])
         q, k = qk.split(C, dim=-1)
         heads = lambda t: t.view(B, L, H, C // H).transpose(1, 2)  # noqa: E731
         drop = a.dropout if self.training else 0.0
         o = F.scaled_dot_product_attention(heads(q), heads(k), heads(v), dropout_p=drop)
-        return F.linear(o.transpose(1, 2).reshape(B, L, C), a.out_proj.weight, a.out_proj.bias)
+        return decoder_ops.linear(o.transpose(1, 2).reshape(B, L, C), a.out_proj)
 
     def forward(self, tgt, tgt_mask: Optional[Tensor] = None, tgt_key_padding_mask: Optional[Tensor] = None,
                 query_pos: Optional[Tensor] = None):
@@ -102,13 +102,13 @@ class CrossAttentionLayer(nn.Module):
         if a.dropout and self.training:
             raise NotImplementedError("attention dropout > 0 is not supported by the masked-attention kernel")
         C = query.shape[-1]
-        w, b = a.in_proj_weight, a.in_proj_bias
+        w, b = decoder_ops.lp(a.in_proj_weight), decoder_ops.lp(a.in_proj_bias)
         q = F.linear(query, w[:C], b[:C])
         k_lp, v_lp = lowp if lowp is not None else (None, None)
         k = decoder_ops.token_linear(key, w[C:2 * C], b[C:2 * C], x_lp=k_lp)
         v = decoder_ops.token_linear(value, w[2 * C:], b[2 * C:], x_lp=v_lp)
         o = decoder_ops.masked_attention(q, k, v, bits, a.num_heads)
-        return F.linear(o, a.out_proj.weight, a.out_proj.bias)
+        return decoder_ops.linear(o, a.out_proj)
 
     def forward(self, tgt, memory, memory_mask=None, memory_key_padding_mask=None, pos=None, query_pos=None,
                 memory_plus_pos=None, memory_lowp=None):
@@ -143,9 +143,10 @@ class FFNLayer(nn.Module):
 
     def forward(self, tgt):
         if self.normalize_before:
-            t2 = self.linear2(self.dropout(self.activation(self.linear1(self.norm(tgt)))))
+            t2 = decoder_ops.linear(self.dropout(self.activation(decoder_ops.linear(self.norm(tgt), self.linear1))),
+                                    self.linear2)
             return tgt + self.dropout(t2)
-        t2 = self.linear2(self.dropout(self.activation(self.linear1(tgt))))
+        t2 = decoder_ops.linear(self.dropout(self.activation(decoder_ops.linear(tgt, self.linear1))), self.linear2)
         return self.norm(tgt + self.dropout(t2))
 
 
@@ -158,7 +159,7 @@ class MLP(nn.Module):
 
     def forward(self, x):
         for i, layer in enumerate(self.layers):
-            x = F.relu(layer(x)) if i < self.num_layers - 1 else layer(x)
+            x = F.relu(decoder_ops.linear(x, layer)) if i < self.num_layers - 1 else decoder_ops.linear(x, layer)
         return x
 
 
@@ -283,10 +284,11 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         return mask_features
 
     def forward(self, x, mask_features, mask=None):
-        # under autocast the GEMM weights are cast once per forward in a few kernels (decoder_ops.lowp_params)
-        out = decoder_ops.call_with_lowp_params(self, (x, mask_features, mask))
-        if out is not None:
-            return out
+        # under autocast the GEMM weights are cast once per forward in a few kernels (decoder_ops.lowp_scope)
+        with decoder_ops.lowp_scope(self):
+            return self._forward(x, mask_features, mask)
+
+    def _forward(self, x, mask_features, mask=None):
         assert len(x) == self.num_feature_levels
         del mask
         src, pos, key, size_list = self._levels(x)
@@ -330,7 +332,7 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         """output (B, Q, C) -> class logits (B, Q, K+1), mask logits (B, Q, H, W), attention bits.
         ``fold`` is the forward's :class:`~bm2f_amd.decoder_ops.MaskFeatureFold` (one is made if absent)."""
         decoder_output = self.decoder_norm(output)
-        outputs_class = self.class_embed(decoder_output)
+        outputs_class = decoder_ops.linear(decoder_output, self.class_embed)
         mask_embed = self.mask_embed(decoder_output)
         if fold is None:
             fold = decoder_ops.image_mask_fold(mask_features, self._lowp_features(mask_features))

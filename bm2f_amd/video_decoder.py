@@ -38,9 +38,10 @@ class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder
         return ret
 
     def forward(self, x, mask_features, mask=None):
-        out = decoder_ops.call_with_lowp_params(self, (x, mask_features, mask))
-        if out is not None:
-            return out
+        with decoder_ops.lowp_scope(self):
+            return self._forward(x, mask_features, mask)
+
+    def _forward(self, x, mask_features, mask=None):
         bt, c_m, h_m, w_m = mask_features.shape
         bs = bt // self.num_frames if self.training else 1
         t = bt // bs
@@ -96,7 +97,7 @@ class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder
 
     def _heads(self, output, fold, size, need_mask=True):
         decoder_output = self.decoder_norm(output)
-        outputs_class = self.class_embed(decoder_output)
+        outputs_class = decoder_ops.linear(decoder_output, self.class_embed)
         mask_embed = self.mask_embed(decoder_output)
         # (b, q, t, h, w): einsum "bqc,btchw->bqthw" (:449) and the per-frame resized bitmask (:453-458)
         outputs_mask, attn_mask = decoder_ops.mask_heads(fold, mask_embed, size if need_mask else None)
