@@ -40,7 +40,7 @@ extern "C" int m2f_abi_version(void) { return 1; }
 namespace {
 constexpr const char* kOptionNames[m2f::kOptCount] = {
     "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
-    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg"};
+    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_quad"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 constexpr int kWalkLanes = 4;   // phase-3 lanes per window pixel (8 channels each)
 constexpr int kMaxBwdWaves = 16;
 constexpr int kSortSamples = 6144;  // samples per workgroup the counting sort holds in registers (max_qt * L * P)
-constexpr int kStageFloats = 16 * 32 + 16;  // per wave: 16 rows x 32 channels + 16 row offsets
+constexpr int kStageFloats = 8 * 32 + 8;  // per wave: 8 rows x 32 channels + 8 row offsets (a flush half)
 
 struct TileState {
   int bb[kTileMaxL][4];  // min y, max y, min x, max x of touched corners (inclusive)
@@ -355,6 +355,7 @@ struct TileState {
   int coff[kTileMaxL + 1];   // extended-cell offsets per level ((wh+1) x (ww+1) cells)
   int qc[kTileMaxL + 1], qy0[kTileMaxL], qx0[kTileMaxL], qw[kTileMaxL];
   int wsum[kMaxBwdWaves];    // block scan
+  float iww[kTileMaxL];      // 1 / ww (phase 3's row -> window coordinates)
   int next_batch;            // phase-3 row batches handed out dynamically
 };
 
@@ -394,7 +395,7 @@ __device__ __forceinline__ int window_cell(const TileState& ts, int l, int h0, i
 // STAMP (diagnostic builds only, M2F_DIAG): s_memtime at the phase barriers of each workgroup into `stamps`;
 // NOFLUSH (diagnostic builds only): phase 3 without its HBM adds, to price them.
 // TPB threads per workgroup: 512 (two workgroups per CU, 12x12 tiles; the default) or 1024 (one, 16x16 tiles).
-template <int LT, bool FUSED, int TPB, bool STAMP = false, bool NOFLUSH = false>
+template <int LT, bool FUSED, int TPB, bool QUAD = true, bool STAMP = false, bool NOFLUSH = false>
 __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
@@ -420,14 +421,14 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int rs = M * D;  // value row stride (elements); N*S*M*D < 2^31 is checked on the host
   const int nsamp_max = geo.max_qt * LP;
-  // LDS carve-up (16-byte aligned pieces): g rows [max_qt][32] | desc [max_qt * LP][3] | stage [waves][528]
-  //   | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32 | slots [max_qt * LP] u16
+  // LDS carve-up (16-byte aligned pieces): g rows [max_qt][32] | desc [max_qt * LP][3] | stage [waves][264]
+  //   | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32 | slots [max_qt * LP + 4] u32
   float* gsh = reinterpret_cast<float*>(lds_raw);
   float* desc = gsh + geo.max_qt * D;
   float* stage = desc + ((nsamp_max * 3 + 3) & ~3);
   int* cstart = reinterpret_cast<int*>(stage + kBwdWaves * kStageFloats);
   unsigned* oow = reinterpret_cast<unsigned*>(cstart + ((geo.max_rows + 1 + 3) & ~3));
-  unsigned short* slots = reinterpret_cast<unsigned short*>(oow + (((nsamp_max + 31) / 32 + 3) & ~3));
+  unsigned* slots = reinterpret_cast<unsigned*>(oow + (((nsamp_max + 31) / 32 + 3) & ~3));
 
   M2F_STAMP(5)
   if (tid < LT) {
@@ -608,6 +609,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         const bool any = wy1 >= wy0 && wx1 >= wx0;
         ts.wy0[l] = wy0; ts.wx0[l] = wx0;
         ts.wh[l] = any ? wy1 - wy0 + 1 : 0; ts.ww[l] = any ? wx1 - wx0 + 1 : 0;
+        ts.iww[l] = any ? 1.f / static_cast<float>(ts.ww[l]) : 0.f;
         ts.roff[l] = rows;
         ts.coff[l] = cells;
         rows += ts.wh[l] * ts.ww[l];
@@ -670,16 +672,158 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortPerThread; ++r)
-      if (cell[r] >= 0) {  // slot = query << 4 | sample-in-query (phase 3 then needs no division by L*P)
+      if (cell[r] >= 0) {  // slot = desc float index << 16 | g row byte offset: phase 3 decodes it in 3 VALU
         const int sid = tid + r * kBwdThreads, qs = sid / LP;
-        slots[cstart[cell[r]] + rank[r]] = static_cast<unsigned short>((qs << 4) | (sid - qs * LP));
+        slots[cstart[cell[r]] + rank[r]] = (static_cast<unsigned>(3 * sid) << 16) | static_cast<unsigned>(qs * D * 4);
       }
   }
   __syncthreads();
   M2F_STAMP(2)
 
   // ---- phase 2: gather, grad_loc / grad_attn; out-of-window samples scatter with atomics ---------------
-  {
+  if constexpr (QUAD) {
+    // Quad form (the default).  The kernel is VALU-issue bound; in the 8-lane form every lane re-derives every
+    // sample's geometry and gradient math for a float4 of channels.  Here a quad of lanes takes one query, lane j
+    // owning channels 4j..4j+3 and 16+4j..16+4j+3 (one load address per corner row: the second half is the
+    // immediate offset).  Per level, lane j derives point j's geometry once; the quad takes the points in turn
+    // with the owner's corner byte offsets by DPP broadcast, each lane forming 16 partial channel dots (4 points x
+    // 4 corners) over its 8 channels; a two-stage quad transpose-reduce (xor 2, xor 1) leaves lane j the 4 full
+    // corner dots of ITS point, so the gradient math and the stores run once per point instead of once per lane.
+    const int j = lane & 3, gq = lane >> 2;
+    const unsigned cjb = 16u * j;
+    const char* vbytes = reinterpret_cast<const char*>(value);
+    char* gvbytes = reinterpret_cast<char*>(gvalue);
+    const int rsb = rs * 4;  // value row stride in bytes; value bytes < 2^31 (host check)
+    for (int base = wid * 16; base < Qt; base += kBwdWaves * 16) {
+      const int qi = base + gq;
+      if (qi >= Qt) continue;  // whole quad (same qi) idles together
+      const int q = tile_query(ts, geo, qi);
+      const int64_t nq = static_cast<int64_t>(n) * S + q;
+      const f4 gA = *reinterpret_cast<const f4*>(gsh + qi * D + 4 * j);
+      const f4 gB = *reinterpret_cast<const f4*>(gsh + qi * D + 16 + 4 * j);
+      float* dq = desc + qi * LP * 3;
+      const int sid0 = qi * LP, sh = sid0 & 31;
+      const unsigned w0f = oow[sid0 >> 5], w1f = oow[min((sid0 + LP - 1) >> 5, (nsamp_max + 31) / 32 - 1)];
+      const unsigned qfar = (sh ? (w0f >> sh) | (w1f << (32 - sh)) : w0f) & ((1u << LP) - 1u);
+      float dot = 0.f;  // FUSED: this lane's points' sum of a * d attn
+      float gaown[LT], aown[LT];
+#pragma unroll
+      for (int l = 0; l < LT; ++l) {
+        const int H = geo.H[l], W = geo.W[l];
+        const int lbase = ((n * S + geo.start[l]) * M + m) * D * 4;
+        // this lane's point (l, j)
+        float* dk = dq + 3 * (l * P + j);
+        const float h = dk[0], w = dk[1], a = dk[2];
+        // not-ok samples carry h = w = -2 (every corner outside, ok false)
+        const QuadPoint k = quad_point(h, w, H, W, lbase, rsb);
+        const bool ok = k.ok;
+        const float ly = k.ly, lx = k.lx, hy = 1.f - ly, hx = 1.f - lx;
+        const int o1 = k.o1, o2 = k.o2, o3 = k.o3, o4 = k.o4;
+        // partial channel dots over this lane's 8 channels, pairs of channels in packed fp32 FMAs (v_pk_fma_f32)
+        auto dot8 = [&](const f4& va, const f4& vb) {
+          f2 t = f2{va.x, va.y} * f2{gA.x, gA.y};
+          t = __builtin_elementwise_fma(f2{va.z, va.w}, f2{gA.z, gA.w}, t);
+          t = __builtin_elementwise_fma(f2{vb.x, vb.y}, f2{gB.x, gB.y}, t);
+          t = __builtin_elementwise_fma(f2{vb.z, vb.w}, f2{gB.z, gB.w}, t);
+          return t.x + t.y;
+        };
+        // points in the batches {0, 2} and {1, 3} (16 corner loads each, issued before any of their math); after
+        // a batch the first transpose-reduce stage (xor 2) folds its 8 partial dots to 4: lanes {0, 1} keep the
+        // batch's lower point, lanes {2, 3} its upper point, summed over the lane pair
+        const bool hi2 = (j & 2) != 0, hi1 = (j & 1) != 0;
+        float s1[2][4];
+        auto batch = [&](auto c0, auto cc1, int pp) {
+          constexpr int C0 = decltype(c0)::value, C1 = decltype(cc1)::value;
+          f4 va[2][8];
+          const char* vhi = vbytes + 64;  // the row's second half: an immediate offset
+          auto load = [&](f4* v, unsigned b1, unsigned b2, unsigned b3, unsigned b4) {
+            v[0] = ldb4(vbytes, b1); v[1] = ldb4(vhi, b1);
+            v[2] = ldb4(vbytes, b2); v[3] = ldb4(vhi, b2);
+            v[4] = ldb4(vbytes, b3); v[5] = ldb4(vhi, b3);
+            v[6] = ldb4(vbytes, b4); v[7] = ldb4(vhi, b4);
+          };
+          load(va[0], qpermi<C0>(o1) + cjb, qpermi<C0>(o2) + cjb, qpermi<C0>(o3) + cjb, qpermi<C0>(o4) + cjb);
+          load(va[1], qpermi<C1>(o1) + cjb, qpermi<C1>(o2) + cjb, qpermi<C1>(o3) + cjb, qpermi<C1>(o4) + cjb);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float plo = dot8(va[0][2 * c], va[0][2 * c + 1]), phi = dot8(va[1][2 * c], va[1][2 * c + 1]);
+            const float lo = plo + qpermf<0x4E>(plo), hi = phi + qpermf<0x4E>(phi);
+            s1[pp][c] = hi2 ? hi : lo;
+          }
+        };
+        batch(std::integral_constant<int, 0x00>{}, std::integral_constant<int, 0xAA>{}, 0);  // points 0, 2
+        batch(std::integral_constant<int, 0x55>{}, std::integral_constant<int, 0xFF>{}, 1);  // points 1, 3
+        // second stage (xor 1): lane j holds the full corner dots of point j
+        float dd[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float lo = s1[0][c] + qpermf<0xB1>(s1[0][c]);
+          const float hi = s1[1][c] + qpermf<0xB1>(s1[1][c]);
+          dd[c] = hi1 ? hi : lo;
+        }
+        // a corner outside the level contributes nothing (as the reference, which skips it)
+        const float d1 = k.c1 ? dd[0] : 0.f, d2 = k.c2 ? dd[1] : 0.f, d3 = k.c3 ? dd[2] : 0.f, d4 = k.c4 ? dd[3] : 0.f;
+        const float pa = k.w1 * d1 + k.w2 * d2 + k.w3 * d3 + k.w4 * d4;
+        const float px = a * (hy * (d2 - d1) + ly * (d4 - d3));
+        const float py = a * (hx * (d3 - d1) + lx * (d4 - d2));
+        if constexpr (FUSED) {
+          const float gak = ok ? pa : 0.f;
+          dot = fmaf(a, gak, dot);
+          gaown[l] = gak;
+          aown[l] = a;
+          *reinterpret_cast<float2*>(gloc + nq * (3 * M * LP) + (m * LT + l) * P * 2 + 2 * j) =
+              ok ? make_float2(px, py) : make_float2(0.f, 0.f);
+        } else {
+          const int64_t kl = ((nq * M + m) * LT + l) * P;
+          gattn[kl + j] = ok ? pa : 0.f;
+          *reinterpret_cast<float2*>(gloc + 2 * (kl + j)) =
+              ok ? make_float2(W * px, H * py) : make_float2(0.f, 0.f);
+        }
+        // out-of-window points (rare; flags are per query, so quad-uniform): every lane adds its 8 channels of
+        // the point's 4 corner rows straight to HBM (fp32 atomics, as the reference)
+        if ((qfar >> (l * P)) & 0xFu) {
+          const int cf = (k.c1 ? 1 : 0) | (k.c2 ? 2 : 0) | (k.c3 ? 4 : 0) | (k.c4 ? 8 : 0);
+          const float wt1 = k.w1 * a, wt2 = k.w2 * a, wt3 = k.w3 * a, wt4 = k.w4 * a;
+          auto scatter = [&](auto cc, int p) {
+            constexpr int C = decltype(cc)::value;
+            const int f = qpermi<C>(cf);
+            const unsigned b1 = qpermi<C>(o1) + cjb, b2 = qpermi<C>(o2) + cjb;
+            const unsigned b3 = qpermi<C>(o3) + cjb, b4 = qpermi<C>(o4) + cjb;
+            const float u1 = qpermf<C>(wt1), u2 = qpermf<C>(wt2), u3 = qpermf<C>(wt3), u4 = qpermf<C>(wt4);
+            if ((qfar >> (l * P + p)) & 1u) {
+              auto add8 = [&](unsigned boff, float u) {
+                float* o = reinterpret_cast<float*>(gvbytes + boff);
+                const f4 ta = u * gA, tb = u * gB;
+                atomicAdd(o, ta.x); atomicAdd(o + 1, ta.y); atomicAdd(o + 2, ta.z); atomicAdd(o + 3, ta.w);
+                atomicAdd(o + 16, tb.x); atomicAdd(o + 17, tb.y); atomicAdd(o + 18, tb.z); atomicAdd(o + 19, tb.w);
+              };
+              if (f & 1) add8(b1, u1);
+              if (f & 2) add8(b2, u2);
+              if (f & 4) add8(b3, u3);
+              if (f & 8) add8(b4, u4);
+            }
+          };
+          scatter(std::integral_constant<int, 0x00>{}, 0);
+          scatter(std::integral_constant<int, 0x55>{}, 1);
+          scatter(std::integral_constant<int, 0xAA>{}, 2);
+          scatter(std::integral_constant<int, 0xFF>{}, 3);
+        }
+        // the point's descriptor becomes phase 3's corner-coefficient form {(1 - ly) a, ly a, lx} (only this lane
+        // reads it in phase 2)
+        dk[0] = hy * a;
+        dk[1] = ly * a;
+        dk[2] = lx;
+      }
+      if constexpr (FUSED) {
+        // softmax backward over the pair's L*P logits: d logit_k = a_k (d a_k - sum_i a_i d a_i)
+        dot += qpermf<0xB1>(dot);
+        dot += qpermf<0x4E>(dot);
+        float* gl = gloc + nq * (3 * M * LP) + 2 * M * LP + m * LP;
+#pragma unroll
+        for (int l = 0; l < LT; ++l) gl[l * P + j] = aown[l] * (gaown[l] - dot);
+      }
+    }
+  } else {
     const int j = lane & 7, gq = lane >> 3;
     const f4 z = {0.f, 0.f, 0.f, 0.f};
     for (int base = wid * 8; base < Qt; base += kBwdWaves * 8) {
@@ -808,8 +952,10 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     constexpr int LPR = kWalkLanes, CPL = D / LPR, RPW = 64 / LPR;  // lanes per row, channels per lane, rows per wave
     const int rows_total = ts.roff[LT];
     const int jl = lane % LPR, rw = lane / LPR;
-    float* wst = stage + wid * kStageFloats;               // this wave's 16 rows x 32 channels
-    int* woff = reinterpret_cast<int*>(wst + 16 * 32);     // and their grad_value element offsets
+    float* wst = stage + wid * kStageFloats;               // this wave's flush half: 8 rows x 32 channels
+    int* woff = reinterpret_cast<int*>(wst + 8 * 32);      // and their grad_value element offsets
+    const char* gbytes = reinterpret_cast<const char*>(gsh);
+    const unsigned jlb = static_cast<unsigned>(CPL * 4 * jl);  // this lane's channel bytes (< 128: ORs into a row offset)
     // row batches of 16 per wave, handed out in order by an LDS counter: the coarse levels' rows (first,
     // ~37 records each at config 2 against ~9 on the finest level) do not pile up on the first waves
     for (int b = wid; b * RPW < rows_total;) {
@@ -824,7 +970,9 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       if (row < rows_total) {
         while (row >= ts.roff[l + 1]) ++l;
         const int ww = ts.ww[l], rr = row - ts.roff[l];
-        ey = rr / ww;
+        // rr / ww by the reciprocal: (rr + 0.5) / ww is at least 0.5 / ww from an integer and the product's error
+        // is below wh * ww * 2^-23 / ww, so the truncation is exact for windows of fewer than 2^22 cells
+        ey = static_cast<int>((static_cast<float>(rr) + 0.5f) * ts.iww[l]);
         ex = rr - ey * ww;  // window coordinates; cells are offset by (1, 1)
         const int cw = ww + 1, cbase = ts.coff[l] + (ey + 1) * cw + ex + 1;
         // corner 1 of cell (y, x), corner 2 of (y, x-1), corner 3 of (y-1, x), corner 4 of (y-1, x-1)
@@ -833,70 +981,66 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           const int cell = cbase - ((c & 2) ? cw : 0) - (c & 1);
           const int s0 = cstart[cell], s1 = cstart[cell + 1];
           any |= s1 > s0;
-          // two records per step: their LDS reads overlap
-          int i = s0;
-          // the next pair's slots are read one step ahead (clamped into the range), so a step waits on one
-          // LDS round trip (descriptors and g rows) instead of two
-          unsigned npa = slots[max(min(i, s1 - 1), 0)], npb = slots[max(min(i + 1, s1 - 1), 0)];
-          for (; i + 1 < s1; i += 2) {
-            const unsigned pa = npa, pb = npb;
-            npa = slots[min(i + 2, s1 - 1)];
-            npb = slots[min(i + 3, s1 - 1)];
-            const unsigned qa = pa >> 4, qb = pb >> 4;
-            const unsigned sa = __umul24(qa, LP) + (pa & 15u), sb = __umul24(qb, LP) + (pb & 15u);
-            // descriptors in coefficient form {(1 - ly) a, ly a, lx} (end of phase 2)
-            const float Aa = desc[3 * sa + ((c & 2) ? 1 : 0)], lxa = desc[3 * sa + 2];
-            const float Ab = desc[3 * sb + ((c & 2) ? 1 : 0)], lxb = desc[3 * sb + 2];
-            const f4* ga = reinterpret_cast<const f4*>(gsh + qa * D + CPL * jl);
-            const f4* gb = reinterpret_cast<const f4*>(gsh + qb * D + CPL * jl);
-            const float ca = Aa * ((c & 1) ? lxa : 1.f - lxa);
-            const float cb = Ab * ((c & 1) ? lxb : 1.f - lxb);
+          // a record: the descriptor in coefficient form {(1 - ly) a, ly a, lx} (end of phase 2) and the query's
+          // g row; coefficient (1 - lx) A as fma(-A, lx, A)
+          auto rec = [&](unsigned p) {
+            const float* dk = desc + (p >> 16);
+            const float A = dk[(c & 2) ? 1 : 0], lx = dk[2];
+            const f4* g = reinterpret_cast<const f4*>(gbytes + ((p & 0xffffu) | jlb));
+            const float cf = (c & 1) ? A * lx : fmaf(-A, lx, A);
 #pragma unroll
             for (int k = 0; k < CPL / 4; ++k) {  // fma chains (pairs of channels pack into v_pk_fma_f32)
-              const f4 va = ga[k], vb2 = gb[k];
+              const f4 v = g[k];
 #pragma unroll
-              for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(cb, vb2[e], fmaf(ca, va[e], acc[4 * k + e]));
+              for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(cf, v[e], acc[4 * k + e]);
             }
+          };
+          // two records per step, the next pair's slots read one step ahead (unclamped: a read past the cell's
+          // range, or past the array into its 4-entry pad, is never used), so a step waits on one LDS round trip
+          const unsigned* sp = slots + s0;
+          unsigned npa = sp[0], npb = sp[1];
+          int i = s0;
+          for (; i + 1 < s1; i += 2, sp += 2) {
+            const unsigned pa = npa, pb = npb;
+            npa = sp[2];
+            npb = sp[3];
+            rec(pa);
+            rec(pb);
           }
-          if (i < s1) {
-            const unsigned pa = npa, qa = pa >> 4, sa = __umul24(qa, LP) + (pa & 15u);
-            const float Aa = desc[3 * sa + ((c & 2) ? 1 : 0)], lxa = desc[3 * sa + 2];
-            const f4* ga = reinterpret_cast<const f4*>(gsh + qa * D + CPL * jl);
-            const float ca = Aa * ((c & 1) ? lxa : 1.f - lxa);
-#pragma unroll
-            for (int k = 0; k < CPL / 4; ++k) {
-              const f4 va = ga[k];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(ca, va[e], acc[4 * k + e]);
-            }
-          }
+          if (i < s1) rec(npa);
         }
       }
       if (any) {
         const int y = ts.wy0[l] + ey, x = ts.wx0[l] + ex;
         off = ((n * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D;
       }
-      // transpose the wave's 16 rows through LDS so that each atomic instruction adds two whole 128-B rows,
-      // one dword per lane (the L2 takes atomics per 64-B request)
+      // transpose the wave's 16 rows through LDS, 8 rows at a time, so that each atomic instruction adds two whole
+      // 128-B rows, one dword per lane (the L2 takes atomics per 64-B request)
 #pragma unroll
-      for (int k = 0; k < CPL / 4; ++k)
-        *reinterpret_cast<f4*>(wst + rw * 32 + CPL * jl + 4 * k) = f4{acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
-      if (jl == 0) woff[rw] = off;
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage writes are in LDS
-      __builtin_amdgcn_wave_barrier();
+      for (int half = 0; half < 2; ++half) {
+        if ((rw >> 3) == half) {
 #pragma unroll
-      for (int i = 0; i < RPW / 2; ++i) {
-        const int r2 = 2 * i + (lane >> 5);
-        const int o = woff[r2];
-        const float v = wst[r2 * 32 + (lane & 31)];
-        if constexpr (NOFLUSH) {
-          asm volatile("" ::"v"(v), "v"(o));
-        } else {
-          if (o >= 0) atomicAdd(gvalue + o + (lane & 31), v);
+          for (int k = 0; k < CPL / 4; ++k)
+            *reinterpret_cast<f4*>(wst + (rw & 7) * 32 + CPL * jl + 4 * k) =
+                f4{acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
+          if (jl == 0) woff[rw & 7] = off;
         }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage writes are in LDS
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r2 = 2 * i + (lane >> 5);
+          const int o = woff[r2];
+          const float v = wst[r2 * 32 + (lane & 31)];
+          if constexpr (NOFLUSH) {
+            asm volatile("" ::"v"(v), "v"(o));
+          } else {
+            if (o >= 0) atomicAdd(gvalue + o + (lane & 31), v);
+          }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the stage is written again
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the next batch overwrites the stage
-      __builtin_amdgcn_wave_barrier();
       int nb = 0;
       if (lane == 0) nb = atomicAdd(&ts.next_batch, 1);
       b = __shfl(nb, 0);
@@ -1027,6 +1171,171 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
 }
 
 // ------------------------------------------------------------------------------------------------
+// Fused forward, quad form (the default on the encoder layout).  The forward is VALU-issue bound, and in the
+// 8-lane form above every lane of a pair re-derives every sample's geometry (about 45 VALU per sample) for a
+// float4 of channels.  Here a QUAD of lanes serves one (query, head) pair, lane j owning channels 4j..4j+3 and
+// 16+4j..16+4j+3 (two 64-byte halves of the 128-byte row, one load address per corner: the second half is the
+// immediate offset).  Lane j derives the geometry of point j of each level ONCE; the quad then takes the four
+// points in turn, each lane reading the owner's corner offsets and premultiplied corner weights by DPP quad
+// broadcasts (a VALU operand modifier, no LDS), so a sample costs the quad one geometry plus 4 x (4 address
+// adds + 4 weight moves + 16 packed FMAs) instead of 8 x (geometry + 16 FMAs + selects).  A sample outside
+// (-1, H) x (-1, W) is skipped by the exec mask (as the reference, which skips it: non-finite values at its
+// clamped rows never reach the output).  Workgroup = one head of an 8 x 8 patch of queries of one level, head
+// the fastest block index (each XCD's L2 gathers one head's value rows).  32-bit offsets (checked on the host).
+// ------------------------------------------------------------------------------------------------
+// The four points of one level for the quad forward kernels: lane j holds point j's geometry (k) and attention
+// weight (wa); the quad takes the points in turn, each lane gathering its 8 channels of the point's 4 corner rows
+// (addresses and weights by DPP quad broadcast) into acc0 (channels 4j..4j+3) and acc1 (16+4j..16+4j+3).
+__device__ __forceinline__ void quad_level_fwd(const char* __restrict__ vbytes, const QuadPoint& k, float wa,
+                                               unsigned cjb, f4& acc0, f4& acc1) {
+  // a corner outside the level weighs 0 (its clamped row is another corner of the same sample)
+  const float w1 = k.w1 * wa, w2 = k.w2 * wa, w3 = k.w3 * wa, w4 = k.w4 * wa;
+  const int okb = k.ok ? 1 : 0;
+  // two points per batch: their 16 loads are issued (clamped, in-level addresses) before any of their math
+  auto batch = [&](auto c0, auto c1) {
+    constexpr int C0 = decltype(c0)::value, C1 = decltype(c1)::value;
+    f4 va[2][8];
+    const char* vhi = vbytes + 64;  // the row's second half (channels 16..31): an immediate offset
+    auto load = [&](f4* v, unsigned o1, unsigned o2, unsigned o3, unsigned o4) {
+      v[0] = ldb4(vbytes, o1); v[1] = ldb4(vhi, o1);
+      v[2] = ldb4(vbytes, o2); v[3] = ldb4(vhi, o2);
+      v[4] = ldb4(vbytes, o3); v[5] = ldb4(vhi, o3);
+      v[6] = ldb4(vbytes, o4); v[7] = ldb4(vhi, o4);
+    };
+    load(va[0], qpermi<C0>(k.o1) + cjb, qpermi<C0>(k.o2) + cjb, qpermi<C0>(k.o3) + cjb, qpermi<C0>(k.o4) + cjb);
+    load(va[1], qpermi<C1>(k.o1) + cjb, qpermi<C1>(k.o2) + cjb, qpermi<C1>(k.o3) + cjb, qpermi<C1>(k.o4) + cjb);
+    // pin the loads here: otherwise each point's loads sink into its exec-masked block below and the two
+    // points' latencies are paid one after the other
+#pragma unroll
+    for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(va[0][i]), "+v"(va[1][i]));
+    auto fmas = [&](const f4* v, float u1, float u2, float u3, float u4) {
+      acc0 += u1 * v[0]; acc1 += u1 * v[1];
+      acc0 += u2 * v[2]; acc1 += u2 * v[3];
+      acc0 += u3 * v[4]; acc1 += u3 * v[5];
+      acc0 += u4 * v[6]; acc1 += u4 * v[7];
+    };
+    // a point outside (-1, H) x (-1, W) is skipped by the exec mask, as the reference skips it
+    if (qpermi<C0>(okb)) fmas(va[0], qpermf<C0>(w1), qpermf<C0>(w2), qpermf<C0>(w3), qpermf<C0>(w4));
+    if (qpermi<C1>(okb)) fmas(va[1], qpermf<C1>(w1), qpermf<C1>(w2), qpermf<C1>(w3), qpermf<C1>(w4));
+  };
+  batch(std::integral_constant<int, 0x00>{}, std::integral_constant<int, 0x55>{});
+  batch(std::integral_constant<int, 0xAA>{}, std::integral_constant<int, 0xFF>{});
+}
+
+// Unfused forward, quad form (the reference op's interface: materialised sampling_loc / attention_weight, device
+// spatial shapes; D = 32, P = 4, value bytes < 2^31): a quad per (n, q, m) pair, lane j reading point j of each
+// level (the quad's four loc pairs / weights are contiguous).
+__global__ void __launch_bounds__(256) msda_fwd_f32_q4(const float* __restrict__ value,
+                                                       const int64_t* __restrict__ shapes,
+                                                       const int64_t* __restrict__ lsi, const float* __restrict__ loc,
+                                                       const float* __restrict__ attn, int64_t npairs, int S, int M,
+                                                       int L, int Lq, float* __restrict__ out) {
+  constexpr int D = 32, P = 4;
+  __shared__ int sH[kMaxLevels], sW[kMaxLevels], sSt[kMaxLevels];
+  if (threadIdx.x < L) {
+    sH[threadIdx.x] = static_cast<int>(shapes[2 * threadIdx.x]);
+    sW[threadIdx.x] = static_cast<int>(shapes[2 * threadIdx.x + 1]);
+    sSt[threadIdx.x] = static_cast<int>(lsi[threadIdx.x]);
+  }
+  __syncthreads();
+  const int64_t pair = static_cast<int64_t>(blockIdx.x) * 64 + (threadIdx.x >> 2);
+  if (pair >= npairs) return;  // whole quads leave together
+  const int j = threadIdx.x & 3;
+  const int m = static_cast<int>(pair % M);
+  const int n = static_cast<int>(pair / M / Lq);
+  const int rsb = M * D * 4;
+  const char* vbytes = reinterpret_cast<const char*>(value);
+  const float* lp = loc + pair * L * P * 2;
+  const float* ap = attn + pair * L * P;
+  const unsigned cjb = 16u * j;
+  f4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  for (int l = 0; l < L; ++l) {
+    const int H = sH[l], W = sW[l];
+    const int obase = ((n * S + sSt[l]) * M + m) * D * 4;
+    const float2 xy = *reinterpret_cast<const float2*>(lp + 2 * (l * P + j));
+    const QuadPoint k = quad_point(xy.y * H - 0.5f, xy.x * W - 0.5f, H, W, obase, rsb);
+    quad_level_fwd(vbytes, k, ap[l * P + j], cjb, acc0, acc1);
+  }
+  float* o = out + pair * D + 4 * j;
+  *reinterpret_cast<f4*>(o) = acc0;
+  *reinterpret_cast<f4*>(o + 16) = acc1;
+}
+
+template <int LT>
+__global__ void __launch_bounds__(256) msda_fused_fwd_q4(const float* __restrict__ value, FrontEnd fe, TileGeom geo,
+                                                         int S, int M, float* __restrict__ out) {
+  constexpr int D = 32, P = 4, LP = LT * P;
+  static_assert(P == 4, "one quad lane per point");
+  const int qd = threadIdx.x >> 2, j = threadIdx.x & 3;
+  int b = blockIdx.x;
+  const int m = b % M;
+  b /= M;
+  int T = 0;
+#pragma unroll
+  for (int l = 0; l < LT; ++l) T += ((geo.H[l] + 7) >> 3) * ((geo.W[l] + 7) >> 3);
+  const int n = b / T;
+  int t = b - n * T, lv = 0;
+#pragma unroll
+  for (int l = 0; l < LT - 1; ++l) {
+    const int nt = ((geo.H[l] + 7) >> 3) * ((geo.W[l] + 7) >> 3);
+    if (lv == l && t >= nt) { t -= nt; lv = l + 1; }
+  }
+  const int Hq = geo.H[lv], Wq = geo.W[lv], tlx = (Wq + 7) >> 3;
+  const int y = (t / tlx) * 8 + (qd >> 3), x = (t % tlx) * 8 + (qd & 7);
+  if (y >= Hq || x >= Wq) return;  // whole quads leave together
+  const int q = geo.start[lv] + y * Wq + x;
+  const int64_t nq = static_cast<int64_t>(n) * S + q;
+  const int rsb = M * D * 4;  // value row stride in bytes
+  const char* vbytes = reinterpret_cast<const char*>(value);
+  const float* prow = fe.proj + nq * fe.ld;
+  const float* rrow = fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * LT * 2;
+  // softmax over the pair's L*P logits (ms_deform_attn.py:103-104): lane j exps logit l*P + j of every level,
+  // the quad max is exact, and every lane sums the exps in logit order (the sequential sum the backward
+  // recomputes, msda_bwd_f32_tiled), so the attention weights are bit-identical to the other kernels'
+  const float* lg = prow + M * LP * 2 + m * LP;
+  float e[LT];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int l = 0; l < LT; ++l) { e[l] = lg[l * P + j]; mx = fmaxf(mx, e[l]); }
+  mx = fmaxf(mx, qpermf<0xB1>(mx));
+  mx = fmaxf(mx, qpermf<0x4E>(mx));
+  float sum = 0.f;
+#pragma unroll
+  for (int l = 0; l < LT; ++l) {
+    e[l] = expf(e[l] - mx);
+    sum += qpermf<0x00>(e[l]);
+    sum += qpermf<0x55>(e[l]);
+    sum += qpermf<0xAA>(e[l]);
+    sum += qpermf<0xFF>(e[l]);
+  }
+  const float inv = 1.f / sum;
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  f4 acc0 = z, acc1 = z;
+  const unsigned cjb = 16u * j;  // this lane's channel bytes within a row half
+  auto level = [&](int l, auto pow2) {
+    constexpr bool POW2 = decltype(pow2)::value;
+    const int H = geo.H[l], W = geo.W[l];
+    const int obase = ((n * S + geo.start[l]) * M + m) * D * 4;
+    const float2 rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
+    const float2 off = *reinterpret_cast<const float2*>(prow + (m * LP + l * P + j) * 2);
+    const float sx = rf.x + div_norm(off.x, static_cast<float>(W), geo.invW[l], POW2);
+    const float sy = rf.y + div_norm(off.y, static_cast<float>(H), geo.invH[l], POW2);
+    // this lane's point: corner byte offsets and weights (a corner outside the level weighted 0: its clamped row
+    // is another corner of the same sample), times the attention weight
+    const QuadPoint k = quad_point(sy * H - 0.5f, sx * W - 0.5f, H, W, obase, rsb);
+    quad_level_fwd(vbytes, k, e[l] * inv, cjb, acc0, acc1);
+  };
+#pragma unroll
+  for (int l = 0; l < LT; ++l) {
+    if (((geo.W[l] & (geo.W[l] - 1)) | (geo.H[l] & (geo.H[l] - 1))) == 0) level(l, std::true_type{});
+    else level(l, std::false_type{});
+  }
+  float* o = out + (nq * M + m) * D + 4 * j;
+  *reinterpret_cast<f4*>(o) = acc0;
+  *reinterpret_cast<f4*>(o + 16) = acc1;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------------
 
@@ -1091,6 +1400,10 @@ int fwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
   if constexpr (std::is_same<T, float>::value) {
     if (fast_f32_ok(d, value, loc, out)) {
       if (d.D == 16) launch_fwd_vec<16>(value, shapes, lsi, loc, attn, d, out, st);
+      else if (d.D == 32 && d.P == 4 && m2f::option(m2f::kOptMsdaFwdQuad, 1) != 0 &&
+               static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 < (int64_t{1} << 31))
+        msda_fwd_f32_q4<<<m2f::ceil_div(d.npairs(), 64), 256, 0, st>>>(value, shapes, lsi, loc, attn, d.npairs(), d.S,
+                                                                        d.M, d.L, d.Lq, out);
       else if (d.D == 32) launch_fwd_vec<32>(value, shapes, lsi, loc, attn, d, out, st);
       else launch_fwd_vec<64>(value, shapes, lsi, loc, attn, d, out, st);
       done = true;
@@ -1127,6 +1440,8 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     // more pixels would silently wrap, so such shapes take the untiled kernels
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] >= (int64_t{1} << 24)) return false;
     geo.start[l] = static_cast<int>(total);
+    geo.invW[l] = 1.f / static_cast<float>(geo.W[l]);
+    geo.invH[l] = 1.f / static_cast<float>(geo.H[l]);
     total += static_cast<int64_t>(geo.H[l]) * geo.W[l];
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
@@ -1157,7 +1472,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   const size_t ns = static_cast<size_t>(qt) * lp;
   lds = (static_cast<size_t>(qt) * 32 + ((ns * 3 + 3) & ~static_cast<size_t>(3)) + (threads / 64) * kStageFloats) * 4 +
         ((static_cast<size_t>(geo.max_rows) + 1 + 3) & ~static_cast<size_t>(3)) * 4 + (((ns + 31) / 32 + 3) & ~static_cast<size_t>(3)) * 4 +
-        ns * 2;
+        (ns + 4) * 4;
   return lds <= 156 * 1024;
 }
 
@@ -1166,12 +1481,20 @@ void launch_tiled_t(const float* value, const float* loc, const float* attn, con
                     const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, hipStream_t st) {
   static bool attr = false;  // one flag per instantiation
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     attr = true;
   }
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
-  msda_bwd_f32_tiled<LT, FUSED, TPB><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+  // quad phase 2: 32-bit byte offsets into value / grad_value
+  const bool quad = m2f::option(m2f::kOptMsdaBwdQuad, 1) != 0 &&
+                    static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 < (int64_t{1} << 31);
+  if (quad)
+    msda_bwd_f32_tiled<LT, FUSED, TPB, true><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+  else
+    msda_bwd_f32_tiled<LT, FUSED, TPB, false><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
 }
 
 template <int LT, bool FUSED>
@@ -1313,6 +1636,8 @@ int fused_check(const char* fn, const float* value, const float* proj, int ld, c
     geo.W[l] = static_cast<int>(host_shapes[2 * l + 1]);
     if (geo.H[l] <= 0 || geo.W[l] <= 0) return m2f::fail(M2F_EINVAL, "%s: bad level shape", fn);
     geo.start[l] = static_cast<int>(total);
+    geo.invW[l] = 1.f / static_cast<float>(geo.W[l]);
+    geo.invH[l] = 1.f / static_cast<float>(geo.H[l]);
     total += static_cast<int64_t>(geo.H[l]) * geo.W[l];
   }
   if (total != d.S) return m2f::fail(M2F_EINVAL, "%s: sum of H*W (%lld) != spatial_size (%d)", fn,
@@ -1336,6 +1661,22 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
   hipStream_t st = static_cast<hipStream_t>(stream);
   // value and out hold N * Lq(=S) * M * 32 elements; 32-bit offsets when those fit
   const bool off32 = static_cast<int64_t>(d.N) * std::max(d.S, d.Lq) * d.M * d.D < (int64_t{1} << 31);
+  // quad form: byte offsets in 32-bit int arithmetic (value bytes < 2^31)
+  const bool boff31 = static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 < (int64_t{1} << 31);
+  if (boff31 && d.Lq == d.S && m2f::option(m2f::kOptMsdaFwdQuad, 1) != 0 && m2f::option(m2f::kOptMsdaFwdTiled, 1) != 0) {
+    int64_t T = 0;
+    for (int l = 0; l < d.L; ++l) T += static_cast<int64_t>((geo.H[l] + 7) / 8) * ((geo.W[l] + 7) / 8);
+    const int64_t nb = T * d.M * d.N;
+    if (nb > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many workgroups", fn);
+    const unsigned tg = static_cast<unsigned>(nb);
+    switch (d.L) {
+      case 1: msda_fused_fwd_q4<1><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output); break;
+      case 2: msda_fused_fwd_q4<2><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output); break;
+      case 3: msda_fused_fwd_q4<3><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output); break;
+      default: msda_fused_fwd_q4<4><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output); break;
+    }
+    return m2f::check_launch(fn);
+  }
   if (m2f::option(m2f::kOptMsdaFwdTiled, 1) != 0 && d.Lq == d.S) {
     int64_t T = 0;
     for (int l = 0; l < d.L; ++l) T += static_cast<int64_t>((geo.H[l] + 3) / 4) * ((geo.W[l] + 7) / 8);
@@ -1432,9 +1773,9 @@ extern "C" int m2f_diag_msda_bwd_stamps_f32(const float* value, const float* loc
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
 #define M2F_DIAG_LAUNCH(TPB, NF)                                                                                  \
   do {                                                                                                           \
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, TPB, true, NF>),      \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, TPB, true, true, NF>),      \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);                    \
-    msda_bwd_f32_tiled<3, false, TPB, true, NF><<<grid, TPB, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, \
+    msda_bwd_f32_tiled<3, false, TPB, true, true, NF><<<grid, TPB, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, \
                                                                        geo, d.S, d.M, grad_value, grad_loc,     \
                                                                        grad_attn, stamps);                      \
   } while (0)

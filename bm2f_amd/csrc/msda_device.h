@@ -7,6 +7,7 @@
 namespace m2f_msda {
 
 using f4 = float __attribute__((ext_vector_type(4)));
+using f2 = float __attribute__((ext_vector_type(2)));
 
 // ------------------------------------------------------------------------------------------------
 // fp32 fast path: G = D/4 lanes per (n,q,m) pair, float4 per lane.
@@ -97,6 +98,7 @@ struct TileGeom {
   int max_rows;   // list-head cells per workgroup (the window grid extended by one row / column)
   int max_halo;   // windows never extend more than this many pixels past the tile
   int max_qt;     // queries of the largest tile (sizes the LDS carve-up)
+  float invW[kTileMaxL], invH[kTileMaxL];  // 1 / W, 1 / H (used where they are powers of two: exact)
 };
 
 __device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }
@@ -130,6 +132,69 @@ __device__ __forceinline__ float max8_dpp(float v) {
   v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false)));
   v = fmaxf(v, __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false)));
   return v;
+}
+
+// DPP quad_perm moves with bound_ctrl (every lane of a quad reads a lane of its own quad, so no "old" operand);
+// CTRL = p * 0x55 broadcasts quad lane p, 0xB1 / 0x4E exchange with lane xor 1 / xor 2
+template <int CTRL>
+__device__ __forceinline__ int qpermi(int v) { return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, true); }
+template <int CTRL>
+__device__ __forceinline__ float qpermf(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+
+// 16 bytes at a 32-bit byte offset from base (global_load with an SGPR base and a 32-bit VGPR offset)
+__device__ __forceinline__ f4 ldb4(const char* base, unsigned boff) {
+  return *reinterpret_cast<const f4*>(base + boff);
+}
+
+// One sampling point's bilinear geometry for the quad kernels, in 32-bit BYTE offsets (value bytes < 2^31):
+// corner byte offsets (rows clamped into the level, so every load stays inside it) and the four bilinear weights
+// with a corner outside the level weighted 0.  (h, w) = (loc_y * H - 0.5, loc_x * W - 0.5); a point outside
+// (-1, H) x (-1, W) (NaN included) is moved to (-2, -2), where every corner lies outside (weights 0, ok false).
+// The clamps run on the floored floats (v_med3_f32 takes the SGPR bound; the integer form needs two ops).
+// a * b + c on the 24-bit multiplier (operands < 2^24, result < 2^32): LLVM turns __umul24(a, b) + c into
+// v_mad_u64_u32, a multi-pass instruction
+__device__ __forceinline__ int mad_u24(int a, int b, int c) {
+  int r;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+struct QuadPoint {
+  int o1, o2, o3, o4;
+  float w1, w2, w3, w4;
+  float ly, lx;
+  bool c1, c2, c3, c4;  // corner inside the level
+  bool ok;
+};
+
+__device__ __forceinline__ QuadPoint quad_point(float h, float w, int H, int W, int lbase, int rsb) {
+  QuadPoint k;
+  const float fHm1 = static_cast<float>(H - 1), fWm1 = static_cast<float>(W - 1);
+  k.ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
+  const float hs = k.ok ? h : -2.f, ws = k.ok ? w : -2.f;
+  const float fh = floorf(hs), fw = floorf(ws);
+  const float ly = hs - fh, lx = ws - fw, hy = 1.f - ly, hx = 1.f - lx;
+  const bool vy0 = fh >= 0.f, vy1 = fh < fHm1, vx0 = fw >= 0.f, vx1 = fw < fWm1;
+  const int y0 = static_cast<int>(__builtin_amdgcn_fmed3f(fh, 0.f, fHm1));
+  const int x0 = static_cast<int>(__builtin_amdgcn_fmed3f(fw, 0.f, fWm1));
+  k.o1 = mad_u24(mad_u24(y0, W, x0), rsb, lbase);
+  const int dx = (vx0 && vx1) ? rsb : 0, dy = (vy0 && vy1) ? W * rsb : 0;
+  k.o2 = k.o1 + dx;
+  k.o3 = k.o1 + dy;
+  k.o4 = k.o3 + dx;
+  k.c1 = vy0 && vx0;
+  k.c2 = vy0 && vx1;
+  k.c3 = vy1 && vx0;
+  k.c4 = vy1 && vx1;
+  k.w1 = k.c1 ? hy * hx : 0.f;
+  k.w2 = k.c2 ? hy * lx : 0.f;
+  k.w3 = k.c3 ? ly * hx : 0.f;
+  k.w4 = k.c4 ? ly * lx : 0.f;
+  k.ly = ly;
+  k.lx = lx;
+  return k;
 }
 
 __device__ __forceinline__ float pick4(const f4& v, int c) {

@@ -185,12 +185,14 @@ def _pyramid_case(shapes, N, M, far_frac, seed):
 
 @pytest.mark.parametrize("tile,rows,halo", [(16, 2304, 8), (12, 2304, 8), (8, 480, 8), (4, 64, 2), (8, 200, 0),
                                            (6, 2304, 12), (16, 700, 8)])
-def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo):
+@pytest.mark.parametrize("quad", [1, 0])
+def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, quad):
     """The tiled backward over tile / cell-budget / halo geometries (m2f_set_option msda_*: geometry only), on a
     non-square pyramid whose tiles do not divide every level evenly, 5 % of the samples thrown far (the
-    direct-atomic path), against the C oracle and the untiled kernel."""
+    direct-atomic path), against the C oracle and the untiled kernel; phase 2 in its quad form (msda_bwd_quad 1,
+    the default) and its 8-lane form."""
     from bm2f_amd import _native, msda
-    with _native.options(msda_tile=tile, msda_win_rows=rows, msda_halo=halo):
+    with _native.options(msda_tile=tile, msda_win_rows=rows, msda_halo=halo, msda_bwd_quad=quad):
         _tiled_backward_case(device, tile, rows)
 
 
@@ -219,17 +221,19 @@ def _tiled_backward_case(device, tile, rows):
     torch.testing.assert_close(gl, gl2, rtol=1e-4, atol=1e-6 * gl2.abs().max().item())
 
 
-def test_tiled_backward_nonfinite_and_zero_grads(device):
-    """A workgroup whose grad bound is 0 or non-finite must fall back to plain atomics: NaN/inf in
-    grad_output propagate into grad_value exactly as the reference's atomics would."""
-    from bm2f_amd import msda
+@pytest.mark.parametrize("quad", [1, 0])
+def test_tiled_backward_nonfinite_and_zero_grads(device, quad):
+    """NaN in grad_output propagates into grad_value exactly where the reference's atomics put it, and zero
+    grad_output rows give zeros, in both phase-2 forms of the tiled backward."""
+    from bm2f_amd import _native, msda
     shapes = [(4, 4), (8, 8), (16, 16)]
     value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 1, 8, 0.0, 7)
     gout[:, :16] = 0.0
     gout[0, 100, 5] = float("nan")
     dst = msda.attach_host_shapes(st.to(device), shapes)
-    gv, gl, ga = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
-                                             attn.to(device), gout.to(device), 64)
+    with _native.options(msda_bwd_quad=quad):
+        gv, gl, ga = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
+                                                 attn.to(device), gout.to(device), 64)
     wv, wl, wa = msda_ref.msda_backward(value.double(), st, lsi, loc.double(), attn.double(), gout.double())
     got, want = gv.cpu().double().numpy(), wv
     assert np.array_equal(np.isnan(got), np.isnan(want))
@@ -237,7 +241,8 @@ def test_tiled_backward_nonfinite_and_zero_grads(device):
     np.testing.assert_allclose(got[fin], want[fin], rtol=1e-3, atol=1e-5 * np.abs(want[fin]).max())
 
 
-def test_forward_nonfinite_values_like_oracle(device):
+@pytest.mark.parametrize("quad", [0, 1])
+def test_forward_nonfinite_values_like_oracle(device, quad):
     """Both forwards (the reference-API op and the fused front end) read a corner outside the level from a
     clamped row and drop it by a zero weight, and drop a sample outside (-1, H) x (-1, W) by a select on its
     sum.  With non-finite values on every level's first pixel (where out-of-range samples are clamped) and
@@ -250,8 +255,10 @@ def test_forward_nonfinite_values_like_oracle(device):
     value[1, 40, 2, 7] = float("nan")
     dst = msda.attach_host_shapes(st.to(device), shapes)
     want = msda_ref.msda_forward(value.double(), st, lsi, loc.double(), attn.double())
-    got = msda.ms_deform_attn_forward(value.to(device), dst, lsi.to(device), loc.to(device), attn.to(device),
-                                      64).cpu().double().numpy().reshape(want.shape)
+    from bm2f_amd import _native
+    with _native.options(msda_fwd_quad=quad):
+        got = msda.ms_deform_attn_forward(value.to(device), dst, lsi.to(device), loc.to(device), attn.to(device),
+                                          64).cpu().double().numpy().reshape(want.shape)
     assert np.array_equal(np.isfinite(got), np.isfinite(want))
     fin = np.isfinite(want)
     np.testing.assert_allclose(got[fin], want[fin], rtol=1e-4, atol=1e-5 * np.abs(want[fin]).max())
@@ -267,7 +274,8 @@ def test_forward_nonfinite_values_like_oracle(device):
     off = (loc - ref[:, :, None, :, None, :]) * norm[None, None, None, :, None, :]
     logits = attn.reshape(N, S, M, L * P).log()
     proj = torch.cat([off.reshape(N, S, -1), logits.reshape(N, S, -1)], -1).contiguous()
-    out = msda.MSDeformAttnFusedFunction.apply(value.to(device), proj.to(device), ref.to(device), shapes, P)
+    with _native.options(msda_fwd_quad=quad):  # the quad form skips an out-of-range point by the exec mask
+        out = msda.MSDeformAttnFusedFunction.apply(value.to(device), proj.to(device), ref.to(device), shapes, P)
     # the fused path recomputes loc and attn (softmax of log attn, ref + off / (W, H)) in fp32: same
     # finite pattern as the oracle on the materialised tensors, values within the rounding of that round trip
     sm = torch.softmax(logits, -1).reshape(attn.shape)
@@ -315,3 +323,42 @@ def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
     torch.testing.assert_close(outs[0], outs[1], rtol=1e-4, atol=1e-5)
     for a, b in zip(grads[0], grads[1]):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-4 * max(b.abs().max().item(), 1e-6))
+
+
+@pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(5, 7), (10, 13), (20, 26)],
+                                    [(9, 17)], [(4, 4), (8, 8), (16, 16), (32, 32)], [(6, 10), (12, 20)]])
+@pytest.mark.parametrize("quad", [0, 1])
+def test_fused_forward_variants_vs_oracle(device, shapes, quad):
+    """The fused forward (m2f_msda_fused_fwd_f32) in its quad form (a lane quad per (query, head), point
+    geometry by DPP broadcast, out-of-range points skipped by the exec mask) and its 8-lane form, against the
+    C oracle on the loc / attn the reference front end derives from the same projection: power-of-two and odd
+    level shapes (tile edges), 1-4 levels, 5 % of the samples thrown far (out of the level and out of range)."""
+    from bm2f_amd import _native
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    from test_scale_gpu import _fused_case, _loc_attn
+    N, P = 2, 4
+    L = len(shapes)
+    value, proj, ref = _fused_case(shapes, N, 0.05, seed=21 + L)
+    S = value.shape[1]
+    rf = ref.float()[None, :, None, :].expand(N, S, L, 2).to(device)
+    with _native.options(msda_fwd_quad=quad):
+        out = MSDeformAttnFusedFunction.apply(value.to(device), proj.to(device), rf, tuple(shapes), P)
+    torch.cuda.synchronize()
+    loc, attn = _loc_attn(proj, ref, shapes)
+    st = torch.tensor(shapes, dtype=torch.int64)
+    lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
+    want = msda_ref.msda_forward(value.double(), st, lsi, loc, attn)
+    _close(out.cpu(), want)
+
+
+@pytest.mark.parametrize("shapes", [[(5, 7), (10, 13), (20, 26)], [(9, 17)], [(4, 4), (8, 8), (16, 16), (32, 32)],
+                                    [(6, 10), (12, 20)]])
+@pytest.mark.parametrize("quad", [1, 0])
+def test_fused_backward_variants_vs_oracle(device, shapes, quad):
+    """The fused backward (d offsets / d logits from the raw projection) in both phase-2 forms, 1-4 levels, odd
+    level shapes, 5 % of the samples thrown far (the out-of-window atomics of every lane of a quad), against the
+    C oracle: grad_value, d offsets (crossing entries one-sided) and d logits."""
+    from bm2f_amd import _native
+    from test_scale_gpu import fused_fwd_bwd_vs_oracle
+    with _native.options(msda_bwd_quad=quad, msda_fwd_quad=quad):
+        fused_fwd_bwd_vs_oracle(device, shapes, N=2, far=0.05, seed=31 + len(shapes))

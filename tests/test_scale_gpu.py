@@ -86,10 +86,16 @@ def _loc_attn(proj, ref, shapes, M=8, P=4):
 
 @pytest.mark.parametrize("variant,far", [("reference_init", 0.0), ("far5pct", 0.05)])
 def test_fused_msda_config2_pyramid_vs_oracle(device, variant, far):
+    fused_fwd_bwd_vs_oracle(device, SHAPES_1024, N=2, far=far, seed=11 if far else 0)
+
+
+def fused_fwd_bwd_vs_oracle(device, shapes, N, far, seed):
+    """MSDeformAttnFusedFunction fwd + bwd (the kernels bench.py times) against the C oracle on the loc / attn
+    the reference front end derives in fp64 from the same fp32 projection."""
     from bm2f_amd.msda import MSDeformAttnFusedFunction
-    shapes = SHAPES_1024
-    N, M, D, L, P = 2, 8, 32, 3, 4
-    value, proj, ref = _fused_case(shapes, N, far, seed=11 if far else 0)
+    M, D, P = 8, 32, 4
+    L = len(shapes)
+    value, proj, ref = _fused_case(shapes, N, far, seed=seed)
     S = value.shape[1]
     gout = torch.randn(N, S, M * D, generator=torch.Generator().manual_seed(5))
     # the kernels bench.py times, through the module's autograd Function, default environment

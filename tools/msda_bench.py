@@ -112,7 +112,13 @@ def main():
     ap.add_argument("--noise", type=float, default=1.0, help="px std of the offsets around the init rays")
     ap.add_argument("--bwd-only", action="store_true")
     ap.add_argument("--fused", action="store_true", help="the fused front-end kernels (the path the bench step runs)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="library option (m2f_set_option) for this run, repeatable; e.g. --opt msda_fwd_quad=0")
     a = ap.parse_args()
+    from bm2f_amd import _native
+    for kv in a.opt:
+        k, v_ = kv.split("=")
+        _native.set_option(k, int(v_))
     r = a.res
     shapes = [(r // 32, r // 32), (r // 16, r // 16), (r // 8, r // 8)]
     v, st, lsi, loc, attn, gout = make_inputs(a.n, shapes, stress=a.stress, noise=a.noise)
@@ -129,7 +135,7 @@ def main():
     tf = 0.0 if a.bwd_only else timeit(fwd, a.iters)
     tb = timeit(bwd, a.iters)
     tf = tf or float("nan")
-    print(f"N={a.n} res={r} fused={a.fused} stress={a.stress} noise={a.noise} : fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
+    print(f"N={a.n} res={r} fused={a.fused} opts={','.join(a.opt) or '-'} stress={a.stress} noise={a.noise} : fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
           f"bwd {tb:.3f} ms ({bwd_bytes / tb / 1e6:.0f} GB/s alg)")
 
 
