@@ -40,7 +40,7 @@ extern "C" int m2f_abi_version(void) { return 1; }
 namespace {
 constexpr const char* kOptionNames[m2f::kOptCount] = {
     "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
-    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_quad"};
+    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -356,6 +356,8 @@ struct TileState {
   int qc[kTileMaxL + 1], qy0[kTileMaxL], qx0[kTileMaxL], qw[kTileMaxL];
   int wsum[kMaxBwdWaves];    // block scan
   float iww[kTileMaxL];      // 1 / ww (phase 3's row -> window coordinates)
+  int H[kTileMaxL], W[kTileMaxL], start[kTileMaxL];  // the level shapes in LDS: a kernarg array indexed by a
+  float invW[kTileMaxL], invH[kTileMaxL];            // per-lane level is a global load per use
   int next_batch;            // phase-3 row batches handed out dynamically
 };
 
@@ -367,11 +369,12 @@ struct FrontEnd {
   int64_t ref_bs;      // batch stride of ref in elements (0 = broadcast)
 };
 
-__device__ __forceinline__ int tile_query(const TileState& ts, const TileGeom& geo, int qi) {
+// pyramid position of the tile's query qi (levels in order, rows of the tile's rectangle on each level)
+__device__ __forceinline__ int tile_query(const TileState& ts, int qi) {
   int lq = 0;
   while (qi >= ts.qc[lq + 1]) ++lq;
   const int r = qi - ts.qc[lq];
-  return geo.start[lq] + (ts.qy0[lq] + r / ts.qw[lq]) * geo.W[lq] + ts.qx0[lq] + r % ts.qw[lq];
+  return ts.start[lq] + (ts.qy0[lq] + r / ts.qw[lq]) * ts.W[lq] + ts.qx0[lq] + r % ts.qw[lq];
 }
 
 __device__ __forceinline__ int wave_incl_scan(int v, int lane) {
@@ -395,7 +398,7 @@ __device__ __forceinline__ int window_cell(const TileState& ts, int l, int h0, i
 // STAMP (diagnostic builds only, M2F_DIAG): s_memtime at the phase barriers of each workgroup into `stamps`;
 // NOFLUSH (diagnostic builds only): phase 3 without its HBM adds, to price them.
 // TPB threads per workgroup: 512 (two workgroups per CU, 12x12 tiles; the default) or 1024 (one, 16x16 tiles).
-template <int LT, bool FUSED, int TPB, bool QUAD = true, bool STAMP = false, bool NOFLUSH = false>
+template <int LT, bool FUSED, int TPB, bool OVERLAP = true, bool STAMP = false, bool NOFLUSH = false>
 __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
@@ -422,13 +425,14 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   const int rs = M * D;  // value row stride (elements); N*S*M*D < 2^31 is checked on the host
   const int nsamp_max = geo.max_qt * LP;
   // LDS carve-up (16-byte aligned pieces): g rows [max_qt][32] | desc [max_qt * LP][3] | stage [waves][264]
-  //   | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32 | slots [max_qt * LP + 4] u32
+  //   | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32 | slots [max_qt * LP + 4] u32 | qmap [max_qt] i32
   float* gsh = reinterpret_cast<float*>(lds_raw);
   float* desc = gsh + geo.max_qt * D;
   float* stage = desc + ((nsamp_max * 3 + 3) & ~3);
   int* cstart = reinterpret_cast<int*>(stage + kBwdWaves * kStageFloats);
   unsigned* oow = reinterpret_cast<unsigned*>(cstart + ((geo.max_rows + 1 + 3) & ~3));
   unsigned* slots = reinterpret_cast<unsigned*>(oow + (((nsamp_max + 31) / 32 + 3) & ~3));
+  int* qmap = reinterpret_cast<int*>(slots + nsamp_max + 4);  // pyramid position of each tile query
 
   M2F_STAMP(5)
   if (tid < LT) {
@@ -440,6 +444,8 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     ts.qw[l] = x1 - x0;
     ts.qc[l + 1] = (y1 - y0) * (x1 - x0);
     ts.bb[l][0] = 0x7fffffff; ts.bb[l][1] = -1; ts.bb[l][2] = 0x7fffffff; ts.bb[l][3] = -1;
+    ts.H[l] = geo.H[l]; ts.W[l] = geo.W[l]; ts.start[l] = geo.start[l];
+    ts.invW[l] = geo.invW[l]; ts.invH[l] = geo.invH[l];
   }
   for (int i = tid; i < (nsamp_max + 31) / 32; i += blockDim.x) oow[i] = 0u;
   if (tid == 0) ts.next_batch = kBwdWaves;
@@ -449,34 +455,24 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     for (int l = 0; l < LT; ++l) ts.qc[l + 1] += ts.qc[l];
   }
   __syncthreads();
-  M2F_STAMP(0)
   const int Qt = ts.qc[LT];
   const int nsamp = Qt * LP;
+  for (int qi = tid; qi < Qt; qi += blockDim.x) qmap[qi] = tile_query(ts, qi);
+  __syncthreads();
+  M2F_STAMP(0)
 
-  // ---- phase 0a: this head's grad_output rows of the tile's queries -> LDS (float4 per lane), the loads of
-  // a thread's rows issued together (a load-store loop waits out each load in turn) -----------------------
-  {
-    constexpr int kGPre = 3;  // max_qt * 8 <= 3 * TPB at the default geometries; the rest loops
-    f4 gpre[kGPre];
+  // ---- phase 0: this head's grad_output rows of the tile's queries -> LDS (float4 per lane); the sample
+  // descriptors (one lane per (query, level)) and the touched-corner boxes.  Every global load of the phase is
+  // issued before any of its math or LDS stores (the g rows, then both task rounds' projection rows), so the
+  // phase waits out one memory round trip instead of three ---------------------------------------------------
+  constexpr int kGPre = 3;  // max_qt * 8 <= 3 * TPB at the default geometries; the rest loops
+  f4 gpre[kGPre];
 #pragma unroll
-    for (int u = 0; u < kGPre; ++u) {
-      const int idx = min(tid + u * kBwdThreads, Qt * 8 - 1), qi = idx >> 3, j = idx & 7;
-      const int64_t pair = (static_cast<int64_t>(n) * S + tile_query(ts, geo, qi)) * M + m;
-      gpre[u] = ld4(gout + pair * D + 4 * j);
-    }
-#pragma unroll
-    for (int u = 0; u < kGPre; ++u) {
-      const int idx = tid + u * kBwdThreads;
-      if (idx < Qt * 8) *reinterpret_cast<f4*>(gsh + (idx >> 3) * D + 4 * (idx & 7)) = gpre[u];
-    }
-    for (int idx = tid + kGPre * kBwdThreads; idx < Qt * 8; idx += kBwdThreads) {
-      const int qi = idx >> 3, j = idx & 7;
-      const int64_t pair = (static_cast<int64_t>(n) * S + tile_query(ts, geo, qi)) * M + m;
-      *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = ld4(gout + pair * D + 4 * j);
-    }
+  for (int u = 0; u < kGPre; ++u) {
+    const int idx = min(tid + u * kBwdThreads, Qt * 8 - 1), qi = idx >> 3, j = idx & 7;
+    const int64_t pair = (static_cast<int64_t>(n) * S + qmap[qi]) * M + m;
+    gpre[u] = ld4(gout + pair * D + 4 * j);
   }
-
-  // ---- phase 0b: sample descriptors (one lane per (query, level)) and the touched-corner boxes --------
   {
     int bmin_y[LT], bmax_y[LT], bmin_x[LT], bmax_x[LT];
 #pragma unroll
@@ -486,21 +482,44 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     // the sum is carried from lane to lane in logit order (the sequential sum the forward forms)
     constexpr int TPQ = FUSED ? 4 : LT;  // tasks per query
     static_assert(!FUSED || LT <= 4, "one quad lane per level");
-    for (int t = tid; t < Qt * TPQ; t += blockDim.x) {  // whole quads enter and leave together
+    const int ntask = Qt * TPQ;
+    struct TaskIn {
+      float x[P];      // logits (FUSED) or attention weights
+      float2 xy[P];    // offsets (FUSED) or sampling locations
+      float2 rf;       // reference point (FUSED)
+    };
+    auto task_load = [&](int t) {
+      TaskIn in;
+      t = min(t, ntask - 1);  // a spare round's addresses stay in range (its results are dropped)
+      const int qi = t / TPQ, lt = t - qi * TPQ;
+      const int l = lt < LT ? lt : LT - 1;
+      const int64_t nq = static_cast<int64_t>(n) * S + qmap[qi];
+      if constexpr (FUSED) {
+        const float* prow = fe.proj + nq * fe.ld;
+        const float* lg = prow + M * LP * 2 + m * LP + l * P;
+        const float* of = prow + (m * LP + l * P) * 2;
+#pragma unroll
+        for (int p = 0; p < P; ++p) { in.x[p] = lg[p]; in.xy[p] = *reinterpret_cast<const float2*>(of + 2 * p); }
+        in.rf = *reinterpret_cast<const float2*>(fe.ref + n * fe.ref_bs + (static_cast<int64_t>(qmap[qi]) * LT + l) * 2);
+      } else {
+        const int64_t kb = (nq * M + m) * LP + l * P;
+#pragma unroll
+        for (int p = 0; p < P; ++p) { in.xy[p] = *reinterpret_cast<const float2*>(loc + 2 * (kb + p)); in.x[p] = attn[kb + p]; }
+        in.rf = make_float2(0.f, 0.f);
+      }
+      return in;
+    };
+    auto task_run = [&](int t, TaskIn& in) {  // whole quads run it together
       const int qi = t / TPQ, lt = t - qi * TPQ;
       const bool act = lt < LT;
       const int l = act ? lt : LT - 1;  // a spare quad lane mirrors the last level (its results are dropped)
-      const int q = tile_query(ts, geo, qi);
-      const int64_t nq = static_cast<int64_t>(n) * S + q;
-      const int H = geo.H[l], W = geo.W[l];
+      const int H = ts.H[l], W = ts.W[l];
       float av[P], lx[P], ly[P];
       if constexpr (FUSED) {
-        const float* prow = fe.proj + nq * fe.ld;
-        const float* lg = prow + M * LP * 2 + m * LP;
-        float x[P];
+        float* x = in.x;
         float mx = -INFINITY;
 #pragma unroll
-        for (int p = 0; p < P; ++p) { x[p] = lg[l * P + p]; mx = fmaxf(mx, x[p]); }
+        for (int p = 0; p < P; ++p) mx = fmaxf(mx, x[p]);
         mx = fmaxf(mx, qperm<0xB1>(mx));  // quad lanes 1 0 3 2
         mx = fmaxf(mx, qperm<0x4E>(mx));  // quad lanes 2 3 0 1
 #pragma unroll
@@ -530,33 +549,24 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           default: sum = qperm<0xFF>(run); break;
         }
         const float inv = 1.f / sum;
-        const float2 rf = *reinterpret_cast<const float2*>(fe.ref + n * fe.ref_bs + (static_cast<int64_t>(q) * LT + l) * 2);
-        const float* of = prow + (m * LP + l * P) * 2;
         const float fW = static_cast<float>(W), fH = static_cast<float>(H);
-        const float iW = 1.f / fW, iH = 1.f / fH;
+        const float iW = ts.invW[l], iH = ts.invH[l];
         auto points = [&](auto pow2) {  // as msda_fused_fwd: exact reciprocals when W and H are powers of two
           constexpr bool POW2 = decltype(pow2)::value;
 #pragma unroll
           for (int p = 0; p < P; ++p) {
-            const float2 off = *reinterpret_cast<const float2*>(of + 2 * p);
-            lx[p] = rf.x + div_norm(off.x, fW, iW, POW2);
-            ly[p] = rf.y + div_norm(off.y, fH, iH, POW2);
+            lx[p] = in.rf.x + div_norm(in.xy[p].x, fW, iW, POW2);
+            ly[p] = in.rf.y + div_norm(in.xy[p].y, fH, iH, POW2);
             av[p] = x[p] * inv;
           }
         };
         if (((W & (W - 1)) | (H & (H - 1))) == 0) points(std::true_type{});
         else points(std::false_type{});
       } else {
-        const int64_t kb = (nq * M + m) * LP + l * P;
 #pragma unroll
-        for (int p = 0; p < P; ++p) {
-          const float2 xy = *reinterpret_cast<const float2*>(loc + 2 * (kb + p));
-          lx[p] = xy.x;
-          ly[p] = xy.y;
-          av[p] = attn[kb + p];
-        }
+        for (int p = 0; p < P; ++p) { lx[p] = in.xy[p].x; ly[p] = in.xy[p].y; av[p] = in.x[p]; }
       }
-      if (!act) continue;
+      if (!act) return;
       float* dq = desc + (qi * LP + l * P) * 3;
 #pragma unroll
       for (int p = 0; p < P; ++p) {
@@ -577,6 +587,24 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             }
         }
       }
+    };
+    // task rounds in pairs, both rounds' loads first (whole quads enter and leave together: ntask and the
+    // round stride are multiples of 4)
+    for (int t = tid; t < ntask; t += 2 * kBwdThreads) {
+      TaskIn i0 = task_load(t), i1 = task_load(t + kBwdThreads);
+      task_run(t, i0);
+      if (t + kBwdThreads < ntask) task_run(t + kBwdThreads, i1);
+    }
+    // the g rows -> LDS (their loads were issued first)
+#pragma unroll
+    for (int u = 0; u < kGPre; ++u) {
+      const int idx = tid + u * kBwdThreads;
+      if (idx < Qt * 8) *reinterpret_cast<f4*>(gsh + (idx >> 3) * D + 4 * (idx & 7)) = gpre[u];
+    }
+    for (int idx = tid + kGPre * kBwdThreads; idx < Qt * 8; idx += kBwdThreads) {
+      const int qi = idx >> 3, j = idx & 7;
+      const int64_t pair = (static_cast<int64_t>(n) * S + qmap[qi]) * M + m;
+      *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = ld4(gout + pair * D + 4 * j);
     }
     // per-level boxes over the wave, then over the workgroup
 #pragma unroll
@@ -640,7 +668,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         const float h = desc[3 * sid], w = desc[3 * sid + 1];
         if (h > -1.f) {  // ok sample
           const int l = (sid % LP) / P;
-          const int c = window_cell(ts, l, static_cast<int>(floorf(h)), static_cast<int>(floorf(w)), geo.H[l], geo.W[l]);
+          const int c = window_cell(ts, l, static_cast<int>(floorf(h)), static_cast<int>(floorf(w)), ts.H[l], ts.W[l]);
           if (c >= 0) {
             cell[r] = c;
             rank[r] = atomicAdd(cstart + c, 1);
@@ -680,28 +708,34 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   __syncthreads();
   M2F_STAMP(2)
 
-  // ---- phase 2: gather, grad_loc / grad_attn; out-of-window samples scatter with atomics ---------------
-  if constexpr (QUAD) {
-    // Quad form (the default).  The kernel is VALU-issue bound; in the 8-lane form every lane re-derives every
-    // sample's geometry and gradient math for a float4 of channels.  Here a quad of lanes takes one query, lane j
-    // owning channels 4j..4j+3 and 16+4j..16+4j+3 (one load address per corner row: the second half is the
-    // immediate offset).  Per level, lane j derives point j's geometry once; the quad takes the points in turn
-    // with the owner's corner byte offsets by DPP broadcast, each lane forming 16 partial channel dots (4 points x
-    // 4 corners) over its 8 channels; a two-stage quad transpose-reduce (xor 2, xor 1) leaves lane j the 4 full
-    // corner dots of ITS point, so the gradient math and the stores run once per point instead of once per lane.
+  // ---- phases 2 and 3: one work queue ----------------------------------------------------------------------
+  // Phase 2 (16 queries per unit) gathers the samples' corner rows through L1 (texture-path bound); phase 3 (16
+  // window rows per unit) walks the slot lists in LDS (LDS bound).  Neither reads what the other writes (phase 3
+  // derives its corner coefficients from the {h, w, a} descriptors), so with OVERLAP the units of both kinds are
+  // dealt from one LDS counter, interleaved, and the waves of a workgroup run both at once instead of one phase
+  // after a barrier.
+  {
+    const int rows_total = ts.roff[LT];
+    const int U2 = (Qt + 15) / 16, U3 = (rows_total + 15) / 16;
+    // phase 2, quad form: a quad of lanes takes one query, lane j owning channels 4j..4j+3 and 16+4j..16+4j+3
+    // (one load address per corner row: the second half is the immediate offset).  Per level, lane j derives
+    // point j's geometry once; the quad takes the points in turn with the owner's corner byte offsets by DPP
+    // broadcast, each lane forming 16 partial channel dots (4 points x 4 corners) over its 8 channels; a two-stage
+    // quad transpose-reduce (xor 2, xor 1) leaves lane j the 4 full corner dots of ITS point, so the gradient math
+    // and the stores run once per point.
     const int j = lane & 3, gq = lane >> 2;
     const unsigned cjb = 16u * j;
     const char* vbytes = reinterpret_cast<const char*>(value);
     char* gvbytes = reinterpret_cast<char*>(gvalue);
     const int rsb = rs * 4;  // value row stride in bytes; value bytes < 2^31 (host check)
-    for (int base = wid * 16; base < Qt; base += kBwdWaves * 16) {
-      const int qi = base + gq;
-      if (qi >= Qt) continue;  // whole quad (same qi) idles together
-      const int q = tile_query(ts, geo, qi);
+    auto phase2_unit = [&](int unit) {
+      const int qi = unit * 16 + gq;
+      if (qi >= Qt) return;  // whole quad (same qi) idles together
+      const int q = qmap[qi];
       const int64_t nq = static_cast<int64_t>(n) * S + q;
       const f4 gA = *reinterpret_cast<const f4*>(gsh + qi * D + 4 * j);
       const f4 gB = *reinterpret_cast<const f4*>(gsh + qi * D + 16 + 4 * j);
-      float* dq = desc + qi * LP * 3;
+      const float* dq = desc + qi * LP * 3;
       const int sid0 = qi * LP, sh = sid0 & 31;
       const unsigned w0f = oow[sid0 >> 5], w1f = oow[min((sid0 + LP - 1) >> 5, (nsamp_max + 31) / 32 - 1)];
       const unsigned qfar = (sh ? (w0f >> sh) | (w1f << (32 - sh)) : w0f) & ((1u << LP) - 1u);
@@ -712,7 +746,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         const int H = geo.H[l], W = geo.W[l];
         const int lbase = ((n * S + geo.start[l]) * M + m) * D * 4;
         // this lane's point (l, j)
-        float* dk = dq + 3 * (l * P + j);
+        const float* dk = dq + 3 * (l * P + j);
         const float h = dk[0], w = dk[1], a = dk[2];
         // not-ok samples carry h = w = -2 (every corner outside, ok false)
         const QuadPoint k = quad_point(h, w, H, W, lbase, rsb);
@@ -727,32 +761,40 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           t = __builtin_elementwise_fma(f2{vb.z, vb.w}, f2{gB.z, gB.w}, t);
           return t.x + t.y;
         };
-        // points in the batches {0, 2} and {1, 3} (16 corner loads each, issued before any of their math); after
-        // a batch the first transpose-reduce stage (xor 2) folds its 8 partial dots to 4: lanes {0, 1} keep the
-        // batch's lower point, lanes {2, 3} its upper point, summed over the lane pair
         const bool hi2 = (j & 2) != 0, hi1 = (j & 1) != 0;
         float s1[2][4];
-        auto batch = [&](auto c0, auto cc1, int pp) {
-          constexpr int C0 = decltype(c0)::value, C1 = decltype(cc1)::value;
-          f4 va[2][8];
+        // one point at a time (8 corner loads in flight per lane: the texture path, not latency, bounds this phase,
+        // and fewer registers keep the merged phase 2/3 loop free of spills); after the points {0, 2} and {1, 3} the
+        // first transpose-reduce stage (xor 2) folds their 8 partial dots to 4: lanes {0, 1} keep the lower point,
+        // lanes {2, 3} the upper one, summed over the lane pair
+        auto point_dots = [&](auto cc, float* part) {
+          constexpr int C = decltype(cc)::value;
           const char* vhi = vbytes + 64;  // the row's second half: an immediate offset
-          auto load = [&](f4* v, unsigned b1, unsigned b2, unsigned b3, unsigned b4) {
-            v[0] = ldb4(vbytes, b1); v[1] = ldb4(vhi, b1);
-            v[2] = ldb4(vbytes, b2); v[3] = ldb4(vhi, b2);
-            v[4] = ldb4(vbytes, b3); v[5] = ldb4(vhi, b3);
-            v[6] = ldb4(vbytes, b4); v[7] = ldb4(vhi, b4);
-          };
-          load(va[0], qpermi<C0>(o1) + cjb, qpermi<C0>(o2) + cjb, qpermi<C0>(o3) + cjb, qpermi<C0>(o4) + cjb);
-          load(va[1], qpermi<C1>(o1) + cjb, qpermi<C1>(o2) + cjb, qpermi<C1>(o3) + cjb, qpermi<C1>(o4) + cjb);
+          const unsigned b1 = qpermi<C>(o1) + cjb, b2 = qpermi<C>(o2) + cjb;
+          const unsigned b3 = qpermi<C>(o3) + cjb, b4 = qpermi<C>(o4) + cjb;
+          const f4 v0 = ldb4(vbytes, b1), v1 = ldb4(vhi, b1), v2 = ldb4(vbytes, b2), v3 = ldb4(vhi, b2);
+          const f4 v4 = ldb4(vbytes, b3), v5 = ldb4(vhi, b3), v6 = ldb4(vbytes, b4), v7 = ldb4(vhi, b4);
+          part[0] = dot8(v0, v1);
+          part[1] = dot8(v2, v3);
+          part[2] = dot8(v4, v5);
+          part[3] = dot8(v6, v7);
+        };
+        auto stage1 = [&](const float* plo, const float* phi, float* out) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            const float plo = dot8(va[0][2 * c], va[0][2 * c + 1]), phi = dot8(va[1][2 * c], va[1][2 * c + 1]);
-            const float lo = plo + qpermf<0x4E>(plo), hi = phi + qpermf<0x4E>(phi);
-            s1[pp][c] = hi2 ? hi : lo;
+            const float lo = plo[c] + qpermf<0x4E>(plo[c]), hi = phi[c] + qpermf<0x4E>(phi[c]);
+            out[c] = hi2 ? hi : lo;
           }
         };
-        batch(std::integral_constant<int, 0x00>{}, std::integral_constant<int, 0xAA>{}, 0);  // points 0, 2
-        batch(std::integral_constant<int, 0x55>{}, std::integral_constant<int, 0xFF>{}, 1);  // points 1, 3
+        {
+          float pa_[4], pb_[4];
+          point_dots(std::integral_constant<int, 0x00>{}, pa_);
+          point_dots(std::integral_constant<int, 0xAA>{}, pb_);
+          stage1(pa_, pb_, s1[0]);
+          point_dots(std::integral_constant<int, 0x55>{}, pa_);
+          point_dots(std::integral_constant<int, 0xFF>{}, pb_);
+          stage1(pa_, pb_, s1[1]);
+        }
         // second stage (xor 1): lane j holds the full corner dots of point j
         float dd[4];
 #pragma unroll
@@ -808,11 +850,6 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           scatter(std::integral_constant<int, 0xAA>{}, 2);
           scatter(std::integral_constant<int, 0xFF>{}, 3);
         }
-        // the point's descriptor becomes phase 3's corner-coefficient form {(1 - ly) a, ly a, lx} (only this lane
-        // reads it in phase 2)
-        dk[0] = hy * a;
-        dk[1] = ly * a;
-        dk[2] = lx;
       }
       if constexpr (FUSED) {
         // softmax backward over the pair's L*P logits: d logit_k = a_k (d a_k - sum_i a_i d a_i)
@@ -822,144 +859,16 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
 #pragma unroll
         for (int l = 0; l < LT; ++l) gl[l * P + j] = aown[l] * (gaown[l] - dot);
       }
-    }
-  } else {
-    const int j = lane & 7, gq = lane >> 3;
-    const f4 z = {0.f, 0.f, 0.f, 0.f};
-    for (int base = wid * 8; base < Qt; base += kBwdWaves * 8) {
-      const int qi = base + gq;
-      if (qi >= Qt) continue;  // whole lane group (same qi) idles together
-      const int q = tile_query(ts, geo, qi);
-      const int64_t nq = static_cast<int64_t>(n) * S + q;
-      const f4 g = *reinterpret_cast<const f4*>(gsh + qi * D + 4 * j);
-      const float* dq = desc + qi * LP * 3;
-      float dot = 0.f, myga0 = 0.f, myga1 = 0.f;
-      // the query's out-of-window flags (LP <= 16 bits) from the two words they can straddle, read once
-      const int sid0 = qi * LP, sh = sid0 & 31;
-      const unsigned w0 = oow[sid0 >> 5], w1 = oow[min((sid0 + LP - 1) >> 5, (nsamp_max + 31) / 32 - 1)];
-      const unsigned qfar = (sh ? (w0 >> sh) | (w1 << (32 - sh)) : w0) & ((1u << LP) - 1u);
-#pragma unroll 1
-      for (int l = 0; l < LT; ++l) {
-        const int H = geo.H[l], W = geo.W[l];
-        const int lbase = ((n * S + geo.start[l]) * M + m) * D + 4 * j;
-        const int Wrs = W * rs;
-        float st_l = 0.f, st_a = 0.f;
-        // points in batches of PB: every corner load of a batch is issued before any of its math
-        constexpr int PB = 2;
-#pragma unroll
-        for (int p0 = 0; p0 < P; p0 += PB) {
-          f4 vb[PB][4];
-          float hh[PB], wwf[PB], aa[PB];
-          int h0s[PB], w0s[PB];
-#pragma unroll
-          for (int pp = 0; pp < PB; ++pp) {
-            const int k = l * P + p0 + pp;
-            hh[pp] = dq[3 * k]; wwf[pp] = dq[3 * k + 1]; aa[pp] = dq[3 * k + 2];
-            const int h0 = static_cast<int>(floorf(hh[pp])), w0 = static_cast<int>(floorf(wwf[pp]));
-            h0s[pp] = h0; w0s[pp] = w0;
-            const int y0 = min(max(h0, 0), H - 1), y1 = min(max(h0 + 1, 0), H - 1);
-            const int x0 = min(max(w0, 0), W - 1), x1 = min(max(w0 + 1, 0), W - 1);
-            // one multiply per sample: corners 2-4 are 0 / 1 pixel right and 0 / 1 row down of corner 1
-            const int o1 = lbase + static_cast<int>(__umul24(__umul24(y0, W) + x0, rs));  // 24-bit products
-            const int dx = x1 != x0 ? rs : 0, dy = y1 != y0 ? Wrs : 0;
-            vb[pp][0] = ld4(value + o1);
-            vb[pp][1] = ld4(value + o1 + dx);
-            vb[pp][2] = ld4(value + o1 + dy);
-            vb[pp][3] = ld4(value + o1 + dy + dx);
-          }
-#pragma unroll
-          for (int pp = 0; pp < PB; ++pp) {
-            const int p = p0 + pp;
-            const int k = l * P + p;
-            const int h0 = h0s[pp], w0 = w0s[pp];
-            const float a = aa[pp];
-            const bool ok = hh[pp] > -1.f;  // not-ok samples carry h = w = -2
-            const float ly = hh[pp] - static_cast<float>(h0), lx = wwf[pp] - static_cast<float>(w0);
-            const float hy = 1.f - ly, hx = 1.f - lx;
-            const bool c1 = h0 >= 0 && w0 >= 0, c2 = h0 >= 0 && w0 + 1 <= W - 1;
-            const bool c3 = h0 + 1 <= H - 1 && w0 >= 0, c4 = h0 + 1 <= H - 1 && w0 + 1 <= W - 1;
-            // per-corner channel dots with g, summed over the group; everything else is scalar.  A corner
-            // outside the level contributes nothing (as the reference, which skips it): its (clamped, in-level)
-            // row is loaded unconditionally and its reduced dot is selected away -- one select per corner, not
-            // four on the loaded vector, and no branch (a branch here makes the compiler sink the load into it)
-            auto dot4 = [&](const f4& v) { return fmaf(g.w, v.w, fmaf(g.z, v.z, fmaf(g.y, v.y, g.x * v.x))); };
-            const float r1 = sum8_dpp(dot4(vb[pp][0])), r2 = sum8_dpp(dot4(vb[pp][1]));
-            const float r3 = sum8_dpp(dot4(vb[pp][2])), r4 = sum8_dpp(dot4(vb[pp][3]));
-            const float d1 = c1 ? r1 : 0.f, d2 = c2 ? r2 : 0.f, d3 = c3 ? r3 : 0.f, d4 = c4 ? r4 : 0.f;
-            const float pa = (hy * hx) * d1 + (hy * lx) * d2 + (ly * hx) * d3 + (ly * lx) * d4;
-            const float px = a * (hy * (d2 - d1) + ly * (d4 - d3));
-            const float py = a * (hx * (d3 - d1) + lx * (d4 - d2));
-            // lane p stores grad_attn of point p; lanes 2p, 2p+1 its grad_loc pair (one store per level)
-            if constexpr (FUSED) {
-              const float gak = ok ? pa : 0.f;
-              dot += a * gak;
-              if (k == j) myga0 = gak;
-              if (k == j + 8) myga1 = gak;
-              if ((j >> 1) == p) st_l = ok ? ((j & 1) ? py : px) : 0.f;
-            } else {
-              if (j == p) st_a = ok ? pa : 0.f;
-              if ((j >> 1) == p) st_l = ok ? ((j & 1) ? H * py : W * px) : 0.f;
-            }
-            if (ok && ((qfar >> k) & 1u)) {
-              // outside the window: the 4 corner rows go straight to HBM (fp32 atomics, as the reference)
-              const f4 tg = g * a;
-              const int o1 = lbase + (min(max(h0, 0), H - 1) * W + min(max(w0, 0), W - 1)) * rs;
-              const int dx = rs, dy = W * rs;
-              if (c1) { const f4 t = (hy * hx) * tg; float* o = gvalue + o1; atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w); }
-              if (c2) { const f4 t = (hy * lx) * tg; float* o = gvalue + o1 + (c1 ? dx : 0); atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w); }
-              if (c3) { const f4 t = (ly * hx) * tg; float* o = gvalue + o1 + (c1 ? dy : 0); atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w); }
-              if (c4) { const f4 t = (ly * lx) * tg; float* o = gvalue + lbase + ((h0 + 1) * W + w0 + 1) * rs; atomicAdd(o, t.x); atomicAdd(o + 1, t.y); atomicAdd(o + 2, t.z); atomicAdd(o + 3, t.w); }
-            }
-          }
-        }
-        if constexpr (FUSED) {
-          // gproj row: offsets (M, L, P, 2) -> this level's 2P values are contiguous
-          if (j < 2 * P) gloc[nq * (3 * M * LP) + (m * LT + l) * P * 2 + j] = st_l;
-        } else {
-          const int64_t kl = ((nq * M + m) * LT + l) * P;
-          if (j < P) gattn[kl + j] = st_a;
-          if (j < 2 * P) gloc[2 * kl + j] = st_l;
-        }
-      }
-      if constexpr (FUSED) {
-        // softmax backward over the pair's L*P logits: d logit_k = a_k (d a_k - sum_i a_i d a_i)
-        float* gl = gloc + nq * (3 * M * LP) + 2 * M * LP + m * LP;
-        static_assert(LP <= 16, "two logits per lane of the 8-lane group");
-        if (j < LP) gl[j] = dq[3 * j + 2] * (myga0 - dot);
-        if (j + 8 < LP) gl[j + 8] = dq[3 * (j + 8) + 2] * (myga1 - dot);
-      }
-      // the query's descriptors become phase 3's corner-coefficient form {(1 - ly) a, ly a, lx}: a record
-      // visit then multiplies two LDS values instead of re-deriving both fractions (lane j: samples j, j + 8)
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int k = j + 8 * r;
-        if (k < LP) {
-          float* dk = desc + (qi * LP + k) * 3;
-          const float h = dk[0], w = dk[1], a = dk[2];
-          const float ly = h - floorf(h), lx = w - floorf(w);
-          dk[0] = (1.f - ly) * a;
-          dk[1] = ly * a;
-          dk[2] = lx;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  M2F_STAMP(3)
-
-  // ---- phase 3: per window pixel, the 4 covering slot ranges; one row-contiguous atomic add per row -----
-  {
+    };
+    // phase 3: per window pixel, the 4 covering slot ranges; one row-contiguous atomic add per row
     constexpr int LPR = kWalkLanes, CPL = D / LPR, RPW = 64 / LPR;  // lanes per row, channels per lane, rows per wave
-    const int rows_total = ts.roff[LT];
     const int jl = lane % LPR, rw = lane / LPR;
     float* wst = stage + wid * kStageFloats;               // this wave's flush half: 8 rows x 32 channels
     int* woff = reinterpret_cast<int*>(wst + 8 * 32);      // and their grad_value element offsets
     const char* gbytes = reinterpret_cast<const char*>(gsh);
     const unsigned jlb = static_cast<unsigned>(CPL * 4 * jl);  // this lane's channel bytes (< 128: ORs into a row offset)
-    // row batches of 16 per wave, handed out in order by an LDS counter: the coarse levels' rows (first,
-    // ~37 records each at config 2 against ~9 on the finest level) do not pile up on the first waves
-    for (int b = wid; b * RPW < rows_total;) {
-      const int base = b * RPW;
+    auto phase3_unit = [&](int unit) {
+      const int base = unit * RPW;
       const int row = base + rw;
       float acc[CPL];
 #pragma unroll
@@ -981,11 +890,13 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           const int cell = cbase - ((c & 2) ? cw : 0) - (c & 1);
           const int s0 = cstart[cell], s1 = cstart[cell + 1];
           any |= s1 > s0;
-          // a record: the descriptor in coefficient form {(1 - ly) a, ly a, lx} (end of phase 2) and the query's
-          // g row; coefficient (1 - lx) A as fma(-A, lx, A)
+          // a record: the sample's descriptor {h, w, a} and its query's g row; the corner coefficient from the
+          // fractions ((1 - ly) a or ly a, times (1 - lx) or lx, the (1 - t) factors as fmas)
           auto rec = [&](unsigned p) {
             const float* dk = desc + (p >> 16);
-            const float A = dk[(c & 2) ? 1 : 0], lx = dk[2];
+            const float h = dk[0], w = dk[1], a = dk[2];
+            const float ly = h - floorf(h), lx = w - floorf(w);
+            const float A = (c & 2) ? ly * a : fmaf(-ly, a, a);
             const f4* g = reinterpret_cast<const f4*>(gbytes + ((p & 0xffffu) | jlb));
             const float cf = (c & 1) ? A * lx : fmaf(-A, lx, A);
 #pragma unroll
@@ -1012,7 +923,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       }
       if (any) {
         const int y = ts.wy0[l] + ey, x = ts.wx0[l] + ex;
-        off = ((n * S + geo.start[l] + y * geo.W[l] + x) * M + m) * D;
+        off = ((n * S + ts.start[l] + y * ts.W[l] + x) * M + m) * D;
       }
       // transpose the wave's 16 rows through LDS, 8 rows at a time, so that each atomic instruction adds two whole
       // 128-B rows, one dword per lane (the L2 takes atomics per 64-B request)
@@ -1041,9 +952,25 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the stage is written again
         __builtin_amdgcn_wave_barrier();
       }
+    };
+    auto next_unit = [&]() {
       int nb = 0;
       if (lane == 0) nb = atomicAdd(&ts.next_batch, 1);
-      b = __shfl(nb, 0);
+      return __shfl(nb, 0);
+    };
+    if constexpr (OVERLAP) {
+      // units interleaved (2, 3, 2, 3, ...) while both kinds last, then the rest of the longer kind; the coarse
+      // levels' rows come first (~37 records each at config 2 against ~9 on the finest level)
+      const int mn = min(U2, U3);
+      for (int u = wid; u < U2 + U3; u = next_unit()) {
+        if (u < 2 * mn ? (u & 1) == 0 : U2 > U3) phase2_unit(u < 2 * mn ? (u >> 1) : u - mn);
+        else phase3_unit(u < 2 * mn ? (u >> 1) : u - mn);
+      }
+    } else {
+      for (int u = wid; u < U2; u += kBwdWaves) phase2_unit(u);
+      __syncthreads();
+      M2F_STAMP(3)
+      for (int u = wid; u < U3; u = next_unit()) phase3_unit(u);
     }
   }
   if constexpr (STAMP) __syncthreads();
@@ -1427,7 +1354,7 @@ int fwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
 //   window fits).  Geometry only: every setting computes the same gradients (tests sweep them).
 bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds, int& threads) {
   if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
-  if (static_cast<int64_t>(d.N) * d.S * d.M * d.D >= (int64_t{1} << 31)) return false;  // 32-bit row offsets
+  if (static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 >= (int64_t{1} << 31)) return false;  // 32-bit byte offsets
   geo = TileGeom{};
   geo.L = d.L;
   int64_t total = 0;
@@ -1472,7 +1399,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   const size_t ns = static_cast<size_t>(qt) * lp;
   lds = (static_cast<size_t>(qt) * 32 + ((ns * 3 + 3) & ~static_cast<size_t>(3)) + (threads / 64) * kStageFloats) * 4 +
         ((static_cast<size_t>(geo.max_rows) + 1 + 3) & ~static_cast<size_t>(3)) * 4 + (((ns + 31) / 32 + 3) & ~static_cast<size_t>(3)) * 4 +
-        (ns + 4) * 4;
+        (ns + 4) * 4 + static_cast<size_t>(qt) * 4;
   return lds <= 156 * 1024;
 }
 
@@ -1489,9 +1416,8 @@ void launch_tiled_t(const float* value, const float* loc, const float* attn, con
   }
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
   // quad phase 2: 32-bit byte offsets into value / grad_value
-  const bool quad = m2f::option(m2f::kOptMsdaBwdQuad, 1) != 0 &&
-                    static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 < (int64_t{1} << 31);
-  if (quad)
+  const bool overlap = m2f::option(m2f::kOptMsdaBwdOverlap, 1) != 0;
+  if (overlap)
     msda_bwd_f32_tiled<LT, FUSED, TPB, true><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
   else
     msda_bwd_f32_tiled<LT, FUSED, TPB, false><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
@@ -1773,9 +1699,9 @@ extern "C" int m2f_diag_msda_bwd_stamps_f32(const float* value, const float* loc
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
 #define M2F_DIAG_LAUNCH(TPB, NF)                                                                                  \
   do {                                                                                                           \
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, TPB, true, true, NF>),      \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, TPB, false, true, NF>),      \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);                    \
-    msda_bwd_f32_tiled<3, false, TPB, true, true, NF><<<grid, TPB, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, \
+    msda_bwd_f32_tiled<3, false, TPB, false, true, NF><<<grid, TPB, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, \
                                                                        geo, d.S, d.M, grad_value, grad_loc,     \
                                                                        grad_attn, stamps);                      \
   } while (0)

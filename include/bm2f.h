@@ -304,8 +304,8 @@ int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, 
 
 /* Explicit tuning options: geometry / engine overrides for tests and tools (the library never reads the
  * environment).  value < 0 restores the built-in default.  Names: msda_threads, msda_tile, msda_tile_w,
- * msda_halo, msda_win_rows, msda_bwd_tiled, msda_fwd_tiled, msda_fwd_quad, msda_bwd_quad (MSDA partitions and
- * variants),
+ * msda_halo, msda_win_rows, msda_bwd_tiled, msda_fwd_tiled, msda_fwd_quad, msda_bwd_overlap (MSDA partitions
+ * and variants),
  * mattn_dq_atomic (masked attention dQ variant), gemm_nt_cfg, x3_tn_nw, x3_tn_blocks, x3_nt_cfg (GEMM tilings).
  * Every option changes the partition or kernel variant only; results agree to fp32 rounding (summation
  * order may differ between variants).  Process-wide; not synchronised

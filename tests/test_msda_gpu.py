@@ -185,14 +185,14 @@ def _pyramid_case(shapes, N, M, far_frac, seed):
 
 @pytest.mark.parametrize("tile,rows,halo", [(16, 2304, 8), (12, 2304, 8), (8, 480, 8), (4, 64, 2), (8, 200, 0),
                                            (6, 2304, 12), (16, 700, 8)])
-@pytest.mark.parametrize("quad", [1, 0])
-def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, quad):
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, overlap):
     """The tiled backward over tile / cell-budget / halo geometries (m2f_set_option msda_*: geometry only), on a
     non-square pyramid whose tiles do not divide every level evenly, 5 % of the samples thrown far (the
-    direct-atomic path), against the C oracle and the untiled kernel; phase 2 in its quad form (msda_bwd_quad 1,
-    the default) and its 8-lane form."""
+    direct-atomic path), against the C oracle and the untiled kernel; phases 2 and 3 as one interleaved work queue
+    (msda_bwd_overlap 1, the default) and one after the other."""
     from bm2f_amd import _native, msda
-    with _native.options(msda_tile=tile, msda_win_rows=rows, msda_halo=halo, msda_bwd_quad=quad):
+    with _native.options(msda_tile=tile, msda_win_rows=rows, msda_halo=halo, msda_bwd_overlap=overlap):
         _tiled_backward_case(device, tile, rows)
 
 
@@ -221,17 +221,17 @@ def _tiled_backward_case(device, tile, rows):
     torch.testing.assert_close(gl, gl2, rtol=1e-4, atol=1e-6 * gl2.abs().max().item())
 
 
-@pytest.mark.parametrize("quad", [1, 0])
-def test_tiled_backward_nonfinite_and_zero_grads(device, quad):
+@pytest.mark.parametrize("overlap", [1, 0])
+def test_tiled_backward_nonfinite_and_zero_grads(device, overlap):
     """NaN in grad_output propagates into grad_value exactly where the reference's atomics put it, and zero
-    grad_output rows give zeros, in both phase-2 forms of the tiled backward."""
+    grad_output rows give zeros, with phases 2 and 3 overlapped or not."""
     from bm2f_amd import _native, msda
     shapes = [(4, 4), (8, 8), (16, 16)]
     value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 1, 8, 0.0, 7)
     gout[:, :16] = 0.0
     gout[0, 100, 5] = float("nan")
     dst = msda.attach_host_shapes(st.to(device), shapes)
-    with _native.options(msda_bwd_quad=quad):
+    with _native.options(msda_bwd_overlap=overlap):
         gv, gl, ga = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
                                                  attn.to(device), gout.to(device), 64)
     wv, wl, wa = msda_ref.msda_backward(value.double(), st, lsi, loc.double(), attn.double(), gout.double())
@@ -355,10 +355,10 @@ def test_fused_forward_variants_vs_oracle(device, shapes, quad):
                                     [(6, 10), (12, 20)]])
 @pytest.mark.parametrize("quad", [1, 0])
 def test_fused_backward_variants_vs_oracle(device, shapes, quad):
-    """The fused backward (d offsets / d logits from the raw projection) in both phase-2 forms, 1-4 levels, odd
+    """The fused forward (quad or 8-lane form) and backward (phases 2 and 3 overlapped or not), 1-4 levels, odd
     level shapes, 5 % of the samples thrown far (the out-of-window atomics of every lane of a quad), against the
     C oracle: grad_value, d offsets (crossing entries one-sided) and d logits."""
     from bm2f_amd import _native
     from test_scale_gpu import fused_fwd_bwd_vs_oracle
-    with _native.options(msda_bwd_quad=quad, msda_fwd_quad=quad):
+    with _native.options(msda_bwd_overlap=quad, msda_fwd_quad=quad):
         fused_fwd_bwd_vs_oracle(device, shapes, N=2, far=0.05, seed=31 + len(shapes))
