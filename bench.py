@@ -370,13 +370,28 @@ def measure_dropin(device, n, res, timer, kern, iters=5):
     def step():
         st = torch.tensor(shapes, dtype=torch.int64, device=device)   # fresh and untagged, as the encoder's
         MSDeformAttnFunction.apply(v, st, lsi, lc, a, 64).backward(gout)
-    step()
-    torch.cuda.synchronize()
-    saved, timer.events, timer.enabled = timer.events, {}, True
-    for _ in range(iters):
-        step()
-    res_k = timer.summary(iters)
-    timer.events, timer.enabled = saved, False
+
+    # the fused kernels on the SAME samples (offsets in pixels from the reference points, logits whose softmax
+    # is attn): the step's own fused launches see the encoder's activations, a different sample spread
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    proj = torch.cat([off.reshape(n, S, -1), attn.log().reshape(n, S, -1)], -1).contiguous()
+    rf = ref[None, :, None, :].expand(n, S, L, 2).contiguous()
+    vf, pf = value.detach().clone().requires_grad_(), proj.requires_grad_()
+
+    def step_fused():
+        MSDeformAttnFusedFunction.apply(vf, pf, rf, tuple(shapes), P).backward(gout)
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize()
+        saved, timer.events, timer.enabled = timer.events, {}, True
+        for _ in range(iters):
+            fn()
+        res_k = timer.summary(iters)
+        timer.events, timer.enabled = saved, False
+        return res_k
+    res_k = timed(step)
+    res_f = timed(step_fused)
     out = {}
     for fam in ("msda_fwd", "msda_bwd"):
         k = res_k.get(fam)
@@ -384,10 +399,13 @@ def measure_dropin(device, n, res, timer, kern, iters=5):
             continue
         ent = roofline_entry(fam, k, "hbm")
         ent["kernel"] = f"{fam} via MSDeformAttnFunction (m2f_msda_{fam[5:]}_f32, untagged device spatial_shapes)"
+        if res_f.get(fam):
+            ent["fused_same_inputs_ms"] = round(res_f[fam]["mean_ms"], 4)
+            ent["vs_fused_same_inputs"] = round(k["mean_ms"] / res_f[fam]["mean_ms"], 3)
         if kern.get(fam):
             ent["vs_fused_step_kernel"] = round(k["mean_ms"] / kern[fam]["mean_ms"], 3)
         out[fam] = ent
-    del v, lc, a, value, loc, attn, gout
+    del v, lc, a, value, loc, attn, gout, vf, pf, proj, rf
     torch.cuda.empty_cache()
     return out
 

@@ -40,7 +40,7 @@ extern "C" int m2f_abi_version(void) { return 1; }
 namespace {
 constexpr const char* kOptionNames[m2f::kOptCount] = {
     "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
-    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap"};
+    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap", "msda_bwd_det"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -322,20 +322,24 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 //            (W, H) on the fused path, or the given loc / attn) into a 12-byte descriptor {h, w, a} per
 //            sample in LDS (h = loc_y * H - 0.5 ...; h = w = -2 when the sample lies outside (-1, H) x
 //            (-1, W)), stages the tile's grad_output rows (this head) in LDS and takes the bounding box of
-//            the touched corners per level.  The window = that box clipped to the tile +- halo.
+//            the touched corners per level (every global load of the phase issued first).  The window = that
+//            box clipped to the tile +- halo.
 //   phase 1  counting sort of the samples by the window cell of their 2x2 corner block (the window grid
 //            extended by one row / column up and left): an LDS counter per cell (returning adds give each
-//            sample its rank), a block-wide exclusive scan, and one u16 sample id per slot.  Samples whose
-//            corners leave the window are flagged instead.
-//   phase 2  an 8-lane group per query (float4 of channels per lane) gathers each sample's 4 corner rows,
-//            forms the 4 per-corner channel dots with g, reduces them by DPP and writes grad_loc /
-//            grad_attn from those four sums.  Flagged samples add their 4 corner rows with fp32 atomics.
+//            sample its rank), a block-wide exclusive scan, and one 32-bit slot per sample (its descriptor
+//            index and its query's g-row offset).  Samples whose corners leave the window are flagged instead.
+//   phase 2  a lane quad per query (8 channels per lane) gathers each sample's 4 corner rows (texture path),
+//            forms the per-corner channel dots with g and writes grad_loc / grad_attn (or d offset / d logit)
+//            once per point (quad transpose-reduce).  Flagged samples add their 4 corner rows with atomics.
 //   phase 3  a 4-lane group per window pixel reads the 4 slot ranges whose cells cover it ((y,x) ->
 //            corner 1 of cell (y,x), corner 2 of (y,x-1), corner 3 of (y-1,x), corner 4 of (y-1,x-1)),
 //            accumulating w_c * a * g[query] in fp32 from the LDS descriptors and g rows (8 channels per
-//            lane); the wave's 16 rows are transposed through LDS so that each fp32 atomic instruction adds
-//            two whole 128-B rows to HBM.
-// Summation order (slot order, atomics across workgroups) is not fixed, as in the reference's atomics.
+//            lane); the wave's 16 rows are transposed through LDS, 8 at a time, so that each atomic
+//            instruction adds two whole 128-B rows to HBM.
+//   Phases 2 and 3 read nothing the other writes: their units are dealt from one counter, interleaved
+//   (OVERLAP), so the texture-bound gather and the LDS-bound walk run at once.
+// Summation order (slot order, atomics across workgroups) is not fixed, as in the reference's atomics, except
+// in the deterministic mode (DET, below).
 // grad_loc / grad_attn (or d offset / d logit) are owned per (q, m) and written once.
 //
 // FUSED = true: the samples come from the raw projection (offsets | logits) and the reference points, and
@@ -360,6 +364,11 @@ struct TileState {
   float invW[kTileMaxL], invH[kTileMaxL];            // per-lane level is a global load per use
   int next_batch;            // phase-3 row batches handed out dynamically
 };
+
+// g rows in LDS: query qi's two 64-byte halves are swapped when bit 1 of qi is set (float offset of logical
+// 16-byte chunk c), so the half-row reads of different queries spread over four bank quarters instead of two
+// (a row's base bank alternates 0 / 32 with qi's bit 0)
+__device__ __forceinline__ int g_chunk_off(int qi, int c) { return qi * 32 + 4 * (c ^ (qi & 2 ? 4 : 0)); }
 
 // Fused-front-end inputs (raw projection + reference points).
 struct FrontEnd {
@@ -398,11 +407,64 @@ __device__ __forceinline__ int window_cell(const TileState& ts, int l, int h0, i
 // STAMP (diagnostic builds only, M2F_DIAG): s_memtime at the phase barriers of each workgroup into `stamps`;
 // NOFLUSH (diagnostic builds only): phase 3 without its HBM adds, to price them.
 // TPB threads per workgroup: 512 (two workgroups per CU, 12x12 tiles; the default) or 1024 (one, 16x16 tiles).
-template <int LT, bool FUSED, int TPB, bool OVERLAP = true, bool STAMP = false, bool NOFLUSH = false>
+// Fixed-point scale of the deterministic mode: 2^(61 - b - e) with max |grad_output| < 2^e and Lq < 2^b.  A
+// grad_value element sums coef * g over samples whose coefficients (bilinear weight * attention weight, each
+// <= 1; a query's attention weights per head sum to 1) total at most the image's Lq queries, so every partial
+// and the total stay below 2^61; the resolution is max|g| * 2^-(61 - b) absolute (2^-46 at config 2's 21,504
+// queries).
+__device__ __forceinline__ float det_scale(unsigned maxbits, int Lq) {
+  const float B = __uint_as_float(maxbits);
+  int e = 0;
+  if (B > 0.f) (void)frexpf(B, &e);
+  const int b = 32 - __clz(Lq);
+  return ldexpf(1.f, min(61 - b - e, 126));
+}
+
+// max |g| over finite entries (as the bits of a non-negative float: the unsigned order is the float order) and a
+// flag for any non-finite entry: out[0], out[1] (zeroed by the caller)
+__global__ void __launch_bounds__(256) msda_det_scale_kernel(const float4* __restrict__ g, int64_t n4,
+                                                             unsigned* __restrict__ out) {
+  unsigned mx = 0u, nf = 0u;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const float4 v = g[i];
+    const float a[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned b = __float_as_uint(fabsf(a[k]));
+      if (b >= 0x7f800000u) nf = 1u;
+      else mx = max(mx, b);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { mx = max(mx, __shfl_xor(mx, o)); nf |= __shfl_xor(nf, o); }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMax(out, mx);
+    if (nf) atomicOr(out + 1, 1u);
+  }
+}
+
+// grad_value = fixed-point sum * 2^-k (skipped when the non-finite flag sent the kernel down the fp32 atomics)
+__global__ void __launch_bounds__(256) msda_det_convert_kernel(const long long* __restrict__ acc, int64_t n, int Lq,
+                                                               const unsigned* __restrict__ detscale,
+                                                               float* __restrict__ gvalue) {
+  if (detscale[1] != 0u) return;
+  const double inv = 1.0 / static_cast<double>(det_scale(detscale[0], Lq));
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256)
+    gvalue[i] = static_cast<float>(static_cast<double>(acc[i]) * inv);
+}
+
+// DET (deterministic mode, m2f_set_option msda_bwd_det): every grad_value contribution leaving a workgroup (the
+// window rows, the out-of-window samples) is converted to 64-bit fixed point (scale 2^k from the launch's max
+// |grad_output|, DetScale below) and added with integer atomics, whose sum does not depend on their order; the
+// slots of each cell are sorted by sample, so a window row's fp32 partial is summed in a fixed order.  A
+// conversion pass writes grad_value.  Non-finite grad_output falls back to the fp32 atomics (flag set by the scale
+// pass), as the reference's kernel propagates them.
+template <int LT, bool FUSED, int TPB, bool OVERLAP = true, bool DET = false, bool STAMP = false, bool NOFLUSH = false>
 __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
-    float* __restrict__ gloc, float* __restrict__ gattn, unsigned long long* __restrict__ stamps = nullptr) {
+    float* __restrict__ gloc, float* __restrict__ gattn, unsigned long long* __restrict__ gacc = nullptr,
+    const unsigned* __restrict__ detscale = nullptr, unsigned long long* __restrict__ stamps = nullptr) {
   constexpr int D = 32, P = 4, LP = LT * P;
   constexpr int kBwdThreads = TPB, kBwdWaves = TPB / 64, kSortPerThread = kSortSamples / TPB;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
@@ -433,6 +495,22 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   unsigned* oow = reinterpret_cast<unsigned*>(cstart + ((geo.max_rows + 1 + 3) & ~3));
   unsigned* slots = reinterpret_cast<unsigned*>(oow + (((nsamp_max + 31) / 32 + 3) & ~3));
   int* qmap = reinterpret_cast<int*>(slots + nsamp_max + 4);  // pyramid position of each tile query
+  float fxscale = 0.f;  // DET: 2^k, grad_value contributions leave the workgroup as round(v * 2^k) in int64
+  bool fixed = false;
+  if constexpr (DET) {
+    fixed = detscale[1] == 0u;
+    fxscale = det_scale(detscale[0], S);
+  }
+  // a grad_value contribution leaving the workgroup
+  auto gv_add = [&](float* dst, float v) {
+    if constexpr (DET) {
+      if (fixed) {
+        atomicAdd(gacc + (dst - gvalue), static_cast<unsigned long long>(__float2ll_rn(v * fxscale)));
+        return;
+      }
+    }
+    atomicAdd(dst, v);
+  };
 
   M2F_STAMP(5)
   if (tid < LT) {
@@ -599,12 +677,12 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
 #pragma unroll
     for (int u = 0; u < kGPre; ++u) {
       const int idx = tid + u * kBwdThreads;
-      if (idx < Qt * 8) *reinterpret_cast<f4*>(gsh + (idx >> 3) * D + 4 * (idx & 7)) = gpre[u];
+      if (idx < Qt * 8) *reinterpret_cast<f4*>(gsh + g_chunk_off(idx >> 3, idx & 7)) = gpre[u];
     }
     for (int idx = tid + kGPre * kBwdThreads; idx < Qt * 8; idx += kBwdThreads) {
       const int qi = idx >> 3, j = idx & 7;
       const int64_t pair = (static_cast<int64_t>(n) * S + qmap[qi]) * M + m;
-      *reinterpret_cast<f4*>(gsh + qi * D + 4 * j) = ld4(gout + pair * D + 4 * j);
+      *reinterpret_cast<f4*>(gsh + g_chunk_off(qi, j)) = ld4(gout + pair * D + 4 * j);
     }
     // per-level boxes over the wave, then over the workgroup
 #pragma unroll
@@ -702,10 +780,25 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     for (int r = 0; r < kSortPerThread; ++r)
       if (cell[r] >= 0) {  // slot = desc float index << 16 | g row byte offset: phase 3 decodes it in 3 VALU
         const int sid = tid + r * kBwdThreads, qs = sid / LP;
-        slots[cstart[cell[r]] + rank[r]] = (static_cast<unsigned>(3 * sid) << 16) | static_cast<unsigned>(qs * D * 4);
+        slots[cstart[cell[r]] + rank[r]] =
+            (static_cast<unsigned>(3 * sid) << 16) | static_cast<unsigned>(4 * g_chunk_off(qs, 0));
       }
   }
   __syncthreads();
+  if constexpr (DET) {
+    // a cell's slots in sample order (the ranks above come from LDS atomics, in arrival order): insertion sort,
+    // one thread per cell (a cell holds a few samples)
+    for (int c = tid; c < cells_total; c += kBwdThreads) {
+      const int b0 = cstart[c], b1 = cstart[c + 1];
+      for (int i = b0 + 1; i < b1; ++i) {
+        const unsigned key = slots[i];
+        int k = i - 1;
+        while (k >= b0 && slots[k] > key) { slots[k + 1] = slots[k]; --k; }
+        slots[k + 1] = key;
+      }
+    }
+    __syncthreads();
+  }
   M2F_STAMP(2)
 
   // ---- phases 2 and 3: one work queue ----------------------------------------------------------------------
@@ -733,8 +826,8 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       if (qi >= Qt) return;  // whole quad (same qi) idles together
       const int q = qmap[qi];
       const int64_t nq = static_cast<int64_t>(n) * S + q;
-      const f4 gA = *reinterpret_cast<const f4*>(gsh + qi * D + 4 * j);
-      const f4 gB = *reinterpret_cast<const f4*>(gsh + qi * D + 16 + 4 * j);
+      const f4 gA = *reinterpret_cast<const f4*>(gsh + g_chunk_off(qi, j));
+      const f4 gB = *reinterpret_cast<const f4*>(gsh + g_chunk_off(qi, 4 + j));
       const float* dq = desc + qi * LP * 3;
       const int sid0 = qi * LP, sh = sid0 & 31;
       const unsigned w0f = oow[sid0 >> 5], w1f = oow[min((sid0 + LP - 1) >> 5, (nsamp_max + 31) / 32 - 1)];
@@ -836,8 +929,8 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
               auto add8 = [&](unsigned boff, float u) {
                 float* o = reinterpret_cast<float*>(gvbytes + boff);
                 const f4 ta = u * gA, tb = u * gB;
-                atomicAdd(o, ta.x); atomicAdd(o + 1, ta.y); atomicAdd(o + 2, ta.z); atomicAdd(o + 3, ta.w);
-                atomicAdd(o + 16, tb.x); atomicAdd(o + 17, tb.y); atomicAdd(o + 18, tb.z); atomicAdd(o + 19, tb.w);
+                gv_add(o, ta.x); gv_add(o + 1, ta.y); gv_add(o + 2, ta.z); gv_add(o + 3, ta.w);
+                gv_add(o + 16, tb.x); gv_add(o + 17, tb.y); gv_add(o + 18, tb.z); gv_add(o + 19, tb.w);
               };
               if (f & 1) add8(b1, u1);
               if (f & 2) add8(b2, u2);
@@ -866,7 +959,8 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     float* wst = stage + wid * kStageFloats;               // this wave's flush half: 8 rows x 32 channels
     int* woff = reinterpret_cast<int*>(wst + 8 * 32);      // and their grad_value element offsets
     const char* gbytes = reinterpret_cast<const char*>(gsh);
-    const unsigned jlb = static_cast<unsigned>(CPL * 4 * jl);  // this lane's channel bytes (< 128: ORs into a row offset)
+    // this lane's channels: 4jl..4jl+3 of each half (bytes 16jl, ORed into the half's 64-byte aligned offset)
+    const unsigned jlb = static_cast<unsigned>(16 * jl);
     auto phase3_unit = [&](int unit) {
       const int base = unit * RPW;
       const int row = base + rw;
@@ -897,11 +991,11 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             const float h = dk[0], w = dk[1], a = dk[2];
             const float ly = h - floorf(h), lx = w - floorf(w);
             const float A = (c & 2) ? ly * a : fmaf(-ly, a, a);
-            const f4* g = reinterpret_cast<const f4*>(gbytes + ((p & 0xffffu) | jlb));
+            const unsigned a0 = (p & 0xffffu) | jlb;  // logical half 0; half 1 is the other 64 bytes
             const float cf = (c & 1) ? A * lx : fmaf(-A, lx, A);
 #pragma unroll
             for (int k = 0; k < CPL / 4; ++k) {  // fma chains (pairs of channels pack into v_pk_fma_f32)
-              const f4 v = g[k];
+              const f4 v = *reinterpret_cast<const f4*>(gbytes + (k ? a0 ^ 64u : a0));
 #pragma unroll
               for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(cf, v[e], acc[4 * k + e]);
             }
@@ -932,7 +1026,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         if ((rw >> 3) == half) {
 #pragma unroll
           for (int k = 0; k < CPL / 4; ++k)
-            *reinterpret_cast<f4*>(wst + (rw & 7) * 32 + CPL * jl + 4 * k) =
+            *reinterpret_cast<f4*>(wst + (rw & 7) * 32 + 16 * k + 4 * jl) =
                 f4{acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
           if (jl == 0) woff[rw & 7] = off;
         }
@@ -946,7 +1040,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           if constexpr (NOFLUSH) {
             asm volatile("" ::"v"(v), "v"(o));
           } else {
-            if (o >= 0) atomicAdd(gvalue + o + (lane & 31), v);
+            if (o >= 0) gv_add(gvalue + o + (lane & 31), v);
           }
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // reads done before the stage is written again
@@ -1403,21 +1497,31 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   return lds <= 156 * 1024;
 }
 
+// Deterministic-mode buffers (msda_bwd_det): the int64 accumulator of grad_value and the scale words.
+struct DetBufs {
+  unsigned long long* acc = nullptr;
+  unsigned* scale = nullptr;  // [max |g| bits, non-finite flag]
+};
+
 template <int LT, bool FUSED, int TPB>
 void launch_tiled_t(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                    const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, hipStream_t st) {
+                    const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, const DetBufs& det,
+                    hipStream_t st) {
   static bool attr = false;  // one flag per instantiation
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB, true, true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
     attr = true;
   }
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
-  // quad phase 2: 32-bit byte offsets into value / grad_value
-  const bool overlap = m2f::option(m2f::kOptMsdaBwdOverlap, 1) != 0;
-  if (overlap)
+  if (det.acc)
+    msda_bwd_f32_tiled<LT, FUSED, TPB, true, true><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv,
+                                                                           gl, ga, det.acc, det.scale);
+  else if (m2f::option(m2f::kOptMsdaBwdOverlap, 1) != 0)
     msda_bwd_f32_tiled<LT, FUSED, TPB, true><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
   else
     msda_bwd_f32_tiled<LT, FUSED, TPB, false><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
@@ -1426,22 +1530,22 @@ void launch_tiled_t(const float* value, const float* loc, const float* attn, con
 template <int LT, bool FUSED>
 void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
                   const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                  hipStream_t st) {
+                  const DetBufs& det, hipStream_t st) {
   if (threads == 1024)
-    launch_tiled_t<LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st);
+    launch_tiled_t<LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
   else
-    launch_tiled_t<LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, st);
+    launch_tiled_t<LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
 }
 
 template <bool FUSED>
 void launch_tiled_levels(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
                          const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                         hipStream_t st) {
+                         hipStream_t st, const DetBufs& det = DetBufs{}) {
   switch (d.L) {
-    case 1: launch_tiled<1, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st); break;
-    case 2: launch_tiled<2, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st); break;
-    case 3: launch_tiled<3, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st); break;
-    default: launch_tiled<4, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, st); break;
+    case 1: launch_tiled<1, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st); break;
+    case 2: launch_tiled<2, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st); break;
+    case 3: launch_tiled<3, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st); break;
+    default: launch_tiled<4, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st); break;
   }
 }
 
@@ -1542,6 +1646,10 @@ extern "C" int m2f_msda_bwd_f64(const double* value, const int64_t* spatial_shap
 // Fused front end C ABI
 // ------------------------------------------------------------------------------------------------
 namespace {
+
+int64_t det_workspace_bytes(const Dims& d) {
+  return static_cast<int64_t>(d.N) * d.S * d.M * d.D * 8 + 16;  // int64 grad_value accumulator + scale words
+}
 
 int fused_check(const char* fn, const float* value, const float* proj, int ld, const float* ref,
                 const int64_t* host_shapes, const Dims& d, TileGeom& geo) {
@@ -1646,7 +1754,8 @@ extern "C" int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, 
   int threads;
   if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout", fn);
-  *workspace_bytes = 0;  // the backward needs no workspace (kept for ABI stability)
+  // deterministic mode (msda_bwd_det): the int64 grad_value accumulator and two scale words; otherwise none
+  *workspace_bytes = m2f::option(m2f::kOptMsdaBwdDet, 0) != 0 ? det_workspace_bytes(d) : 0;
   return m2f::ok();
 }
 
@@ -1668,15 +1777,30 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
   int threads;
   if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
     return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout (num_query == spatial_size)", fn);
-  (void)workspace;
-  (void)workspace_bytes;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const size_t gv_bytes = static_cast<size_t>(d.N) * d.S * d.M * d.D * sizeof(float);
+  const int64_t nval = static_cast<int64_t>(d.N) * d.S * d.M * d.D;
+  const size_t gv_bytes = static_cast<size_t>(nval) * sizeof(float);
   hipError_t e = hipMemsetAsync(grad_value, 0, gv_bytes, st);
   if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
   const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
+  DetBufs det;
+  if (m2f::option(m2f::kOptMsdaBwdDet, 0) != 0) {
+    const int64_t need = det_workspace_bytes(d);
+    if (!workspace || workspace_bytes < need || !m2f::aligned(workspace, 16))
+      return m2f::fail(M2F_EINVAL, "%s: deterministic mode needs a 16-byte aligned workspace of %lld bytes "
+                       "(m2f_msda_fused_bwd_workspace)", fn, static_cast<long long>(need));
+    det.acc = static_cast<unsigned long long*>(workspace);
+    det.scale = reinterpret_cast<unsigned*>(det.acc + nval);
+    e = hipMemsetAsync(workspace, 0, static_cast<size_t>(need), st);
+    if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset workspace: %s", fn, hipGetErrorString(e));
+    const int64_t n4 = static_cast<int64_t>(d.N) * d.Lq * d.M * d.D / 4;  // grad_output (N, Lq, M*32) fp32
+    msda_det_scale_kernel<<<2048, 256, 0, st>>>(reinterpret_cast<const float4*>(grad_output), n4, det.scale);
+  }
   launch_tiled_levels<true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj,
-                            nullptr, st);
+                            nullptr, st, det);
+  if (det.acc)
+    msda_det_convert_kernel<<<4096, 256, 0, st>>>(reinterpret_cast<const long long*>(det.acc), nval, d.Lq, det.scale,
+                                                  grad_value);
   return m2f::check_launch(fn);
 }
 
@@ -1699,11 +1823,11 @@ extern "C" int m2f_diag_msda_bwd_stamps_f32(const float* value, const float* loc
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
 #define M2F_DIAG_LAUNCH(TPB, NF)                                                                                  \
   do {                                                                                                           \
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, TPB, false, true, NF>),      \
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, TPB, false, false, true, NF>),      \
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);                    \
-    msda_bwd_f32_tiled<3, false, TPB, false, true, NF><<<grid, TPB, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, \
+    msda_bwd_f32_tiled<3, false, TPB, false, false, true, NF><<<grid, TPB, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, \
                                                                        geo, d.S, d.M, grad_value, grad_loc,     \
-                                                                       grad_attn, stamps);                      \
+                                                                       grad_attn, nullptr, nullptr, stamps);    \
   } while (0)
   if (threads == 1024) {
     if (noflush) M2F_DIAG_LAUNCH(1024, true); else M2F_DIAG_LAUNCH(1024, false);

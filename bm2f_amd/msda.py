@@ -265,9 +265,19 @@ class MSDeformAttnFusedFunction(Function):
         hs = _host_shape_buffer(host_shapes)
         grad_value = torch.empty_like(value)
         grad_proj = torch.empty((N, S, M * L * n_points * 3), dtype=proj.dtype, device=proj.device)
+        # deterministic mode (native option msda_bwd_det, or torch.use_deterministic_algorithms(True)) needs an
+        # int64 accumulator workspace; 0 bytes otherwise
+        if torch.are_deterministic_algorithms_enabled() and _native.get_option("msda_bwd_det") < 0:
+            with _native.options(msda_bwd_det=1):
+                return MSDeformAttnFusedFunction.backward(ctx, grad_out)
+        ws_bytes = ctypes.c_int64(0)
+        _native.call("m2f_msda_fused_bwd_workspace", ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, n_points,
+                     ctypes.byref(ws_bytes))
+        ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=value.device) if ws_bytes.value else None
         _native.call("m2f_msda_fused_bwd_f32", _ptr(value), _ptr(proj), proj.stride(1), _ptr(ref), ref.stride(0),
                      ctypes.cast(hs, ctypes.c_void_p), _ptr(grad_out), N, S, M, D, L, S, n_points, _ptr(grad_value),
-                     _ptr(grad_proj), None, ctypes.c_int64(0), _stream(value.device))
+                     _ptr(grad_proj), None if ws is None else _ptr(ws), ctypes.c_int64(ws_bytes.value),
+                     _stream(value.device))
         return grad_value, grad_proj, None, None, None
 
 

@@ -113,8 +113,13 @@ int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int proj_ld, c
                            int num_point, float* output, void* stream);
 
 /* grad_value rows are added with fp32 atomics from the tiled workgroups' LDS windows (each window row is
- * flushed once; values repeat to within fp32 rounding, not bit for bit).  The workspace arguments are kept
- * for ABI stability: m2f_msda_fused_bwd_workspace() reports 0 bytes and the workspace is not read. */
+ * flushed once; values repeat to within fp32 rounding, not bit for bit), and no workspace is needed
+ * (m2f_msda_fused_bwd_workspace() reports 0 bytes).  Deterministic mode (m2f_set_option("msda_bwd_det", 1)):
+ * grad_value is bitwise repeatable -- each workgroup sums its window rows in a fixed order and adds them, and
+ * the out-of-window samples, as 64-bit fixed point (scale 2^k from the launch's max |grad_output|, resolution
+ * max|g| * 2^-(61 - ceil(log2 Lq))) with integer atomics, then a pass converts to fp32; it needs the workspace
+ * m2f_msda_fused_bwd_workspace() then reports (8 bytes per grad_value element + 16, 16-byte aligned) and
+ * returns M2F_EINVAL without it.  A non-finite grad_output sends it down the fp32 atomics (as the reference). */
 int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, int batch, int spatial_size, int num_heads,
                                  int channels, int num_levels, int num_point, int64_t* workspace_bytes);
 int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
@@ -304,8 +309,8 @@ int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, 
 
 /* Explicit tuning options: geometry / engine overrides for tests and tools (the library never reads the
  * environment).  value < 0 restores the built-in default.  Names: msda_threads, msda_tile, msda_tile_w,
- * msda_halo, msda_win_rows, msda_bwd_tiled, msda_fwd_tiled, msda_fwd_quad, msda_bwd_overlap (MSDA partitions
- * and variants),
+ * msda_halo, msda_win_rows, msda_bwd_tiled, msda_fwd_tiled, msda_fwd_quad, msda_bwd_overlap, msda_bwd_det (MSDA
+ * partitions, variants, deterministic mode),
  * mattn_dq_atomic (masked attention dQ variant), gemm_nt_cfg, x3_tn_nw, x3_tn_blocks, x3_nt_cfg (GEMM tilings).
  * Every option changes the partition or kernel variant only; results agree to fp32 rounding (summation
  * order may differ between variants).  Process-wide; not synchronised

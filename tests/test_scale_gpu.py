@@ -155,6 +155,69 @@ def test_fused_msda_config2_backward_repeatable(device):
     assert torch.equal(grads[0][1], grads[1][1])
 
 
+def test_fused_msda_config2_backward_deterministic_mode(device):
+    """Deterministic mode (msda_bwd_det: fixed-order window sums, 64-bit fixed-point integer atomics across
+    workgroups and for the out-of-window samples): grad_value is bitwise equal over runs at full size with 5 %
+    far samples, and matches the C oracle like the default mode; torch.use_deterministic_algorithms(True)
+    selects it too."""
+    from bm2f_amd import _native
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    shapes = SHAPES_1024
+    N, L = 2, 3
+    value, proj, ref = _fused_case(shapes, N, 0.05, seed=3)
+    S = value.shape[1]
+    gout = torch.randn(N, S, 256, generator=torch.Generator().manual_seed(6)).to(device)
+    rf = ref.float().to(device)[None, :, None, :].expand(N, S, L, 2)
+
+    def run():
+        v = value.to(device).requires_grad_()
+        pj = proj.to(device).requires_grad_()
+        MSDeformAttnFusedFunction.apply(v, pj, rf, tuple(shapes), 4).backward(gout)
+        return v.grad.clone(), pj.grad.clone()
+    with _native.options(msda_bwd_det=1):
+        g1, g2 = run(), run()
+    assert torch.equal(g1[0], g2[0]) and torch.equal(g1[1], g2[1])
+    torch.use_deterministic_algorithms(True)
+    try:
+        g3 = run()
+    finally:
+        torch.use_deterministic_algorithms(False)
+    assert torch.equal(g1[0], g3[0])
+    g0 = run()  # default mode: the same values up to fp32 summation order
+    torch.testing.assert_close(g1[0], g0[0], rtol=1e-5, atol=1e-6 * g0[0].abs().max().item())
+    loc, attn = _loc_attn(proj, ref, shapes)
+    st = torch.tensor(shapes, dtype=torch.int64)
+    lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
+    wv, _, _ = msda_ref.msda_backward(value.double(), st, lsi, loc, attn, gout.cpu().double())
+    _close(g1[0].cpu(), wv)
+
+
+def test_fused_msda_deterministic_mode_nonfinite_grad(device):
+    """Deterministic mode with a NaN in grad_output falls back to the fp32 atomics: NaN lands in exactly the
+    grad_value elements the oracle's scatter puts it in, the rest match."""
+    from bm2f_amd import _native
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    shapes = [(8, 8), (16, 16)]
+    N, L = 1, 2
+    value, proj, ref = _fused_case(shapes, N, 0.05, seed=4)
+    S = value.shape[1]
+    gout = torch.randn(N, S, 256, generator=torch.Generator().manual_seed(9))
+    gout[0, 70, 37] = float("nan")
+    v = value.to(device).requires_grad_()
+    pj = proj.to(device).requires_grad_()
+    rf = ref.float().to(device)[None, :, None, :].expand(N, S, L, 2)
+    with _native.options(msda_bwd_det=1):
+        MSDeformAttnFusedFunction.apply(v, pj, rf, tuple(shapes), 4).backward(gout.to(device))
+    loc, attn = _loc_attn(proj, ref, shapes)
+    st = torch.tensor(shapes, dtype=torch.int64)
+    lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
+    wv, _, _ = msda_ref.msda_backward(value.double(), st, lsi, loc, attn, gout.double())
+    got = v.grad.cpu().double().numpy()
+    assert np.array_equal(np.isnan(got), np.isnan(wv)) and np.isnan(wv).any()
+    fin = np.isfinite(wv)
+    np.testing.assert_allclose(got[fin], wv[fin], rtol=1e-3, atol=1e-5 * np.abs(wv[fin]).max())
+
+
 def _random_bits(B, Q, Lk, device, seed, p_block=0.6):
     g = torch.Generator(device=device).manual_seed(seed)
     blocked = torch.rand(B, Q, Lk, device=device, generator=g) < p_block

@@ -82,10 +82,14 @@ def fused_calls(value, shapes, gout, noise, M=8, P=4, seed=1):
         _native.call("m2f_msda_fused_fwd_f32", msda._ptr(value), msda._ptr(proj), proj.stride(1), msda._ptr(ref),
                      ref.stride(0), ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, S, P, msda._ptr(out), st)
 
+    wsb = ctypes.c_int64(0)  # deterministic mode (--opt msda_bwd_det=1) needs a workspace
+    _native.call("m2f_msda_fused_bwd_workspace", ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, P, ctypes.byref(wsb))
+    ws = torch.empty(wsb.value, dtype=torch.uint8, device=dev) if wsb.value else None
+
     def bwd():
         _native.call("m2f_msda_fused_bwd_f32", msda._ptr(value), msda._ptr(proj), proj.stride(1), msda._ptr(ref),
                      ref.stride(0), ctypes.cast(hs, ctypes.c_void_p), msda._ptr(gout), N, S, M, D, L, S, P,
-                     msda._ptr(gv), msda._ptr(gp), None, ctypes.c_int64(0), st)
+                     msda._ptr(gv), msda._ptr(gp), None if ws is None else msda._ptr(ws), ctypes.c_int64(wsb.value), st)
     return fwd, bwd
 
 
