@@ -374,7 +374,7 @@ def measure_dropin(device, n, res, timer, kern, iters=5):
     # the fused kernels on the SAME samples (offsets in pixels from the reference points, logits whose softmax
     # is attn): the step's own fused launches see the encoder's activations, a different sample spread
     from bm2f_amd.msda import MSDeformAttnFusedFunction
-    proj = torch.cat([off.reshape(n, S, -1), attn.log().reshape(n, S, -1)], -1).contiguous()
+    proj = torch.cat([off.reshape(n, S, -1), attn.detach().log().reshape(n, S, -1)], -1).detach().contiguous()
     rf = ref[None, :, None, :].expand(n, S, L, 2).contiguous()
     vf, pf = value.detach().clone().requires_grad_(), proj.requires_grad_()
 

@@ -365,10 +365,8 @@ struct TileState {
   int next_batch;            // phase-3 row batches handed out dynamically
 };
 
-// g rows in LDS: query qi's two 64-byte halves are swapped when bit 1 of qi is set (float offset of logical
-// 16-byte chunk c), so the half-row reads of different queries spread over four bank quarters instead of two
-// (a row's base bank alternates 0 / 32 with qi's bit 0)
-__device__ __forceinline__ int g_chunk_off(int qi, int c) { return qi * 32 + 4 * (c ^ (qi & 2 ? 4 : 0)); }
+// g rows in LDS: query qi's 16-byte chunk c (float offset)
+__device__ __forceinline__ int g_chunk_off(int qi, int c) { return qi * 32 + 4 * c; }
 
 // Fused-front-end inputs (raw projection + reference points).
 struct FrontEnd {
@@ -526,6 +524,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     ts.invW[l] = geo.invW[l]; ts.invH[l] = geo.invH[l];
   }
   for (int i = tid; i < (nsamp_max + 31) / 32; i += blockDim.x) oow[i] = 0u;
+  for (int i = tid; i <= geo.max_rows; i += blockDim.x) cstart[i] = 0;  // the sort's counters (any window fits)
   if (tid == 0) ts.next_batch = kBwdWaves;
   __syncthreads();
   if (tid == 0) {
@@ -732,8 +731,6 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   }
   __syncthreads();
   const int cells_total = ts.coff[LT];
-  for (int i = tid; i <= cells_total; i += blockDim.x) cstart[i] = 0;
-  __syncthreads();
 
   // ---- phase 1: counting sort of the in-window samples by cell ------------------------------------------
   {
@@ -959,8 +956,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     float* wst = stage + wid * kStageFloats;               // this wave's flush half: 8 rows x 32 channels
     int* woff = reinterpret_cast<int*>(wst + 8 * 32);      // and their grad_value element offsets
     const char* gbytes = reinterpret_cast<const char*>(gsh);
-    // this lane's channels: 4jl..4jl+3 of each half (bytes 16jl, ORed into the half's 64-byte aligned offset)
-    const unsigned jlb = static_cast<unsigned>(16 * jl);
+    const unsigned jlb = static_cast<unsigned>(CPL * 4 * jl);  // this lane's channel bytes (< 128: ORs into a row offset)
     auto phase3_unit = [&](int unit) {
       const int base = unit * RPW;
       const int row = base + rw;
@@ -991,11 +987,11 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             const float h = dk[0], w = dk[1], a = dk[2];
             const float ly = h - floorf(h), lx = w - floorf(w);
             const float A = (c & 2) ? ly * a : fmaf(-ly, a, a);
-            const unsigned a0 = (p & 0xffffu) | jlb;  // logical half 0; half 1 is the other 64 bytes
+            const f4* g = reinterpret_cast<const f4*>(gbytes + ((p & 0xffffu) | jlb));
             const float cf = (c & 1) ? A * lx : fmaf(-A, lx, A);
 #pragma unroll
             for (int k = 0; k < CPL / 4; ++k) {  // fma chains (pairs of channels pack into v_pk_fma_f32)
-              const f4 v = *reinterpret_cast<const f4*>(gbytes + (k ? a0 ^ 64u : a0));
+              const f4 v = g[k];
 #pragma unroll
               for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(cf, v[e], acc[4 * k + e]);
             }
@@ -1026,7 +1022,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         if ((rw >> 3) == half) {
 #pragma unroll
           for (int k = 0; k < CPL / 4; ++k)
-            *reinterpret_cast<f4*>(wst + (rw & 7) * 32 + 16 * k + 4 * jl) =
+            *reinterpret_cast<f4*>(wst + (rw & 7) * 32 + CPL * jl + 4 * k) =
                 f4{acc[4 * k], acc[4 * k + 1], acc[4 * k + 2], acc[4 * k + 3]};
           if (jl == 0) woff[rw & 7] = off;
         }
