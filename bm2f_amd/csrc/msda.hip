@@ -684,17 +684,36 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       *reinterpret_cast<f4*>(gsh + g_chunk_off(qi, j)) = ld4(gout + pair * D + 4 * j);
     }
     // per-level boxes over the wave, then over the workgroup
+    if constexpr (TPQ == 4) {
+      // a lane only ever touches its own level (tid & 3: the task stride is a multiple of 4), so the lanes of
+      // one level (lane & 3 equal) reduce it over xor 4..32, and lane l < LT publishes level l
+      const int ol = (lane & 3) < LT ? (lane & 3) : LT - 1;
+      int a0 = 0x7fffffff, a1 = -1, a2 = 0x7fffffff, a3 = -1;
 #pragma unroll
-    for (int l = 0; l < LT; ++l) {
-      int a0 = bmin_y[l], a1 = bmax_y[l], a2 = bmin_x[l], a3 = bmax_x[l];
+      for (int l = 0; l < LT; ++l)
+        if (l == ol) { a0 = bmin_y[l]; a1 = bmax_y[l]; a2 = bmin_x[l]; a3 = bmax_x[l]; }
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
+      for (int o = 32; o >= 4; o >>= 1) {
         a0 = min(a0, __shfl_xor(a0, o)); a1 = max(a1, __shfl_xor(a1, o));
         a2 = min(a2, __shfl_xor(a2, o)); a3 = max(a3, __shfl_xor(a3, o));
       }
-      if (lane == 0 && a1 >= 0) {
-        atomicMin(&ts.bb[l][0], a0); atomicMax(&ts.bb[l][1], a1);
-        atomicMin(&ts.bb[l][2], a2); atomicMax(&ts.bb[l][3], a3);
+      if (lane < LT && a1 >= 0) {
+        atomicMin(&ts.bb[lane][0], a0); atomicMax(&ts.bb[lane][1], a1);
+        atomicMin(&ts.bb[lane][2], a2); atomicMax(&ts.bb[lane][3], a3);
+      }
+    } else {
+#pragma unroll
+      for (int l = 0; l < LT; ++l) {
+        int a0 = bmin_y[l], a1 = bmax_y[l], a2 = bmin_x[l], a3 = bmax_x[l];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          a0 = min(a0, __shfl_xor(a0, o)); a1 = max(a1, __shfl_xor(a1, o));
+          a2 = min(a2, __shfl_xor(a2, o)); a3 = max(a3, __shfl_xor(a3, o));
+        }
+        if (lane == 0 && a1 >= 0) {
+          atomicMin(&ts.bb[l][0], a0); atomicMax(&ts.bb[l][1], a1);
+          atomicMin(&ts.bb[l][2], a2); atomicMax(&ts.bb[l][3], a3);
+        }
       }
     }
   }
