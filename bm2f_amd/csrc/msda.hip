@@ -40,7 +40,7 @@ extern "C" int m2f_abi_version(void) { return 1; }
 namespace {
 constexpr const char* kOptionNames[m2f::kOptCount] = {
     "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
-    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap", "msda_bwd_det"};
+    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap", "msda_bwd_det", "msda_fwd_pb"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -1222,15 +1222,17 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
 // The four points of one level for the quad forward kernels: lane j holds point j's geometry (k) and attention
 // weight (wa); the quad takes the points in turn, each lane gathering its 8 channels of the point's 4 corner rows
 // (addresses and weights by DPP quad broadcast) into acc0 (channels 4j..4j+3) and acc1 (16+4j..16+4j+3).
+template <int PB = 2>
 __device__ __forceinline__ void quad_level_fwd(const char* __restrict__ vbytes, const QuadPoint& k, float wa,
                                                unsigned cjb, f4& acc0, f4& acc1) {
   // a corner outside the level weighs 0 (its clamped row is another corner of the same sample)
   const float w1 = k.w1 * wa, w2 = k.w2 * wa, w3 = k.w3 * wa, w4 = k.w4 * wa;
   const int okb = k.ok ? 1 : 0;
-  // two points per batch: their 16 loads are issued (clamped, in-level addresses) before any of their math
-  auto batch = [&](auto c0, auto c1) {
-    constexpr int C0 = decltype(c0)::value, C1 = decltype(c1)::value;
-    f4 va[2][8];
+  // PB points per batch: their 8 * PB loads are issued (clamped, in-level addresses) before any of their math
+  constexpr int kCtrl[4] = {0x00, 0x55, 0xAA, 0xFF};
+  auto batch = [&](auto first) {
+    constexpr int F = decltype(first)::value;
+    f4 va[PB][8];
     const char* vhi = vbytes + 64;  // the row's second half (channels 16..31): an immediate offset
     auto load = [&](f4* v, unsigned o1, unsigned o2, unsigned o3, unsigned o4) {
       v[0] = ldb4(vbytes, o1); v[1] = ldb4(vhi, o1);
@@ -1238,12 +1240,20 @@ __device__ __forceinline__ void quad_level_fwd(const char* __restrict__ vbytes, 
       v[4] = ldb4(vbytes, o3); v[5] = ldb4(vhi, o3);
       v[6] = ldb4(vbytes, o4); v[7] = ldb4(vhi, o4);
     };
-    load(va[0], qpermi<C0>(k.o1) + cjb, qpermi<C0>(k.o2) + cjb, qpermi<C0>(k.o3) + cjb, qpermi<C0>(k.o4) + cjb);
-    load(va[1], qpermi<C1>(k.o1) + cjb, qpermi<C1>(k.o2) + cjb, qpermi<C1>(k.o3) + cjb, qpermi<C1>(k.o4) + cjb);
-    // pin the loads here: otherwise each point's loads sink into its exec-masked block below and the two
-    // points' latencies are paid one after the other
+    auto load_pt = [&](auto pp) {
+      constexpr int C = kCtrl[F + decltype(pp)::value];
+      load(va[decltype(pp)::value], qpermi<C>(k.o1) + cjb, qpermi<C>(k.o2) + cjb, qpermi<C>(k.o3) + cjb,
+           qpermi<C>(k.o4) + cjb);
+    };
+    load_pt(std::integral_constant<int, 0>{});
+    if constexpr (PB > 1) load_pt(std::integral_constant<int, 1>{});
+    if constexpr (PB > 2) { load_pt(std::integral_constant<int, 2>{}); load_pt(std::integral_constant<int, 3>{}); }
+    // pin the loads here: otherwise each point's loads sink into its exec-masked block below and the points'
+    // latencies are paid one after the other
 #pragma unroll
-    for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(va[0][i]), "+v"(va[1][i]));
+    for (int pp = 0; pp < PB; ++pp)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(va[pp][i]));
     auto fmas = [&](const f4* v, float u1, float u2, float u3, float u4) {
       acc0 += u1 * v[0]; acc1 += u1 * v[1];
       acc0 += u2 * v[2]; acc1 += u2 * v[3];
@@ -1251,11 +1261,22 @@ __device__ __forceinline__ void quad_level_fwd(const char* __restrict__ vbytes, 
       acc0 += u4 * v[6]; acc1 += u4 * v[7];
     };
     // a point outside (-1, H) x (-1, W) is skipped by the exec mask, as the reference skips it
-    if (qpermi<C0>(okb)) fmas(va[0], qpermf<C0>(w1), qpermf<C0>(w2), qpermf<C0>(w3), qpermf<C0>(w4));
-    if (qpermi<C1>(okb)) fmas(va[1], qpermf<C1>(w1), qpermf<C1>(w2), qpermf<C1>(w3), qpermf<C1>(w4));
+    auto fma_pt = [&](auto pp) {
+      constexpr int C = kCtrl[F + decltype(pp)::value];
+      if (qpermi<C>(okb)) fmas(va[decltype(pp)::value], qpermf<C>(w1), qpermf<C>(w2), qpermf<C>(w3), qpermf<C>(w4));
+    };
+    fma_pt(std::integral_constant<int, 0>{});
+    if constexpr (PB > 1) fma_pt(std::integral_constant<int, 1>{});
+    if constexpr (PB > 2) { fma_pt(std::integral_constant<int, 2>{}); fma_pt(std::integral_constant<int, 3>{}); }
   };
-  batch(std::integral_constant<int, 0x00>{}, std::integral_constant<int, 0x55>{});
-  batch(std::integral_constant<int, 0xAA>{}, std::integral_constant<int, 0xFF>{});
+  batch(std::integral_constant<int, 0>{});
+  if constexpr (PB == 1) {
+    batch(std::integral_constant<int, 1>{});
+    batch(std::integral_constant<int, 2>{});
+    batch(std::integral_constant<int, 3>{});
+  } else if constexpr (PB == 2) {
+    batch(std::integral_constant<int, 2>{});
+  }
 }
 
 // Unfused forward, quad form (the reference op's interface: materialised sampling_loc / attention_weight, device
@@ -1297,7 +1318,7 @@ __global__ void __launch_bounds__(256) msda_fwd_f32_q4(const float* __restrict__
   *reinterpret_cast<f4*>(o + 16) = acc1;
 }
 
-template <int LT>
+template <int LT, int PB = 2>
 __global__ void __launch_bounds__(256) msda_fused_fwd_q4(const float* __restrict__ value, FrontEnd fe, TileGeom geo,
                                                          int S, int M, float* __restrict__ out) {
   constexpr int D = 32, P = 4, LP = LT * P;
@@ -1359,7 +1380,7 @@ __global__ void __launch_bounds__(256) msda_fused_fwd_q4(const float* __restrict
     // this lane's point: corner byte offsets and weights (a corner outside the level weighted 0: its clamped row
     // is another corner of the same sample), times the attention weight
     const QuadPoint k = quad_point(sy * H - 0.5f, sx * W - 0.5f, H, W, obase, rsb);
-    quad_level_fwd(vbytes, k, e[l] * inv, cjb, acc0, acc1);
+    quad_level_fwd<PB>(vbytes, k, e[l] * inv, cjb, acc0, acc1);
   };
 #pragma unroll
   for (int l = 0; l < LT; ++l) {
@@ -1718,12 +1739,18 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
     const int64_t nb = T * d.M * d.N;
     if (nb > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many workgroups", fn);
     const unsigned tg = static_cast<unsigned>(nb);
+    const int pb = m2f::option(m2f::kOptMsdaFwdPb, 2);  // points per load batch (1, 2 or 4)
+#define M2F_FQ(LT)                                                                                       \
+  (pb == 1   ? msda_fused_fwd_q4<LT, 1><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output)            \
+   : pb >= 4 ? msda_fused_fwd_q4<LT, 4><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output)            \
+             : msda_fused_fwd_q4<LT, 2><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output))
     switch (d.L) {
-      case 1: msda_fused_fwd_q4<1><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output); break;
-      case 2: msda_fused_fwd_q4<2><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output); break;
-      case 3: msda_fused_fwd_q4<3><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output); break;
-      default: msda_fused_fwd_q4<4><<<tg, 256, 0, st>>>(value, fe, geo, d.S, d.M, output); break;
+      case 1: M2F_FQ(1); break;
+      case 2: M2F_FQ(2); break;
+      case 3: M2F_FQ(3); break;
+      default: M2F_FQ(4); break;
     }
+#undef M2F_FQ
     return m2f::check_launch(fn);
   }
   if (m2f::option(m2f::kOptMsdaFwdTiled, 1) != 0 && d.Lq == d.S) {

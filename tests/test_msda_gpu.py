@@ -327,10 +327,11 @@ def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
 
 @pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(5, 7), (10, 13), (20, 26)],
                                     [(9, 17)], [(4, 4), (8, 8), (16, 16), (32, 32)], [(6, 10), (12, 20)]])
-@pytest.mark.parametrize("quad", [0, 1])
-def test_fused_forward_variants_vs_oracle(device, shapes, quad):
+@pytest.mark.parametrize("quad,pb", [(0, 2), (1, 1), (1, 2), (1, 4)])
+def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb):
     """The fused forward (m2f_msda_fused_fwd_f32) in its quad form (a lane quad per (query, head), point
-    geometry by DPP broadcast, out-of-range points skipped by the exec mask) and its 8-lane form, against the
+    geometry by DPP broadcast, out-of-range points skipped by the exec mask; 1, 2 or 4 points per load batch)
+    and its 8-lane form, against the
     C oracle on the loc / attn the reference front end derives from the same projection: power-of-two and odd
     level shapes (tile edges), 1-4 levels, 5 % of the samples thrown far (out of the level and out of range)."""
     from bm2f_amd import _native
@@ -341,7 +342,7 @@ def test_fused_forward_variants_vs_oracle(device, shapes, quad):
     value, proj, ref = _fused_case(shapes, N, 0.05, seed=21 + L)
     S = value.shape[1]
     rf = ref.float()[None, :, None, :].expand(N, S, L, 2).to(device)
-    with _native.options(msda_fwd_quad=quad):
+    with _native.options(msda_fwd_quad=quad, msda_fwd_pb=pb):
         out = MSDeformAttnFusedFunction.apply(value.to(device), proj.to(device), rf, tuple(shapes), P)
     torch.cuda.synchronize()
     loc, attn = _loc_attn(proj, ref, shapes)
