@@ -40,7 +40,8 @@ extern "C" int m2f_abi_version(void) { return 1; }
 namespace {
 constexpr const char* kOptionNames[m2f::kOptCount] = {
     "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
-    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap", "msda_bwd_det", "msda_fwd_pb"};
+    "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap",
+    "msda_bwd_det", "msda_fwd_pb", "msda_bwd_ratio"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -826,6 +827,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   {
     const int rows_total = ts.roff[LT];
     const int U2 = (Qt + 15) / 16, U3 = (rows_total + 15) / 16;
+    const int ratio = max(geo.ratio23, 1);
     // phase 2, quad form: a quad of lanes takes one query, lane j owning channels 4j..4j+3 and 16+4j..16+4j+3
     // (one load address per corner row: the second half is the immediate offset).  Per level, lane j derives
     // point j's geometry once; the quad takes the points in turn with the owner's corner byte offsets by DPP
@@ -1068,12 +1070,16 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       return __shfl(nb, 0);
     };
     if constexpr (OVERLAP) {
-      // units interleaved (2, 3, 2, 3, ...) while both kinds last, then the rest of the longer kind; the coarse
-      // levels' rows come first (~37 records each at config 2 against ~9 on the finest level)
-      const int mn = min(U2, U3);
-      for (int u = wid; u < U2 + U3; u = next_unit()) {
-        if (u < 2 * mn ? (u & 1) == 0 : U2 > U3) phase2_unit(u < 2 * mn ? (u >> 1) : u - mn);
-        else phase3_unit(u < 2 * mn ? (u >> 1) : u - mn);
+      // R phase-2 units per phase-3 unit while phase 2 lasts (msda_bwd_ratio, default 1), then the rest of phase 3:
+      // with c3(k) = max(min(U3, k / (R + 1)), k - U2) phase-3 units among the first k, unit u is phase-3 unit c3(u)
+      // when c3 steps up at u, else phase-2 unit u - c3(u).  Texture-path work early, LDS work to the end (a
+      // schedule spreading the phase-2 units evenly over the queue measured 2.7 % slower: a gather unit late in
+      // the queue is a straggler); the coarse levels' rows come first (~37 records each at config 2 against ~9)
+      const int T = U2 + U3, R1 = ratio + 1;
+      for (int u = wid; u < T; u = next_unit()) {
+        const int c0 = max(min(U3, u / R1), u - U2), c1 = max(min(U3, (u + 1) / R1), u + 1 - U2);
+        if (c1 > c0) phase3_unit(c0);
+        else phase2_unit(u - c0);
       }
     } else {
       for (int u = wid; u < U2; u += kBwdWaves) phase2_unit(u);
@@ -1504,6 +1510,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   }
   if (total != d.S) return false;
   threads = m2f::option(m2f::kOptMsdaThreads, 512) >= 1024 ? 1024 : 512;
+  geo.ratio23 = std::max(1, m2f::option(m2f::kOptMsdaBwdRatio, 1));
   // 512 threads: 12x12 tiles (78 KB of LDS, two workgroups per CU) measured 2.44 ms at config 2 against 2.45
   // (8x16), 2.52 (16x8) and 2.65 for 1024 threads with 16x16 tiles (tools/msda_bench.py, r2k)
   const int tile_h = std::max(1, m2f::option(m2f::kOptMsdaTile, threads == 1024 ? 16 : 12));
