@@ -1825,7 +1825,8 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
   size_t lds;
   int threads;
   if (!make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
-    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout (num_query == spatial_size)", fn);
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs the encoder layout (num_query == spatial_size), value under 2 GiB "
+                     "and levels under 2^24 pixels", fn);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t nval = static_cast<int64_t>(d.N) * d.S * d.M * d.D;
   const size_t gv_bytes = static_cast<size_t>(nval) * sizeof(float);
