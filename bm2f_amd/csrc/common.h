@@ -44,7 +44,8 @@ inline unsigned ceil_div(int64_t a, int64_t b) { return static_cast<unsigned>((a
 // option changes the partition or the kernel variant only, never the arithmetic's result.
 enum Option : int {
   kOptMsdaThreads, kOptMsdaTile, kOptMsdaTileW, kOptMsdaHalo, kOptMsdaWinRows, kOptMsdaBwdTiled, kOptMsdaFwdTiled,
-  kOptMattnDqAtomic, kOptGemmNtCfg, kOptX3TnNw, kOptX3TnBlocks, kOptX3NtCfg, kOptMsdaFwdQuad, kOptMsdaBwdOverlap, kOptMsdaBwdDet, kOptMsdaFwdPb, kOptMsdaBwdRatio, kOptCount
+  kOptMattnDqAtomic, kOptGemmNtCfg, kOptX3TnNw, kOptX3TnBlocks, kOptX3NtCfg, kOptMsdaFwdQuad, kOptMsdaBwdOverlap, kOptMsdaBwdDet, kOptMsdaFwdPb, kOptMsdaBwdRatio,
+  kOptMsdaFwdLds, kOptMsdaFwdTile, kOptMsdaFwdTileW, kOptMsdaFwdCap, kOptMsdaFwdHalo, kOptCount
 };
 int64_t option_raw(Option o);  // -1 when unset
 inline int option(Option o, int dflt) {

@@ -41,7 +41,8 @@ namespace {
 constexpr const char* kOptionNames[m2f::kOptCount] = {
     "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
     "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap",
-    "msda_bwd_det", "msda_fwd_pb", "msda_bwd_ratio"};
+    "msda_bwd_det", "msda_fwd_pb", "msda_bwd_ratio", "msda_fwd_lds", "msda_fwd_tile", "msda_fwd_tile_w",
+    "msda_fwd_cap", "msda_fwd_halo"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -351,6 +352,7 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 constexpr int kWalkLanes = 4;   // phase-3 lanes per window pixel (8 channels each)
 constexpr int kMaxBwdWaves = 16;
 constexpr int kSortSamples = 6144;  // samples per workgroup the counting sort holds in registers (max_qt * L * P)
+static_assert(3 * kSortSamples < 65536, "phase 3's slots hold the descriptor float index 3 * sid in 16 bits");
 constexpr int kStageFloats = 8 * 32 + 8;  // per wave: 8 rows x 32 channels + 8 row offsets (a flush half)
 
 struct TileState {
@@ -442,14 +444,15 @@ __global__ void __launch_bounds__(256) msda_det_scale_kernel(const float4* __res
   }
 }
 
-// grad_value = fixed-point sum * 2^-k (skipped when the non-finite flag sent the kernel down the fp32 atomics)
+// grad_value = fixed-point sum * 2^-k, added to what the non-finite contributions left there in fp32 (zero almost
+// everywhere); skipped when the non-finite flag sent the whole kernel down the fp32 atomics
 __global__ void __launch_bounds__(256) msda_det_convert_kernel(const long long* __restrict__ acc, int64_t n, int Lq,
                                                                const unsigned* __restrict__ detscale,
                                                                float* __restrict__ gvalue) {
   if (detscale[1] != 0u) return;
   const double inv = 1.0 / static_cast<double>(det_scale(detscale[0], Lq));
   for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256)
-    gvalue[i] = static_cast<float>(static_cast<double>(acc[i]) * inv);
+    gvalue[i] += static_cast<float>(static_cast<double>(acc[i]) * inv);
 }
 
 // DET (deterministic mode, m2f_set_option msda_bwd_det): every grad_value contribution leaving a workgroup (the
@@ -501,9 +504,12 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     fxscale = det_scale(detscale[0], S);
   }
   // a grad_value contribution leaving the workgroup
+  // (DET: a non-finite contribution -- a NaN / Inf from the projection's offsets or logits, which the pre-pass over
+  // grad_output does not see -- goes to grad_value itself in fp32, where the conversion pass adds the fixed-point
+  // sum to it: the element is then non-finite as the reference's atomics leave it)
   auto gv_add = [&](float* dst, float v) {
     if constexpr (DET) {
-      if (fixed) {
+      if (fixed && __builtin_isfinite(v)) {
         atomicAdd(gacc + (dst - gvalue), static_cast<unsigned long long>(__float2ll_rn(v * fxscale)));
         return;
       }
@@ -1399,6 +1405,312 @@ __global__ void __launch_bounds__(256) msda_fused_fwd_q4(const float* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------
+// Fused forward with LDS-staged value windows (the default on the encoder layout).
+//
+// The quad kernel above gathers every sample's four 128-byte corner rows through the texture path (L1,
+// 64 B/clk/CU): 16.9 GB per config-2 launch, which bounds it.  Neighbouring queries sample one neighbourhood,
+// so here a workgroup takes one head of one spatial tile -- the same normalised rectangle on every level (8 x 16
+// pixels on the finest), its queries drawn from all levels -- and, level by level:
+//   1. each quad lane derives its point's geometry for its queries (three rounds of 64 queries), and the
+//      workgroup reduces the touched corners to a box;
+//   2. the box, clipped to the tile +- msda_fwd_halo and shrunk until it fits msda_fwd_cap rows, is copied into
+//      LDS by LDS-DMA (global_load_lds_dwordx4, 8 whole rows per wave-instruction, no VGPRs), once;
+//   3. the quads read their corners with ds_read_b128 (256 B/clk/CU), a sample whose corners leave the window
+//      reading them from HBM as before.
+// Rows sit at a 128-byte stride with the two 64-byte halves of row r swapped when bit 1 of r is set, so the four
+// quads of a ds_read_b128 lane group (a wave's quads are consecutive queries) read four distinct bank quarters
+// when their samples lie in consecutive window rows; the swizzle is applied on the DMA's per-lane source address.
+// Arithmetic per sample and per output element is the quad kernel's, in the same order (same results bit for bit).
+// ------------------------------------------------------------------------------------------------
+constexpr int kFwdLdsThreads = 256;
+constexpr int kFwdLdsRounds = 3;   // queries per workgroup <= 3 * 64
+constexpr int kFwdLdsCap = 416;    // window rows at most: 52 KB + the boxes, three workgroups per CU
+
+// b_i = (quad lane C's a_i) + c for the four corners, as v_add_u32_dpp (hipcc leaves the DPP broadcast and the add
+// apart when the broadcast source comes out of a select).  The s_nop covers the DPP read-after-VALU-write hazard,
+// which the compiler's hazard recognizer does not see inside inline asm.
+template <int C>
+__device__ __forceinline__ void dpp_add4(unsigned& b1, unsigned& b2, unsigned& b3, unsigned& b4, unsigned a1, unsigned a2,
+                                         unsigned a3, unsigned a4, unsigned c) {
+#define M2F_DPP4(QP)                                                                                         \
+  asm("s_nop 1\n\t"                                                                                          \
+      "v_add_u32_dpp %0, %4, %8 quad_perm:" QP " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                \
+      "v_add_u32_dpp %1, %5, %8 quad_perm:" QP " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                \
+      "v_add_u32_dpp %2, %6, %8 quad_perm:" QP " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                \
+      "v_add_u32_dpp %3, %7, %8 quad_perm:" QP " row_mask:0xf bank_mask:0xf bound_ctrl:1"                     \
+      : "=&v"(b1), "=&v"(b2), "=&v"(b3), "=&v"(b4)                                                            \
+      : "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(c))
+  if constexpr (C == 0x00) M2F_DPP4("[0,0,0,0]");
+  else if constexpr (C == 0x55) M2F_DPP4("[1,1,1,1]");
+  else if constexpr (C == 0xAA) M2F_DPP4("[2,2,2,2]");
+  else M2F_DPP4("[3,3,3,3]");
+#undef M2F_DPP4
+}
+
+// The four points of one level for one query: lane j of the quad owns point j (mode md: 0 = skipped (nothing read),
+// 1 = corners in the LDS window at byte offsets a1..a4 (row bases with the half swap), 2 = corners in HBM at byte
+// offsets a1..a4);
+// weights premultiplied by the attention weight, a corner outside the level weighted 0.
+__device__ __forceinline__ void quad_gather_win(const char* __restrict__ vbytes,
+                                                const __attribute__((address_space(3))) unsigned char* win, int md,
+                                                unsigned a1, unsigned a2, unsigned a3, unsigned a4, float w1, float w2,
+                                                float w3, float w4, unsigned cjb, f4& acc0, f4& acc1) {
+  constexpr int kCtrl[4] = {0x00, 0x55, 0xAA, 0xFF};
+  auto batch = [&](auto first) {
+    constexpr int F = decltype(first)::value;
+    f4 va[2][8];
+    int mdp[2];
+    auto load_pt = [&](auto pp) {
+      constexpr int I = decltype(pp)::value, C = kCtrl[F + I];
+      const int mq = qpermi<C>(md);
+      unsigned b1, b2, b3, b4;
+      dpp_add4<C>(b1, b2, b3, b4, a1, a2, a3, a4, cjb);
+      mdp[I] = mq;
+      f4* v = va[I];
+      if (mq == 2) {
+        const char* vhi = vbytes + 64;
+        v[0] = ldb4(vbytes, b1); v[1] = ldb4(vhi, b1);
+        v[2] = ldb4(vbytes, b2); v[3] = ldb4(vhi, b2);
+        v[4] = ldb4(vbytes, b3); v[5] = ldb4(vhi, b3);
+        v[6] = ldb4(vbytes, b4); v[7] = ldb4(vhi, b4);
+      } else if (mq == 1) {  // the other half of a window row is the 64-byte xor (b < 64 within the half)
+        // an address-space-3 load: with generic pointers the compiler merges the two branches' loads into one flat
+        // load of a selected 64-bit address
+        auto lds4 = [&](unsigned o) { return *(const __attribute__((address_space(3))) f4*)(win + o); };
+        v[0] = lds4(b1); v[1] = lds4(b1 ^ 64u);
+        v[2] = lds4(b2); v[3] = lds4(b2 ^ 64u);
+        v[4] = lds4(b3); v[5] = lds4(b3 ^ 64u);
+        v[6] = lds4(b4); v[7] = lds4(b4 ^ 64u);
+      }
+    };
+    load_pt(std::integral_constant<int, 0>{});
+    load_pt(std::integral_constant<int, 1>{});
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) asm volatile("" : "+v"(va[pp][i]));
+    auto fma_pt = [&](auto pp) {
+      constexpr int I = decltype(pp)::value, C = kCtrl[F + I];
+      const float u1 = qpermf<C>(w1), u2 = qpermf<C>(w2), u3 = qpermf<C>(w3), u4 = qpermf<C>(w4);
+      if (mdp[I] != 0) {
+        const f4* v = va[I];
+        acc0 += u1 * v[0]; acc1 += u1 * v[1];
+        acc0 += u2 * v[2]; acc1 += u2 * v[3];
+        acc0 += u3 * v[4]; acc1 += u3 * v[5];
+        acc0 += u4 * v[6]; acc1 += u4 * v[7];
+      }
+    };
+    fma_pt(std::integral_constant<int, 0>{});
+    fma_pt(std::integral_constant<int, 1>{});
+  };
+  batch(std::integral_constant<int, 0>{});
+  batch(std::integral_constant<int, 2>{});
+}
+
+// window row r's LDS byte base (the 64-byte halves swapped when bit 1 of r is set)
+__device__ __forceinline__ unsigned win_row(int r) { return (static_cast<unsigned>(r) << 7) | ((r & 2) << 5); }
+
+template <int LT>
+__global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const float* __restrict__ value, FrontEnd fe,
+                                                                      TileGeom geo, int S, int M,
+                                                                      float* __restrict__ out) {
+  constexpr int D = 32, P = 4, LP = LT * P, R = kFwdLdsRounds, NW = kFwdLdsThreads / 64;
+  // one static array (a constant base folds into the ds_read addresses): window rows | per-wave boxes [LT][NW]
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kFwdLdsCap * 128 + kTileMaxL * NW * 16];
+  const int cap = geo.max_rows;  // window rows in use (a multiple of 8, <= kFwdLdsCap)
+  int4* bbw = reinterpret_cast<int4*>(smem + kFwdLdsCap * 128);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, j = lane & 3;
+  // block -> (image, tile, head), the head fastest: XCD x (blocks are dealt round-robin) gathers one head's rows
+  int b = blockIdx.x;
+  const int m = b % M;
+  b /= M;
+  const int ntiles = geo.nty * geo.ntx;
+  const int n = b / ntiles, tile = b - n * ntiles;
+  const int ty = tile / geo.ntx, tx = tile - ty * geo.ntx;
+  int qy0[LT], qy1[LT], qx0[LT], qx1[LT], qc[LT + 1];
+  qc[0] = 0;
+#pragma unroll
+  for (int l = 0; l < LT; ++l) {
+    qy0[l] = tile_lo(ty, geo.H[l], geo.nty); qy1[l] = tile_lo(ty + 1, geo.H[l], geo.nty);
+    qx0[l] = tile_lo(tx, geo.W[l], geo.ntx); qx1[l] = tile_lo(tx + 1, geo.W[l], geo.ntx);
+    qc[l + 1] = qc[l] + (qy1[l] - qy0[l]) * (qx1[l] - qx0[l]);
+  }
+  const int Qt = qc[LT];
+  const char* vbytes = reinterpret_cast<const char*>(value);
+  const int rsb = M * D * 4;  // value row stride in bytes; value bytes < 2^31 (host check)
+  unsigned cjb = 16u * j;
+  asm volatile("" : "+v"(cjb));  // materialised once, here: the corner broadcasts then fold into v_add_u32_dpp
+  // byte offsets from the kernarg bases are 32-bit (proj, ref, value and out under 2^31 bytes: host check)
+  const char* pbytes = reinterpret_cast<const char*>(fe.proj);
+  const char* rbytes = reinterpret_cast<const char*>(fe.ref) + static_cast<int64_t>(n) * fe.ref_bs * 4;
+  const unsigned pld = static_cast<unsigned>(fe.ld) * 4u;
+  // this quad's query in each round: the tile's queries level by level, row-major in each level's rectangle
+  int qpos[R];
+  unsigned vmask = 0u;  // bit r: round r's query exists
+  float wa[R][LT];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const int qi = r * (kFwdLdsThreads / 4) + (tid >> 2);
+    vmask |= qi < Qt ? 1u << r : 0u;
+    const int qq = min(qi, Qt - 1);
+    int lq = 0;
+#pragma unroll
+    for (int l = 1; l < LT; ++l) lq = qq >= qc[l] ? l : lq;
+    int qb = 0, qw = 1, y0 = 0, x0 = 0, W = 1;
+#pragma unroll
+    for (int l = 0; l < LT; ++l)
+      if (l == lq) { qb = qc[l]; qw = qx1[l] - qx0[l]; y0 = qy0[l]; x0 = qx0[l]; W = geo.W[l]; }
+    const int rr = qq - qb;
+    // rr / qw by the reciprocal ((rr + 0.5) / qw is >= 0.5 / qw from an integer; rr < 2^16)
+    const int yy = static_cast<int>((static_cast<float>(rr) + 0.5f) * __builtin_amdgcn_rcpf(static_cast<float>(qw)));
+    const int xx = rr - yy * qw;
+    int st = 0;
+#pragma unroll
+    for (int l = 0; l < LT; ++l) st = l == lq ? geo.start[l] : st;
+    qpos[r] = st + (y0 + yy) * W + x0 + xx;
+    // softmax over the pair's L*P logits, exactly as msda_fused_fwd_q4 (and the backward's recomputation)
+    const unsigned lgb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>(M * LP * 2 + m * LP + j) * 4u;
+    float e[LT];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int l = 0; l < LT; ++l) {
+      e[l] = *reinterpret_cast<const float*>(pbytes + lgb + l * P * 4);
+      mx = fmaxf(mx, e[l]);
+    }
+    mx = fmaxf(mx, qpermf<0xB1>(mx));
+    mx = fmaxf(mx, qpermf<0x4E>(mx));
+    float sum = 0.f;
+#pragma unroll
+    for (int l = 0; l < LT; ++l) {
+      e[l] = expf(e[l] - mx);
+      sum += qpermf<0x00>(e[l]);
+      sum += qpermf<0x55>(e[l]);
+      sum += qpermf<0xAA>(e[l]);
+      sum += qpermf<0xFF>(e[l]);
+    }
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int l = 0; l < LT; ++l) wa[r][l] = e[l] * inv;
+  }
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  f4 acc0[R], acc1[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) { acc0[r] = z; acc1[r] = z; }
+
+#pragma unroll
+  for (int l = 0; l < LT; ++l) {
+    const int H = geo.H[l], W = geo.W[l];
+    const int lbase = ((n * S + geo.start[l]) * M + m) * D * 4;
+    // 1. lane j's point (l, j) of each round's query: corner block (y0, x0) clamped into the level, whether the
+    //    +1 row / column is a corner inside the level (ey, ex), the four weights (x attention weight), ok
+    int gy[R], gx[R], gfl[R];
+    float gw[R][4];
+    int bmin_y = 0x7fffffff, bmax_y = -1, bmin_x = 0x7fffffff, bmax_x = -1;
+    auto geometry = [&](auto pow2) {
+      constexpr bool POW2 = decltype(pow2)::value;
+      const float fH = static_cast<float>(H), fW = static_cast<float>(W);
+      const float fHm1 = static_cast<float>(H - 1), fWm1 = static_cast<float>(W - 1);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const unsigned rfb = static_cast<unsigned>(qpos[r] * LT + l) * 8u;
+        const unsigned ofb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>((m * LP + l * P + j) * 2) * 4u;
+        const float2 rf = *reinterpret_cast<const float2*>(rbytes + rfb);
+        const float2 off = *reinterpret_cast<const float2*>(pbytes + ofb);
+        const float sx = rf.x + div_norm(off.x, fW, geo.invW[l], POW2);
+        const float sy = rf.y + div_norm(off.y, fH, geo.invH[l], POW2);
+        const float h = sy * H - 0.5f, w = sx * W - 0.5f;
+        const bool ok = ((vmask >> r) & 1u) && h > -1.f && w > -1.f && h < fH && w < fW;
+        const float hs = ok ? h : -2.f, ws = ok ? w : -2.f;
+        const float fh = floorf(hs), fw = floorf(ws);
+        const float ly = hs - fh, lx = ws - fw, hy = 1.f - ly, hx = 1.f - lx;
+        const bool vy0 = fh >= 0.f, vy1 = fh < fHm1, vx0 = fw >= 0.f, vx1 = fw < fWm1;
+        const int y0 = static_cast<int>(__builtin_amdgcn_fmed3f(fh, 0.f, fHm1));
+        const int x0 = static_cast<int>(__builtin_amdgcn_fmed3f(fw, 0.f, fWm1));
+        const int ey = (vy0 && vy1) ? 1 : 0, ex = (vx0 && vx1) ? 1 : 0;
+        const float a = wa[r][l];
+        gw[r][0] = (vy0 && vx0) ? hy * hx * a : 0.f;
+        gw[r][1] = (vy0 && vx1) ? hy * lx * a : 0.f;
+        gw[r][2] = (vy1 && vx0) ? ly * hx * a : 0.f;
+        gw[r][3] = (vy1 && vx1) ? ly * lx * a : 0.f;
+        gy[r] = y0;
+        gx[r] = x0;
+        gfl[r] = (ok ? 1 : 0) | (ey << 1) | (ex << 2);
+        if (ok) {
+          bmin_y = min(bmin_y, y0); bmax_y = max(bmax_y, y0 + ey);
+          bmin_x = min(bmin_x, x0); bmax_x = max(bmax_x, x0 + ex);
+        }
+      }
+    };
+    if (((W & (W - 1)) | (H & (H - 1))) == 0) geometry(std::true_type{});
+    else geometry(std::false_type{});
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      bmin_y = min(bmin_y, __shfl_xor(bmin_y, o)); bmax_y = max(bmax_y, __shfl_xor(bmax_y, o));
+      bmin_x = min(bmin_x, __shfl_xor(bmin_x, o)); bmax_x = max(bmax_x, __shfl_xor(bmax_x, o));
+    }
+    if (lane == 0) bbw[l * NW + wid] = make_int4(bmin_y, bmax_y, bmin_x, bmax_x);
+    __syncthreads();  // the boxes are in; every wave is done reading the previous level's window
+    // 2. the window: the box clipped to the tile +- halo, the halo shrinking until the rows fit (uniform)
+    int by0 = 0x7fffffff, by1 = -1, bx0 = 0x7fffffff, bx1 = -1;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int4 t = bbw[l * NW + w];
+      by0 = min(by0, t.x); by1 = max(by1, t.y); bx0 = min(bx0, t.z); bx1 = max(bx1, t.w);
+    }
+    by0 = __builtin_amdgcn_readfirstlane(by0); by1 = __builtin_amdgcn_readfirstlane(by1);
+    bx0 = __builtin_amdgcn_readfirstlane(bx0); bx1 = __builtin_amdgcn_readfirstlane(bx1);
+    int wy0 = 0, wy1 = -1, wx0 = 0, wx1 = -1;
+    for (int halo = geo.max_halo; halo >= 0 && by1 >= 0; --halo) {
+      wy0 = max(by0, qy0[l] - halo); wy1 = min(by1, qy1[l] - 1 + halo);
+      wx0 = max(bx0, qx0[l] - halo); wx1 = min(bx1, qx1[l] - 1 + halo);
+      if (wy1 < wy0 || wx1 < wx0) { wy1 = wy0 - 1; break; }
+      if ((wy1 - wy0 + 1) * (wx1 - wx0 + 1) <= cap) break;
+      if (halo == 0) wy1 = wy0 - 1;  // the tile itself does not fit (the host sizes cap so it does): no window
+    }
+    const int wh = wy1 >= wy0 ? wy1 - wy0 + 1 : 0, ww = wh > 0 ? wx1 - wx0 + 1 : 0;
+    const int rows = wh * ww;
+    {
+      const float iww = ww > 0 ? 1.f / static_cast<float>(ww) : 0.f;
+      const int nblk = (rows + 7) >> 3;
+      for (int blk = wid; blk < nblk; blk += NW) {
+        const int r = min(blk * 8 + (lane >> 3), rows - 1);
+        const int yy = static_cast<int>((static_cast<float>(r) + 0.5f) * iww), xx = r - yy * ww;
+        const unsigned c = static_cast<unsigned>((lane & 7) ^ ((r & 2) << 1));
+        const unsigned goff = static_cast<unsigned>(mad_u24((wy0 + yy) * W + wx0 + xx, rsb, lbase)) + 16u * c;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(vbytes + goff),
+                                         (__attribute__((address_space(3))) void*)(smem + blk * 1024),
+                                         16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();  // the window is in LDS
+    // 3. gather: window corners from LDS, the rest from HBM
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int fl = gfl[r], y0 = gy[r], x0 = gx[r];
+      const int ey = (fl >> 1) & 1, ex = (fl >> 2) & 1;
+      const bool ok = fl & 1;
+      const bool inwin = ok && y0 >= wy0 && y0 + ey <= wy1 && x0 >= wx0 && x0 + ex <= wx1;
+      // both address forms, then a select (straight-line code keeps the broadcasts foldable into v_add_u32_dpp)
+      const int r1 = (y0 - wy0) * ww + (x0 - wx0), r3 = r1 + (ey ? ww : 0);
+      const unsigned g1 = static_cast<unsigned>(mad_u24(mad_u24(y0, W, x0), rsb, lbase));
+      const unsigned dx = ex ? rsb : 0u, dy = ey ? static_cast<unsigned>(W * rsb) : 0u;
+      const unsigned a1 = inwin ? win_row(r1) : g1, a2 = inwin ? win_row(r1 + ex) : g1 + dx;
+      const unsigned a3 = inwin ? win_row(r3) : g1 + dy, a4 = inwin ? win_row(r3 + ex) : g1 + dy + dx;
+      const int md = ok ? (inwin ? 1 : 2) : 0;
+      quad_gather_win(vbytes, (const __attribute__((address_space(3))) unsigned char*)smem, md, a1, a2, a3, a4, gw[r][0], gw[r][1], gw[r][2], gw[r][3], cjb, acc0[r], acc1[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (!((vmask >> r) & 1u)) continue;
+    char* o = reinterpret_cast<char*>(out) + (static_cast<unsigned>((n * S + qpos[r]) * M + m) * 128u + cjb);
+    *reinterpret_cast<f4*>(o) = acc0[r];
+    *reinterpret_cast<f4*>(o + 64) = acc1[r];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------------
 
@@ -1531,7 +1843,8 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   geo.max_rows = m2f::option(m2f::kOptMsdaWinRows, full);
   geo.max_qt = qt;
   const int lp = d.L * d.P;
-  if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff) return false;
+  // phase 3's 32-bit slots hold the g-row byte offset 128 * qs (qs < qt) in their low 16 bits: qt <= 512
+  if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff || qt > 512) return false;
   if (static_cast<int64_t>(qt) * lp > kSortSamples) return false;
   const size_t ns = static_cast<size_t>(qt) * lp;
   lds = (static_cast<size_t>(qt) * 32 + ((ns * 3 + 3) & ~static_cast<size_t>(3)) + (threads / 64) * kStageFloats) * 4 +
@@ -1722,6 +2035,41 @@ int fused_check(const char* fn, const float* value, const float* proj, int ld, c
   return M2F_OK;
 }
 
+// Geometry of the LDS-window forward; false when the configuration does not qualify (then the quad kernel runs).
+// Options: msda_fwd_tile / msda_fwd_tile_w (8 / 16): tile rows / columns on the finest level; msda_fwd_cap (416):
+// window rows (three workgroups per CU at 52 KB); msda_fwd_halo (8): window halo.  Partition only: every setting
+// computes the same output.
+bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeom& geo, size_t& lds) {
+  if (d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
+  // 32-bit byte offsets into value / out, proj and one image's reference points
+  if (static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 >= (int64_t{1} << 31)) return false;
+  if (static_cast<int64_t>(d.N) * d.S * proj_ld * 4 >= (int64_t{1} << 31)) return false;
+  if (static_cast<int64_t>(d.S) * d.L * 8 >= (int64_t{1} << 31)) return false;
+  geo = base;
+  int fi = 0;
+  for (int l = 0; l < d.L; ++l) {
+    if (static_cast<int64_t>(geo.H[l]) * geo.W[l] >= (int64_t{1} << 24)) return false;  // 24-bit multiplies
+    if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
+  }
+  const int th = std::max(1, m2f::option(m2f::kOptMsdaFwdTile, 8));
+  const int tw = std::max(1, m2f::option(m2f::kOptMsdaFwdTileW, 16));
+  geo.nty = (geo.H[fi] + th - 1) / th;
+  geo.ntx = (geo.W[fi] + tw - 1) / tw;
+  geo.max_halo = std::max(0, m2f::option(m2f::kOptMsdaFwdHalo, 8));
+  const int cap = std::min(m2f::option(m2f::kOptMsdaFwdCap, kFwdLdsCap), kFwdLdsCap) & ~7;
+  int qt = 0, own = 0;
+  for (int l = 0; l < d.L; ++l) {
+    const int h = (geo.H[l] + geo.nty - 1) / geo.nty, w = (geo.W[l] + geo.ntx - 1) / geo.ntx;
+    qt += h * w;
+    own = std::max(own, std::min(h + 1, geo.H[l]) * std::min(w + 1, geo.W[l]));
+  }
+  if (qt > kFwdLdsRounds * (kFwdLdsThreads / 4) || cap < own) return false;
+  geo.max_rows = cap;
+  geo.max_qt = qt;
+  lds = 0;  // static
+  return true;
+}
+
 }  // namespace
 
 extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
@@ -1740,6 +2088,23 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
   const bool off32 = static_cast<int64_t>(d.N) * std::max(d.S, d.Lq) * d.M * d.D < (int64_t{1} << 31);
   // quad form: byte offsets in 32-bit int arithmetic (value bytes < 2^31)
   const bool boff31 = static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 < (int64_t{1} << 31);
+  TileGeom lgeo;
+  size_t llds = 0;
+  if (m2f::option(m2f::kOptMsdaFwdLds, 1) != 0 && m2f::option(m2f::kOptMsdaFwdQuad, 1) != 0 &&
+      m2f::option(m2f::kOptMsdaFwdTiled, 1) != 0 && make_fwd_lds_geom(d, proj_ld, geo, lgeo, llds)) {
+    const int64_t nb = static_cast<int64_t>(lgeo.nty) * lgeo.ntx * d.M * d.N;
+    if (nb > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many workgroups", fn);
+    const unsigned tg = static_cast<unsigned>(nb);
+#define M2F_FL(LT) msda_fused_fwd_lds<LT><<<tg, kFwdLdsThreads, llds, st>>>(value, fe, lgeo, d.S, d.M, output)
+    switch (d.L) {
+      case 1: M2F_FL(1); break;
+      case 2: M2F_FL(2); break;
+      case 3: M2F_FL(3); break;
+      default: M2F_FL(4); break;
+    }
+#undef M2F_FL
+    return m2f::check_launch(fn);
+  }
   if (boff31 && d.Lq == d.S && m2f::option(m2f::kOptMsdaFwdQuad, 1) != 0 && m2f::option(m2f::kOptMsdaFwdTiled, 1) != 0) {
     int64_t T = 0;
     for (int l = 0; l < d.L; ++l) T += static_cast<int64_t>((geo.H[l] + 7) / 8) * ((geo.W[l] + 7) / 8);

@@ -499,6 +499,7 @@ class _FlatCast(Function):
 
     @staticmethod
     def forward(ctx, dtype, *params):
+        ctx.set_materialize_grads(False)  # an output no loss reached arrives as None, not zeros
         ctx.shapes = [p.shape for p in params]
         ctx.numels = [p.numel() for p in params]
         ctx.src_dtype = params[0].dtype
@@ -507,12 +508,16 @@ class _FlatCast(Function):
 
     @staticmethod
     def backward(ctx, *grads):
-        ref = next((g for g in grads if g is not None), None)
-        if ref is None:
+        # a parameter no output reached keeps grad None (as autocast's per-call casts leave it), so AdamW skips
+        # it as the reference's optimizer does; the others are cast back in one cat + cast
+        live = [i for i, g in enumerate(grads) if g is not None]
+        if not live:
             return (None,) * (len(grads) + 1)
-        parts = [(g if g is not None else ref.new_zeros(sh)).reshape(-1) for g, sh in zip(grads, ctx.shapes)]
-        flat = torch.cat(parts).to(ctx.src_dtype)
-        return (None,) + tuple(o.view(sh) for o, sh in zip(flat.split(ctx.numels), ctx.shapes))
+        flat = torch.cat([grads[i].reshape(-1) for i in live]).to(ctx.src_dtype)
+        out = [None] * len(grads)
+        for i, o in zip(live, flat.split([ctx.numels[i] for i in live])):
+            out[i] = o.view(ctx.shapes[i])
+        return (None,) + tuple(out)
 
 
 _LOWP = [None]   # {id(param): low-precision view} of the decoder forward in progress (lowp_scope)

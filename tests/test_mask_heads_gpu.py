@@ -38,7 +38,7 @@ def _fold(f, T):
 def _check_logits(out, e, f, dt):
     """Within one dtype ulp of the exact (fp64) product of the same operands rounded once.  (An fp32 GEMM
     rounded to the dtype is itself up to 1 ulp off that, so it is not the yardstick: the two may sit 2 ulp
-    apart near a binade edge, as measured with tools/dbg_mask_heads.py.)"""
+    apart near a binade edge, as measured in round 2.)"""
     B, C = f.shape[:2]
     ref = torch.bmm(e.double(), f.double().reshape(B, C, -1)).to(out.dtype).view(out.shape)
     d = (out.float() - ref.float()).abs()

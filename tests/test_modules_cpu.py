@@ -62,3 +62,18 @@ def test_decoder_forward_backward_cpu(fixture):
         for key in g.files:
             if key.startswith("pgrad_"):
                 assert rel_err(params[key[6:]].grad, g[key]) < 1e-4, key
+
+
+def test_flat_cast_leaves_unreached_parameters_without_grad():
+    """The decoder's one-buffer weight cast (decoder_ops._FlatCast) returns the cast gradients of the parameters an
+    output reached and None for the others (autocast's per-call casts leave those None, and AdamW skips them)."""
+    from bm2f_amd.decoder_ops import _FlatCast
+    a = torch.randn(3, 4, requires_grad=True)
+    b = torch.randn(5, requires_grad=True)
+    c = torch.randn(2, 2, requires_grad=True)
+    la, lb, lc = _FlatCast.apply(torch.float16, a, b, c)
+    assert la.dtype == torch.float16 and torch.equal(la, a.detach().half())
+    (la.float().sum() * 2 + lc.float().pow(2).sum()).backward()
+    assert b.grad is None
+    torch.testing.assert_close(a.grad, torch.full_like(a, 2.0))
+    torch.testing.assert_close(c.grad, (2 * c.detach().half().float()).half().float())

@@ -197,9 +197,19 @@ def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, overlap
         _tiled_backward_case(device, tile, rows)
 
 
-def _tiled_backward_case(device, tile, rows):
+@pytest.mark.parametrize("shapes,tile,tile_w", [([(48, 48)], 24, 24), ([(24, 24), (48, 48)], 24, 24),
+                                                ([(64, 64)], 16, 32), ([(32, 64)], 16, 32)])
+def test_tiled_backward_large_tiles_vs_oracle(device, shapes, tile, tile_w):
+    """Tiles of more than 512 queries (phase 3's slots hold a g-row byte offset below 2^16) take the untiled
+    kernel; 512 exactly stays tiled.  1- and 2-level pyramids, against the C oracle."""
+    from bm2f_amd import _native
+    with _native.options(msda_tile=tile, msda_tile_w=tile_w, msda_threads=1024):
+        _tiled_backward_case(device, tile, 0, shapes)
+
+
+def _tiled_backward_case(device, tile, rows, shapes=((6, 10), (12, 20), (24, 40))):
     from bm2f_amd import _native, msda
-    shapes = [(6, 10), (12, 20), (24, 40)]   # non-square, tiles not dividing every level evenly
+    shapes = [tuple(s) for s in shapes]   # default: non-square, tiles not dividing every level evenly
     value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 2, 8, 0.05, tile + rows)
     dst = msda.attach_host_shapes(st.to(device), shapes)
     gv, gl, ga = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
@@ -328,12 +338,12 @@ def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
 
 @pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(5, 7), (10, 13), (20, 26)],
                                     [(9, 17)], [(4, 4), (8, 8), (16, 16), (32, 32)], [(6, 10), (12, 20)]])
-@pytest.mark.parametrize("quad,pb", [(0, 2), (1, 1), (1, 2), (1, 4)])
-def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb):
-    """The fused forward (m2f_msda_fused_fwd_f32) in its quad form (a lane quad per (query, head), point
-    geometry by DPP broadcast, out-of-range points skipped by the exec mask; 1, 2 or 4 points per load batch)
-    and its 8-lane form, against the
-    C oracle on the loc / attn the reference front end derives from the same projection: power-of-two and odd
+@pytest.mark.parametrize("quad,pb,lds", [(0, 2, 0), (1, 1, 0), (1, 2, 0), (1, 4, 0), (1, 2, 1)])
+def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb, lds):
+    """The fused forward (m2f_msda_fused_fwd_f32) in its LDS-window form (value windows staged in LDS per tile and
+    level, the default), its quad form (a lane quad per (query, head), point geometry by DPP broadcast,
+    out-of-range points skipped by the exec mask; 1, 2 or 4 points per load batch) and its 8-lane form, against
+    the C oracle on the loc / attn the reference front end derives from the same projection: power-of-two and odd
     level shapes (tile edges), 1-4 levels, 5 % of the samples thrown far (out of the level and out of range)."""
     from bm2f_amd import _native
     from bm2f_amd.msda import MSDeformAttnFusedFunction
@@ -343,7 +353,7 @@ def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb):
     value, proj, ref = _fused_case(shapes, N, 0.05, seed=21 + L)
     S = value.shape[1]
     rf = ref.float()[None, :, None, :].expand(N, S, L, 2).to(device)
-    with _native.options(msda_fwd_quad=quad, msda_fwd_pb=pb):
+    with _native.options(msda_fwd_quad=quad, msda_fwd_pb=pb, msda_fwd_lds=lds):
         out = MSDeformAttnFusedFunction.apply(value.to(device), proj.to(device), rf, tuple(shapes), P)
     torch.cuda.synchronize()
     loc, attn = _loc_attn(proj, ref, shapes)
@@ -351,6 +361,31 @@ def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb):
     lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
     want = msda_ref.msda_forward(value.double(), st, lsi, loc, attn)
     _close(out.cpu(), want)
+
+
+@pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(5, 7), (10, 13), (20, 26)], [(9, 17)],
+                                    [(4, 4), (8, 8), (16, 16), (32, 32)], [(6, 10), (12, 20)]])
+@pytest.mark.parametrize("tile,tile_w,cap,halo", [(4, 8, 64, 2), (16, 16, 1024, 8), (8, 16, 96, 0), (3, 5, 48, 1)])
+def test_fused_forward_lds_geometries_bitwise(device, shapes, tile, tile_w, cap, halo):
+    """The LDS-window forward computes each output element with the quad kernel's arithmetic in the same order,
+    so every window geometry (tile, window rows, halo; small budgets force the halo to shrink and send samples
+    to the HBM path) returns the quad kernel's output bit for bit, 5 % of the samples thrown far."""
+    from bm2f_amd import _native
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    from test_scale_gpu import _fused_case
+    N, P = 2, 4
+    L = len(shapes)
+    value, proj, ref = _fused_case(shapes, N, 0.05, seed=41 + L)
+    S = value.shape[1]
+    args = (value.to(device), proj.to(device), ref.float()[None, :, None, :].expand(N, S, L, 2).to(device),
+            tuple(shapes), P)
+    with _native.options(msda_fwd_lds=0):
+        want = MSDeformAttnFusedFunction.apply(*args)
+    with _native.options(msda_fwd_lds=1, msda_fwd_tile=tile, msda_fwd_tile_w=tile_w, msda_fwd_cap=cap,
+                         msda_fwd_halo=halo):
+        got = MSDeformAttnFusedFunction.apply(*args)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
 
 
 @pytest.mark.parametrize("shapes", [[(5, 7), (10, 13), (20, 26)], [(9, 17)], [(4, 4), (8, 8), (16, 16), (32, 32)],

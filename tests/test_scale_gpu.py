@@ -134,6 +134,36 @@ def fused_fwd_bwd_vs_oracle(device, shapes, N, far, seed):
     _close(gp[..., M * L * P * 2:], d_logit, atol_frac=1e-4)
 
 
+@pytest.mark.parametrize("regime", ["reference_init", "spread4px", "far5pct", "uniform"])
+def test_fused_forward_lds_config2_bitwise_vs_quad(device, regime):
+    """The LDS-window forward (the default) against the quad kernel at config 2's full pyramid, N=2: bit-identical
+    outputs in the sampling regimes the windows meet -- the reference init, N(0, 4 px) offsets (a trained model's
+    spread: boxes grow, the halo clips them, samples spill to the HBM path), 5 % far samples, and uniformly random
+    locations (nearly every sample outside the windows)."""
+    from bm2f_amd import _native
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    N, M, L, P = 2, 8, 3, 4
+    value, proj, ref = _fused_case(SHAPES_1024, N, 0.05 if regime == "far5pct" else 0.0, seed=17)
+    S = value.shape[1]
+    g = torch.Generator().manual_seed(23)
+    off = proj[..., :M * L * P * 2].view(N, S, M, L, P, 2)
+    if regime == "spread4px":
+        off.add_(torch.randn(off.shape, generator=g) * 4.0)
+    elif regime == "uniform":
+        wh = torch.tensor([[w_, h_] for h_, w_ in SHAPES_1024], dtype=torch.float32).view(1, 1, 1, L, 1, 2)
+        loc = torch.rand(off.shape, generator=g)
+        off.copy_((loc - ref.float()[None, :, None, None, None, :]) * wh)
+    args = (value.to(device), proj.to(device), ref.float()[None, :, None, :].expand(N, S, L, 2).to(device),
+            tuple(SHAPES_1024), P)
+    with _native.options(msda_fwd_lds=0):
+        want = MSDeformAttnFusedFunction.apply(*args)
+    with _native.options(msda_fwd_lds=1):
+        got = MSDeformAttnFusedFunction.apply(*args)
+    torch.cuda.synchronize()
+    assert torch.isfinite(got).all()
+    assert torch.equal(got, want)
+
+
 def test_fused_msda_config2_backward_repeatable(device):
     """Two backward runs at full size agree to fp32 summation-order rounding (grad_value rows are summed in
     list order inside a workgroup and added across workgroups with fp32 atomics, like the reference's own
@@ -214,6 +244,35 @@ def test_fused_msda_deterministic_mode_nonfinite_grad(device):
     wv, _, _ = msda_ref.msda_backward(value.double(), st, lsi, loc, attn, gout.double())
     got = v.grad.cpu().double().numpy()
     assert np.array_equal(np.isnan(got), np.isnan(wv)) and np.isnan(wv).any()
+    fin = np.isfinite(wv)
+    np.testing.assert_allclose(got[fin], wv[fin], rtol=1e-3, atol=1e-5 * np.abs(wv[fin]).max())
+
+
+def test_fused_msda_deterministic_mode_nonfinite_logit(device):
+    """Deterministic mode with a NaN logit in the projection (grad_output finite, so the pre-pass keeps the
+    fixed-point path): the NaN contributions reach grad_value in fp32 and the conversion adds the fixed-point sums
+    to them, so grad_value is NaN in exactly the oracle's elements (not the int64 conversion's garbage) and equal
+    elsewhere."""
+    from bm2f_amd import _native
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    shapes = [(8, 8), (16, 16)]
+    N, L, M, P = 1, 2, 8, 4
+    value, proj, ref = _fused_case(shapes, N, 0.05, seed=4)
+    S = value.shape[1]
+    proj[0, 70, M * L * P * 2 + 3 * L * P + 5] = float("nan")   # query 70, head 3, level 1 point 1
+    gout = torch.randn(N, S, 256, generator=torch.Generator().manual_seed(9))
+    v = value.to(device).requires_grad_()
+    pj = proj.to(device).requires_grad_()
+    rf = ref.float().to(device)[None, :, None, :].expand(N, S, L, 2)
+    with _native.options(msda_bwd_det=1):
+        MSDeformAttnFusedFunction.apply(v, pj, rf, tuple(shapes), P).backward(gout.to(device))
+    loc, attn = _loc_attn(proj, ref, shapes)
+    st = torch.tensor(shapes, dtype=torch.int64)
+    lsi = torch.cat((st.new_zeros(1), st.prod(1).cumsum(0)[:-1]))
+    wv, _, _ = msda_ref.msda_backward(value.double(), st, lsi, loc, attn, gout.double())
+    got = v.grad.cpu().double().numpy()
+    assert np.isnan(wv).any()
+    assert np.array_equal(np.isnan(got), np.isnan(wv))
     fin = np.isfinite(wv)
     np.testing.assert_allclose(got[fin], wv[fin], rtol=1e-3, atol=1e-5 * np.abs(wv[fin]).max())
 

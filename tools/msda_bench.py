@@ -115,6 +115,7 @@ def main():
     ap.add_argument("--no-host-shapes", action="store_true")
     ap.add_argument("--noise", type=float, default=1.0, help="px std of the offsets around the init rays")
     ap.add_argument("--bwd-only", action="store_true")
+    ap.add_argument("--fwd-only", action="store_true")
     ap.add_argument("--fused", action="store_true", help="the fused front-end kernels (the path the bench step runs)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library option (m2f_set_option) for this run, repeatable; e.g. --opt msda_fwd_quad=0")
@@ -137,7 +138,7 @@ def main():
         fwd = lambda: msda.ms_deform_attn_forward(v, st, lsi, loc, attn, 64)  # noqa: E731
         bwd = lambda: msda.ms_deform_attn_backward(v, st, lsi, loc, attn, gout, 64)  # noqa: E731
     tf = 0.0 if a.bwd_only else timeit(fwd, a.iters)
-    tb = timeit(bwd, a.iters)
+    tb = float("nan") if a.fwd_only else timeit(bwd, a.iters)
     tf = tf or float("nan")
     print(f"N={a.n} res={r} fused={a.fused} opts={','.join(a.opt) or '-'} stress={a.stress} noise={a.noise} : fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
           f"bwd {tb:.3f} ms ({bwd_bytes / tb / 1e6:.0f} GB/s alg)")

@@ -73,6 +73,7 @@ def summarize(per):
                   "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE"):
             if c in mean:
                 row[c] = mean[c]
+        row["counters"] = {c: v for c, v in mean.items() if c != "_dur"}
         rows.append(row)
     rows.sort(key=lambda r: -r["total_ms"])
     return rows
@@ -83,6 +84,7 @@ def main():
     ap.add_argument("csv", nargs="+")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--all", action="store_true", help="every counter's per-dispatch mean, per kernel")
     a = ap.parse_args()
     rows = summarize(load(a.csv))
     cols = ["dispatches", "mean_ms", "total_ms", "clk_GHz", "mfma_busy", "mfma_BF16_TF", "mfma_BF16_frac",
@@ -91,6 +93,11 @@ def main():
     for r in rows[: a.top]:
         print(r["kernel"][:69].ljust(70) + "".join(
             (f"{r[c]:13.4g}" if isinstance(r.get(c), float) else str(r.get(c, "")).rjust(13)) for c in cols))
+    if a.all:
+        for r in rows[: a.top]:
+            print(f"\n{r['kernel']}  ({r['dispatches']} dispatches, {r['mean_ms']:.4f} ms)")
+            for c, v in sorted(r["counters"].items()):
+                print(f"  {c:32s} {v:16.6g}")
     if a.json:
         with open(a.json, "w") as f:
             json.dump(rows, f, indent=1)
