@@ -174,6 +174,9 @@ MFMA_NOTE = {
     "mask_heads_fwd": "bqc,bchw->bqhw on bf16/f16 MFMA with the fused bitmask epilogue (HBM-bound: mfma_tflops)",
     "mask_heads_bwd_embed": "d embed = G F^T on bf16/f16 MFMA, split over HW (HBM-bound: mfma_tflops)",
     "mask_heads_bwd_feats": "d features = sum_h E_h^T G_h on bf16/f16 MFMA over the heads in place (HBM-bound)",
+    "masked_attn_fwd": "flash-style masked attention on 16x16x32 bf16/f16 MFMA: 4 B H Lq Lk hd flops (HBM-bound: "
+                       "mfma_tflops)",
+    "masked_attn_bwd": "its backward (P recomputed from the saved LSE): 10 B H Lq Lk hd flops (HBM-bound: mfma_tflops)",
 }
 
 
@@ -332,6 +335,65 @@ def head_config_line(args, world, value, knobs):
                        "model": "video_maskformer2_swin_tiny head", "global_batch": world * args.batch,
                        "frames": frames, "seq_len": 5040, "queries": args.queries, "parallelism": f"dp{world}",
                        "env": knobs}}
+
+
+def _msda_layer_case(device, n, res, noise, seed=7):
+    """Config-2 layer-shaped MSDA inputs: reference-init rays (ms_deform_attn.py:66-80, 1..P px per level) plus
+    N(0, noise px) offsets around each query's reference point, random logits, value and grad_output."""
+    import math
+    import torch
+    shapes = [(res // s, res // s) for s in (32, 16, 8)]
+    M, D, L, P = 8, 32, 3, 4
+    S = sum(h * w for h, w in shapes)
+    g = torch.Generator(device=device).manual_seed(seed)
+    refs = []
+    for h, w in shapes:
+        ys, xs = torch.meshgrid(torch.linspace(0.5, h - 0.5, h, device=device),
+                                torch.linspace(0.5, w - 0.5, w, device=device), indexing="ij")
+        refs.append(torch.stack([xs.reshape(-1) / w, ys.reshape(-1) / h], -1))
+    ref = torch.cat(refs, 0)
+    th = torch.arange(M, device=device) * (2 * math.pi / M)
+    grid = torch.stack([th.cos(), th.sin()], -1)
+    grid = grid / grid.abs().max(-1, keepdim=True)[0]
+    off = (grid.view(M, 1, 1, 2) * torch.arange(1, P + 1, device=device).view(1, 1, P, 1)).expand(M, L, P, 2)
+    off = off[None, None] + noise * torch.randn(n, S, M, L, P, 2, device=device, generator=g)
+    logits = torch.randn(n, S, M, L * P, device=device, generator=g)
+    value = torch.randn(n, S, M, D, device=device, generator=g)
+    gout = torch.randn(n, S, M * D, device=device, generator=g)
+    proj = torch.cat([off.reshape(n, S, -1), logits.reshape(n, S, -1)], -1).contiguous()
+    rf = ref[None, :, None, :].expand(n, S, L, 2).contiguous()
+    return shapes, value, proj, rf, gout
+
+
+def measure_spread(device, n, res, timer, noise=4.0, iters=5):
+    """The fused MSDA kernels (what the step runs) at the config-2 layer shape in the sampling regime of a trained
+    model: reference-init rays plus N(0, 4 px) offsets (the step's own encoder sees near-init offsets).  The
+    backward's windows then spill samples to the direct path and flush more rows."""
+    import torch
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    shapes, value, proj, rf, gout = _msda_layer_case(device, n, res, noise, seed=11)
+    v, pj = value.requires_grad_(), proj.requires_grad_()
+
+    def step():
+        MSDeformAttnFusedFunction.apply(v, pj, rf, tuple(shapes), 4).backward(gout)
+    step()
+    torch.cuda.synchronize()
+    saved, timer.events, timer.enabled = timer.events, {}, True
+    for _ in range(iters):
+        step()
+    res_k = timer.summary(iters)
+    timer.events, timer.enabled = saved, False
+    out = []
+    for fam in ("msda_fwd", "msda_bwd"):
+        if res_k.get(fam):
+            ent = roofline_entry(fam, res_k[fam], "hbm")
+            ent["kernel"] = f"{fam}_spread{noise:g}"
+            ent["note"] = (f"fused kernels, config-2 layer shape, reference-init rays + N(0, {noise:g} px) offsets "
+                           f"(a trained model's spread), mean of {iters} launches")
+            out.append(ent)
+    del v, pj, value, proj, rf, gout
+    torch.cuda.empty_cache()
+    return out
 
 
 def measure_dropin(device, n, res, timer, kern, iters=5):
@@ -510,8 +572,10 @@ def main():
         timer.enabled = False
 
     dropin = None
+    spread = []
     if world == 1 and args.config == 2 and not args.no_dropin:
         dropin = measure_dropin(device, args.batch, args.res, timer, kern)
+        spread = measure_spread(device, args.batch, args.res, timer)
     modes = None
     if world == 1 and args.config == 2 and not args.no_modes:
         modes = {}
@@ -545,6 +609,7 @@ def main():
         bounds = {v[0]: v[1] for v in ENTRIES.values()}
         roof_all = [add_achievable(roofline_entry(fam, k, bounds[fam]), peaks)
                     for fam, k in sorted(kern.items(), key=lambda x: -x[1]["total_ms"])]
+        roof_all += [add_achievable(ent, peaks) for ent in spread]
         cpu = None
         if world == 1 and args.config == 2 and not args.no_cpu_baseline:
             from oracle.cpu_path import cpu_model, time_cpu_step

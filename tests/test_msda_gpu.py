@@ -365,7 +365,8 @@ def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb, lds):
 
 @pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(5, 7), (10, 13), (20, 26)], [(9, 17)],
                                     [(4, 4), (8, 8), (16, 16), (32, 32)], [(6, 10), (12, 20)]])
-@pytest.mark.parametrize("tile,tile_w,cap,halo", [(4, 8, 64, 2), (16, 16, 1024, 8), (8, 16, 96, 0), (3, 5, 48, 1)])
+@pytest.mark.parametrize("tile,tile_w,cap,halo", [(4, 8, 64, 2), (16, 16, 1024, 8), (8, 16, 96, 0), (3, 5, 48, 1),
+                                               (8, 16, 312, 4)])
 def test_fused_forward_lds_geometries_bitwise(device, shapes, tile, tile_w, cap, halo):
     """The LDS-window forward computes each output element with the quad kernel's arithmetic in the same order,
     so every window geometry (tile, window rows, halo; small budgets force the halo to shrink and send samples
