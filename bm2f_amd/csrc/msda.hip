@@ -1511,10 +1511,15 @@ __device__ __forceinline__ void quad_gather_win(const char* __restrict__ vbytes,
 // window row r's LDS byte base (the 64-byte halves swapped when bit 1 of r is set)
 __device__ __forceinline__ unsigned win_row(int r) { return (static_cast<unsigned>(r) << 7) | ((r & 2) << 5); }
 
-template <int LT>
+// FUSED: the samples come from the projection and the reference points (fe); otherwise (the reference op's
+// interface, m2f_msda_fwd_f32) from materialised sampling locations loc (N, S, M, L, P, 2) and attention weights
+// attn (N, S, M, L, P), the encoder layout (query i at pyramid position i; host shapes).
+template <int LT, bool FUSED = true>
 __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const float* __restrict__ value, FrontEnd fe,
                                                                       TileGeom geo, int S, int M,
-                                                                      float* __restrict__ out) {
+                                                                      float* __restrict__ out,
+                                                                      const float* __restrict__ loc = nullptr,
+                                                                      const float* __restrict__ attn = nullptr) {
   constexpr int D = 32, P = 4, LP = LT * P, R = kFwdLdsRounds, NW = kFwdLdsThreads / 64;
   // one static array (a constant base folds into the ds_read addresses): window rows | per-wave boxes [LT][NW]
   __shared__ __attribute__((aligned(16))) unsigned char smem[kFwdLdsCap * 128 + kTileMaxL * NW * 16];
@@ -1569,6 +1574,7 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
 #pragma unroll
     for (int l = 0; l < LT; ++l) st = l == lq ? geo.start[l] : st;
     qpos[r] = st + (y0 + yy) * W + x0 + xx;
+    if constexpr (!FUSED) continue;  // the attention weights are read per level
     // softmax over the pair's L*P logits, exactly as msda_fused_fwd_q4 (and the backward's recomputation)
     const unsigned lgb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>(M * LP * 2 + m * LP + j) * 4u;
     float e[LT];
@@ -1602,6 +1608,10 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
   for (int l = 0; l < LT; ++l) {
     const int H = geo.H[l], W = geo.W[l];
     const int lbase = ((n * S + geo.start[l]) * M + m) * D * 4;
+    // the level's loads hang on an opaque zero defined here, after the previous level's gather: otherwise the
+    // compiler hoists every level's loads to the kernel's start and spills
+    int zq = 0;
+    asm volatile("" : "+v"(zq));
     // 1. lane j's point (l, j) of each round's query: corner block (y0, x0) clamped into the level, whether the
     //    +1 row / column is a corner inside the level (ey, ex), the four weights (x attention weight), ok
     int gy[R], gx[R], gfl[R];
@@ -1613,12 +1623,21 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
       const float fHm1 = static_cast<float>(H - 1), fWm1 = static_cast<float>(W - 1);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const unsigned rfb = static_cast<unsigned>(qpos[r] * LT + l) * 8u;
-        const unsigned ofb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>((m * LP + l * P + j) * 2) * 4u;
-        const float2 rf = *reinterpret_cast<const float2*>(rbytes + rfb);
-        const float2 off = *reinterpret_cast<const float2*>(pbytes + ofb);
-        const float sx = rf.x + div_norm(off.x, fW, geo.invW[l], POW2);
-        const float sy = rf.y + div_norm(off.y, fH, geo.invH[l], POW2);
+        float sx, sy;
+        if constexpr (FUSED) {
+          const unsigned rfb = static_cast<unsigned>((qpos[r] + zq) * LT + l) * 8u;
+          const unsigned ofb = static_cast<unsigned>(n * S + qpos[r] + zq) * pld + static_cast<unsigned>((m * LP + l * P + j) * 2) * 4u;
+          const float2 rf = *reinterpret_cast<const float2*>(rbytes + rfb);
+          const float2 off = *reinterpret_cast<const float2*>(pbytes + ofb);
+          sx = rf.x + div_norm(off.x, fW, geo.invW[l], POW2);
+          sy = rf.y + div_norm(off.y, fH, geo.invH[l], POW2);
+        } else {
+          const unsigned ki = static_cast<unsigned>(((n * S + qpos[r] + zq) * M + m) * LP + l * P + j);
+          const float2 xy = *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(loc) + ki * 8u);
+          sx = xy.x;
+          sy = xy.y;
+          wa[r][l] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(attn) + ki * 4u);
+        }
         const float h = sy * H - 0.5f, w = sx * W - 0.5f;
         const bool ok = ((vmask >> r) & 1u) && h > -1.f && w > -1.f && h < fH && w < fW;
         const float hs = ok ? h : -2.f, ws = ok ? w : -2.f;
@@ -1636,13 +1655,17 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
         gy[r] = y0;
         gx[r] = x0;
         gfl[r] = (ok ? 1 : 0) | (ey << 1) | (ex << 2);
+        // materialised here: left to the compiler, the weights sink past the barriers into the gather and their
+        // inputs (fractions, corner masks) stay live instead
+        asm volatile("" : "+v"(gw[r][0]), "+v"(gw[r][1]), "+v"(gw[r][2]), "+v"(gw[r][3]), "+v"(gy[r]), "+v"(gx[r]),
+                     "+v"(gfl[r]));
         if (ok) {
           bmin_y = min(bmin_y, y0); bmax_y = max(bmax_y, y0 + ey);
           bmin_x = min(bmin_x, x0); bmax_x = max(bmax_x, x0 + ex);
         }
       }
     };
-    if (((W & (W - 1)) | (H & (H - 1))) == 0) geometry(std::true_type{});
+    if (FUSED && ((W & (W - 1)) | (H & (H - 1))) == 0) geometry(std::true_type{});
     else geometry(std::false_type{});
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1700,6 +1723,8 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
       const unsigned a3 = inwin ? win_row(r3) : g1 + dy, a4 = inwin ? win_row(r3 + ex) : g1 + dy + dx;
       const int md = ok ? (inwin ? 1 : 2) : 0;
       quad_gather_win(vbytes, (const __attribute__((address_space(3))) unsigned char*)smem, md, a1, a2, a3, a4, gw[r][0], gw[r][1], gw[r][2], gw[r][3], cjb, acc0[r], acc1[r]);
+      if constexpr (!FUSED) asm volatile("" ::: "memory");  // one round's gather at a time (else the scheduler
+                                                             // overlaps rounds and spills)
     }
   }
 #pragma unroll
@@ -1766,16 +1791,22 @@ void launch_bwd_vec(const float* value, const int64_t* shapes, const int64_t* ls
                                                   d.L, d.Lq, d.P, gv, gl, ga);
 }
 
+bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeom& geo, size_t& lds);
+bool launch_fwd_lds_unfused(const float* value, const float* loc, const float* attn, const Dims& d,
+                            const int64_t* host_shapes, float* out, hipStream_t st);
+
 template <typename T>
 int fwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_t* lsi, const T* loc,
-             const T* attn, const Dims& d, int im2col_step, T* out, hipStream_t st) {
+             const T* attn, const Dims& d, int im2col_step, T* out, hipStream_t st,
+             const int64_t* host_shapes = nullptr) {
   int rc = check_dims(fn, value, shapes, lsi, loc, attn, d, im2col_step);
   if (rc) return rc;
   if (!out) return m2f::fail(M2F_EINVAL, "%s: null output", fn);
   bool done = false;
   if constexpr (std::is_same<T, float>::value) {
     if (fast_f32_ok(d, value, loc, out)) {
-      if (d.D == 16) launch_fwd_vec<16>(value, shapes, lsi, loc, attn, d, out, st);
+      if (launch_fwd_lds_unfused(value, loc, attn, d, host_shapes, out, st)) {
+      } else if (d.D == 16) launch_fwd_vec<16>(value, shapes, lsi, loc, attn, d, out, st);
       else if (d.D == 32 && d.P == 4 && m2f::option(m2f::kOptMsdaFwdQuad, 1) != 0 &&
                static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 < (int64_t{1} << 31))
         msda_fwd_f32_q4<<<m2f::ceil_div(d.npairs(), 64), 256, 0, st>>>(value, shapes, lsi, loc, attn, d.npairs(), d.S,
@@ -1958,10 +1989,9 @@ extern "C" int m2f_msda_fwd_f32(const float* value, const int64_t* spatial_shape
                                 const float* sampling_loc, const float* attn_weight, int batch, int spatial_size,
                                 int num_heads, int channels, int num_levels, int num_query, int num_point,
                                 int im2col_step, const int64_t* host_spatial_shapes, float* output, void* stream) {
-  (void)host_spatial_shapes;
   const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
   return fwd_impl<float>("m2f_msda_fwd_f32", value, spatial_shapes, level_start_index, sampling_loc, attn_weight,
-                         d, im2col_step, output, static_cast<hipStream_t>(stream));
+                         d, im2col_step, output, static_cast<hipStream_t>(stream), host_spatial_shapes);
 }
 
 extern "C" int m2f_msda_fwd_f64(const double* value, const int64_t* spatial_shapes,
@@ -2068,6 +2098,44 @@ bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeo
   geo.max_rows = cap;
   geo.max_qt = qt;
   lds = 0;  // static
+  return true;
+}
+
+// The reference op's forward (materialised loc / attn) on the LDS-window kernel: encoder layout with host shapes,
+// the options that select the windowed forward, and every byte offset under 2^31; false otherwise.
+bool launch_fwd_lds_unfused(const float* value, const float* loc, const float* attn, const Dims& d,
+                            const int64_t* host_shapes, float* out, hipStream_t st) {
+  if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L < 1 || d.L > kTileMaxL) return false;
+  if (m2f::option(m2f::kOptMsdaFwdLds, 1) == 0 || m2f::option(m2f::kOptMsdaFwdQuad, 1) == 0 ||
+      m2f::option(m2f::kOptMsdaFwdTiled, 1) == 0)
+    return false;
+  if (!m2f::aligned(loc, 8) || static_cast<int64_t>(d.N) * d.S * d.M * d.L * d.P * 8 >= (int64_t{1} << 31)) return false;
+  TileGeom base{};
+  base.L = d.L;
+  int64_t total = 0;
+  for (int l = 0; l < d.L; ++l) {
+    base.H[l] = static_cast<int>(host_shapes[2 * l]);
+    base.W[l] = static_cast<int>(host_shapes[2 * l + 1]);
+    if (base.H[l] <= 0 || base.W[l] <= 0) return false;
+    base.start[l] = static_cast<int>(total);
+    base.invW[l] = 1.f / static_cast<float>(base.W[l]);
+    base.invH[l] = 1.f / static_cast<float>(base.H[l]);
+    total += static_cast<int64_t>(base.H[l]) * base.W[l];
+  }
+  if (total != d.S) return false;
+  TileGeom geo;
+  size_t lds = 0;
+  if (!make_fwd_lds_geom(d, 0, base, geo, lds)) return false;
+  const int64_t nb = static_cast<int64_t>(geo.nty) * geo.ntx * d.M * d.N;
+  if (nb > 0x7fffffff) return false;
+  const unsigned tg = static_cast<unsigned>(nb);
+  const FrontEnd fe{};
+  switch (d.L) {
+    case 1: msda_fused_fwd_lds<1, false><<<tg, kFwdLdsThreads, lds, st>>>(value, fe, geo, d.S, d.M, out, loc, attn); break;
+    case 2: msda_fused_fwd_lds<2, false><<<tg, kFwdLdsThreads, lds, st>>>(value, fe, geo, d.S, d.M, out, loc, attn); break;
+    case 3: msda_fused_fwd_lds<3, false><<<tg, kFwdLdsThreads, lds, st>>>(value, fe, geo, d.S, d.M, out, loc, attn); break;
+    default: msda_fused_fwd_lds<4, false><<<tg, kFwdLdsThreads, lds, st>>>(value, fe, geo, d.S, d.M, out, loc, attn); break;
+  }
   return true;
 }
 
