@@ -45,7 +45,8 @@ inline unsigned ceil_div(int64_t a, int64_t b) { return static_cast<unsigned>((a
 enum Option : int {
   kOptMsdaThreads, kOptMsdaTile, kOptMsdaTileW, kOptMsdaHalo, kOptMsdaWinRows, kOptMsdaBwdTiled, kOptMsdaFwdTiled,
   kOptMattnDqAtomic, kOptGemmNtCfg, kOptX3TnNw, kOptX3TnBlocks, kOptX3NtCfg, kOptMsdaFwdQuad, kOptMsdaBwdOverlap, kOptMsdaBwdDet, kOptMsdaFwdPb, kOptMsdaBwdRatio,
-  kOptMsdaFwdLds, kOptMsdaFwdTile, kOptMsdaFwdTileW, kOptMsdaFwdCap, kOptMsdaFwdHalo, kOptCount
+  kOptMsdaFwdLds, kOptMsdaFwdTile, kOptMsdaFwdTileW, kOptMsdaFwdCap, kOptMsdaFwdHalo,
+  kOptMattnFwdMinblk, kOptMattnBwdMinblk, kOptCount
 };
 int64_t option_raw(Option o);  // -1 when unset
 inline int option(Option o, int dflt) {

@@ -75,13 +75,33 @@ __device__ __forceinline__ s4 tr_read(const void* lds_ptr) {
       (lds_s4*)(reinterpret_cast<uintptr_t>(lds_ptr)));
 }
 
-__device__ __forceinline__ float wave_max16(float x) {  // reduce over the 4 lane groups (same r)
-  x = fmaxf(x, __shfl_xor(x, 16));
-  return fmaxf(x, __shfl_xor(x, 32));
+// Reduce over the 4 lane groups (same r) with gfx950's row-swap moves (VALU; __shfl_xor is an LDS permute with
+// its round trip): v_permlane16_swap pairs rows 0-1 and 2-3 (lane ^ 16), v_permlane32_swap the halves (lane ^ 32).
+// With both operands the same value, the swapped pair holds {x_lo, x_hi} in every lane of the pair: the sum is
+// x_lo + x_hi on both sides (the order __shfl_xor's x + x^16 gives, float addition being commutative).
+__device__ __forceinline__ float xor16_pair(float x, float& other) {
+  const auto p = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  other = __uint_as_float(p[1]);
+  return __uint_as_float(p[0]);
+}
+__device__ __forceinline__ float xor32_pair(float x, float& other) {
+  const auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  other = __uint_as_float(p[1]);
+  return __uint_as_float(p[0]);
+}
+__device__ __forceinline__ float wave_max16(float x) {
+  float b;
+  float a = xor16_pair(x, b);
+  x = fmaxf(a, b);
+  a = xor32_pair(x, b);
+  return fmaxf(a, b);
 }
 __device__ __forceinline__ float wave_sum16(float x) {
-  x += __shfl_xor(x, 16);
-  return x + __shfl_xor(x, 32);
+  float b;
+  float a = xor16_pair(x, b);
+  x = a + b;
+  a = xor32_pair(x, b);
+  return a + b;
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -478,24 +498,59 @@ __global__ void __launch_bounds__(256) mattn_bwd_kernel(
   const int NT = Lqp / 16;
   const int HD = H * kD;
 
-  // stage Q, dO (rows >= Lq zero), lse, delta; clear dQ accumulator
-  for (int idx = threadIdx.x; idx < Lqp * kD; idx += 256) {
-    const int qi = idx / kD, d = idx % kD;
-    T qv = Elt<T>::from_f(0.f), gv = Elt<T>::from_f(0.f);
-    if (qi < Lq) {
-      qv = q[(static_cast<int64_t>(b) * Lq + qi) * qs + h * kD + d];
-      gv = dout[(static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + d];
+  // stage Q, dO (rows >= Lq zero), lse, delta; clear dQ accumulator.  16-bit operands move in 16-byte pieces (the
+  // 72-byte LDS rows take them as two 8-byte halves); delta = sum_d O dO in d order from a thread's four pieces
+  if constexpr (k16) {
+    for (int idx = threadIdx.x; idx < Lqp * 4; idx += 256) {
+      const int qi = idx >> 2, part = idx & 3;
+      f4 qv = {0.f, 0.f, 0.f, 0.f}, gv = qv;
+      if (qi < Lq) {
+        qv = *reinterpret_cast<const f4*>(q + (static_cast<int64_t>(b) * Lq + qi) * qs + h * kD + part * 8);
+        gv = *reinterpret_cast<const f4*>(dout + (static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + part * 8);
+      }
+      const s4* qh = reinterpret_cast<const s4*>(&qv);
+      const s4* gh = reinterpret_cast<const s4*>(&gv);
+      s4* qd = reinterpret_cast<s4*>(Qs + qi * RS + part * 8);
+      s4* gd = reinterpret_cast<s4*>(dOs + qi * RS + part * 8);
+      qd[0] = qh[0]; qd[1] = qh[1];
+      gd[0] = gh[0]; gd[1] = gh[1];
     }
-    Qs[qi * RS + d] = qv;
-    dOs[qi * RS + d] = gv;
-    dqa[idx] = 0.f;
+    for (int idx = threadIdx.x; idx < Lqp * kD / 4; idx += 256) reinterpret_cast<f4*>(dqa)[idx] = f4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    for (int idx = threadIdx.x; idx < Lqp * kD; idx += 256) {
+      const int qi = idx / kD, d = idx % kD;
+      T qv = Elt<T>::from_f(0.f), gv = Elt<T>::from_f(0.f);
+      if (qi < Lq) {
+        qv = q[(static_cast<int64_t>(b) * Lq + qi) * qs + h * kD + d];
+        gv = dout[(static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + d];
+      }
+      Qs[qi * RS + d] = qv;
+      dOs[qi * RS + d] = gv;
+      dqa[idx] = 0.f;
+    }
   }
   for (int qi = threadIdx.x; qi < Lqp; qi += 256) {
     float dl = 0.f, ls = INFINITY;
     if (qi < Lq) {
       const T* orow = out + (static_cast<int64_t>(b) * Lq + qi) * HD + h * kD;
       const T* grow = dout + (static_cast<int64_t>(b) * Lq + qi) * HD + h * kD;
-      for (int d = 0; d < kD; ++d) dl += Elt<T>::to_f(orow[d]) * Elt<T>::to_f(grow[d]);
+      if constexpr (k16) {
+        f4 ov[4], gv[4];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          ov[p] = *reinterpret_cast<const f4*>(orow + p * 8);
+          gv[p] = *reinterpret_cast<const f4*>(grow + p * 8);
+        }
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const T* oe = reinterpret_cast<const T*>(&ov[p]);
+          const T* ge = reinterpret_cast<const T*>(&gv[p]);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dl += Elt<T>::to_f(oe[e]) * Elt<T>::to_f(ge[e]);
+        }
+      } else {
+        for (int d = 0; d < kD; ++d) dl += Elt<T>::to_f(orow[d]) * Elt<T>::to_f(grow[d]);
+      }
       ls = lse2[static_cast<int64_t>(bh) * Lq + qi];
     }
     del_s[qi] = dl;
@@ -736,17 +791,20 @@ __global__ void __launch_bounds__(256) mattn_dq_reduce_kernel(const float* __res
 // ----------------------------------------------------------------------------------------------
 // host
 // ----------------------------------------------------------------------------------------------
-int plan_chunks(int B, int H, int Lk, int* chunk_len, int* nchunks) {
+// Key chunks per (b, head): aim for >= ~1024 workgroups, but no chunk shorter than minblk key blocks (each
+// workgroup stages its queries and writes a partial once: short chunks are all prologue and epilogue).
+int plan_chunks(int B, int H, int Lk, int* chunk_len, int* nchunks, int minblk = 2) {
   const int BH = B * H;
   const int nblocks = (Lk + 63) / 64;
-  // aim for >= ~1024 workgroups, but no chunk shorter than 2 key blocks
   int per = (nblocks * BH + 1023) / 1024;
-  per = per < 2 ? 2 : per;
+  per = per < minblk ? minblk : per;
   if (per > nblocks) per = nblocks;
   *chunk_len = per * 64;
   *nchunks = (Lk + *chunk_len - 1) / *chunk_len;
   return 0;
 }
+int fwd_minblk() { return std::max(1, m2f::option(m2f::kOptMattnFwdMinblk, 2)); }
+int bwd_minblk() { return std::max(1, m2f::option(m2f::kOptMattnBwdMinblk, 2)); }
 
 size_t bwd_lds_bytes(int Lqp, bool k16, int elt, int dq_copies = 1) {
   const int RS = k16 ? kDP : kD + 1;
@@ -786,7 +844,7 @@ int mattn_fwd_impl(const char* fn, const void* q, const void* k, const void* v, 
       !m2f::aligned(out, 16))
     return m2f::fail(M2F_EINVAL, "%s: misaligned operand or stride", fn);
   int chunk, nch;
-  plan_chunks(B, H, Lk, &chunk, &nch);
+  plan_chunks(B, H, Lk, &chunk, &nch, fwd_minblk());
   const size_t need = nch > 1 ? sizeof(float) * static_cast<size_t>(nch) * B * H * Lq * (kD + 2) : 0;
   if (ws_bytes < need || (need && !ws)) return m2f::fail(M2F_EINVAL, "%s: workspace %zu < %zu", fn, ws_bytes, need);
   float* ws_o = ws;
@@ -829,7 +887,7 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
       !m2f::aligned(dv, 16))
     return m2f::fail(M2F_EINVAL, "%s: misaligned operand or stride", fn);
   int chunk, nch;
-  plan_chunks(B, H, Lk, &chunk, &nch);
+  plan_chunks(B, H, Lk, &chunk, &nch, bwd_minblk());
   const size_t need = nch > 1 ? sizeof(float) * static_cast<size_t>(nch) * B * H * Lq * kD : 0;
   if (ws_bytes < need || (need && !ws)) return m2f::fail(M2F_EINVAL, "%s: workspace %zu < %zu", fn, ws_bytes, need);
   const int Lqp = (Lq + 15) / 16 * 16;
@@ -881,13 +939,14 @@ extern "C" int m2f_attn_mask_bits(const void* logits, int dtype, int batch, int 
 
 extern "C" int m2f_masked_attn_plan(int batch, int num_queries, int num_keys, int num_heads, int* chunk_len,
                                     int* num_chunks, int64_t* fwd_workspace_bytes, int64_t* bwd_workspace_bytes) {
-  int cl, nc;
-  plan_chunks(batch, num_heads, num_keys, &cl, &nc);
+  int cl, nc, clb, ncb;
+  plan_chunks(batch, num_heads, num_keys, &cl, &nc, fwd_minblk());
+  plan_chunks(batch, num_heads, num_keys, &clb, &ncb, bwd_minblk());
   if (chunk_len) *chunk_len = cl;
   if (num_chunks) *num_chunks = nc;
-  const int64_t rows = static_cast<int64_t>(nc) * batch * num_heads * num_queries;
-  if (fwd_workspace_bytes) *fwd_workspace_bytes = nc > 1 ? rows * (kD + 2) * 4 : 0;
-  if (bwd_workspace_bytes) *bwd_workspace_bytes = nc > 1 ? rows * kD * 4 : 0;
+  const int64_t rows = static_cast<int64_t>(batch) * num_heads * num_queries;
+  if (fwd_workspace_bytes) *fwd_workspace_bytes = nc > 1 ? nc * rows * (kD + 2) * 4 : 0;
+  if (bwd_workspace_bytes) *bwd_workspace_bytes = ncb > 1 ? ncb * rows * kD * 4 : 0;
   return m2f::ok();
 }
 

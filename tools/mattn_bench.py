@@ -40,9 +40,15 @@ def timeit(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--dq-atomic", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
+                    help="library option (m2f_set_option) for this run, repeatable; e.g. --opt mattn_bwd_minblk=4")
     a = ap.parse_args()
     if a.dq_atomic:
         _native.set_option("mattn_dq_atomic", 1)
+    for kv in a.opt:
+        k_, v_ = kv.split("=")
+        _native.set_option(k_, int(v_))
+    print(f"opts: {','.join(a.opt) or '-'}", flush=True)
     dev = torch.device("cuda")
     dt = torch.float16
     for B, Q in ((16, 100), (2, 200)):
