@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(256) mattn_combine_kernel(const float* __restr
 // NTR == 0 (more queries) each tile's dQ^T goes to LDS float atomics (~190 cycles per wave-instruction
 // on gfx950, the reason for the other two paths).  Chunks are summed by a reduce pass (deterministic).
 template <typename T, int NTR>
-__global__ void __launch_bounds__(256) mattn_bwd_kernel(
+__global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
     const T* __restrict__ out, const T* __restrict__ dout, const float* __restrict__ lse2, int Lq, int Lk, int H,
     int qs, int kvs, int nw, float sl2, float scale, int chunk_len, int Lqp, T* __restrict__ dq,
@@ -895,11 +895,17 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   // of them fit (config 4's Q = 200), else LDS atomics; option mattn_dq_atomic = 1 forces the atomics
   const bool reg_dq = m2f::option(m2f::kOptMattnDqAtomic, 0) != 1;
   const size_t lds_wave = bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T), 4);
-  const int mode = !reg_dq ? 0 : Lqp <= 128 ? 1 : lds_wave <= 160 * 1024 ? 2 : 0;
+  // registers up to 208 queries (config 4's Q = 200 takes 13 tiles: two waves per SIMD, where the four per-wave LDS
+  // copies of mode 2 hold 106 KB and leave one wave per SIMD); mattn_dq_atomic = 2 forces the per-wave copies
+  const int dqopt = m2f::option(m2f::kOptMattnDqAtomic, 0);
+  const int mode = !reg_dq ? 0 : Lqp <= 128 ? 1 : (Lqp <= 208 && dqopt != 2) ? 3 : lds_wave <= 160 * 1024 ? 2 : 0;
   const size_t lds = mode == 2 ? lds_wave : bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T));
   if (lds > 160 * 1024) return m2f::fail(M2F_EUNSUPPORTED, "%s: %zu B of LDS", fn, lds);
-  auto kern = mode == 1 ? &mattn_bwd_kernel<T, 8> : mode == 2 ? &mattn_bwd_kernel<T, -1> : &mattn_bwd_kernel<T, 0>;
-  static bool attr_set[3][3] = {{false, false, false}, {false, false, false}, {false, false, false}};
+  auto kern = mode == 1   ? &mattn_bwd_kernel<T, 8>
+              : mode == 3 ? &mattn_bwd_kernel<T, 13>
+              : mode == 2 ? &mattn_bwd_kernel<T, -1>
+                          : &mattn_bwd_kernel<T, 0>;
+  static bool attr_set[3][4] = {{false, false, false, false}, {false, false, false, false}, {false, false, false, false}};
   const int ai = std::is_same<T, float>::value ? 0 : (std::is_same<T, __bf16>::value ? 1 : 2);
   const int ki = mode;
   if (!attr_set[ai][ki]) {

@@ -290,10 +290,18 @@ def _random_bits(B, Q, Lk, device, seed, p_block=0.6):
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-@pytest.mark.parametrize("Q,Lk", [(100, 16384), (200, 16384), (200, 4096)])
-def test_masked_attention_long_keys_vs_oracle(device, dtype, Q, Lk):
+@pytest.mark.parametrize("Q,Lk,dq", [(100, 16384, 0), (200, 16384, 0), (200, 4096, 0), (200, 4096, 1), (200, 4096, 2),
+                                     (100, 1024, 0)])
+def test_masked_attention_long_keys_vs_oracle(device, dtype, Q, Lk, dq):
     """Config 2's 1/8 level (Lk = 16,384 keys) at B=2, Q=100 and config 4's Q=200: the key-chunk split and
-    combine of the forward, the chunked dQ reduction of the backward."""
+    combine of the forward, the chunked dQ reduction of the backward; the backward's dQ accumulation in registers
+    (the default up to 208 queries), in LDS float atomics (mattn_dq_atomic 1) and in per-wave LDS copies (2)."""
+    from bm2f_amd import _native
+    with _native.options(mattn_dq_atomic=dq):
+        _masked_attention_case(device, dtype, Q, Lk)
+
+
+def _masked_attention_case(device, dtype, Q, Lk):
     from bm2f_amd import decoder_ops
     B, H, C = 2, 8, 256
     g = torch.Generator(device=device).manual_seed(Q + Lk)
