@@ -36,6 +36,10 @@ import subprocess
 import sys
 import time
 
+# before any HIP call: the runtime's graph packet capture replays captured memsets wrongly on this ROCm
+# (bm2f_amd/__init__.py); the graph-replayed configs need it off
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -70,6 +74,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-dropin", action="store_true", help="skip the op-level MSDeformAttnFunction timing")
     ap.add_argument("--mode-steps", type=int, default=4)
     ap.add_argument("--kernel-steps", type=int, default=2, help="instrumented steps for roofline_all")
+    ap.add_argument("--graph", type=int, default=None, choices=[0, 1],
+                    help="capture the step in a HIP graph and replay it (default: on for the per-rank configs 4 / 5 "
+                         "at one rank, whose small steps are host-launch bound; off for config 2)")
     ap.add_argument("--allow-knobs", action="store_true")
     ap.add_argument("--master-port", type=int, default=29531)
     a = ap.parse_args(argv)
@@ -77,6 +84,8 @@ def parse_args(argv=None):
         a.batch = 16 if a.config == 2 else 2
     if a.queries is None:
         a.queries = 200 if a.config == 4 else 100
+    if a.graph is None:
+        a.graph = 1 if a.config in (4, 5) and a.gpus == 1 else 0
     return a
 
 
@@ -174,7 +183,7 @@ MFMA_NOTE = {
     "mask_heads_fwd": "bqc,bchw->bqhw on bf16/f16 MFMA with the fused bitmask epilogue (HBM-bound: mfma_tflops)",
     "mask_heads_bwd_embed": "d embed = G F^T on bf16/f16 MFMA, split over HW (HBM-bound: mfma_tflops)",
     "mask_heads_bwd_feats": "d features = sum_h E_h^T G_h on bf16/f16 MFMA over the heads in place (HBM-bound)",
-    "masked_attn_fwd": "flash-style masked attention on 16x16x32 bf16/f16 MFMA: 4 B H Lq Lk hd flops (HBM-bound: "
+    "masked_attn_fwd": "flash-style masked attention on 16x16x16 bf16/f16 MFMA: 4 B H Lq Lk hd flops (HBM-bound: "
                        "mfma_tflops)",
     "masked_attn_bwd": "its backward (P recomputed from the saved LSE): 10 B H Lq Lk hd flops (HBM-bound: mfma_tflops)",
 }
@@ -504,8 +513,8 @@ def main():
     device = torch.device("cuda", local)
 
     from bm2f_amd import _native
-    from bm2f_amd.bench_model import (HeadBench, MaskFormerR50, default_cfg, head_features, make_optimizer, make_scaler,
-                                      train_step, wrap_ddp)
+    from bm2f_amd.bench_model import (GraphStep, HeadBench, MaskFormerR50, default_cfg, head_features, make_optimizer,
+                                      make_scaler, train_step, wrap_ddp)
 
     timer = KernelTimer()
     timer.install(_native)
@@ -521,28 +530,36 @@ def main():
     else:                    # 2 clips x T frames at 360x640 padded to 384x640, Swin-T features
         model = HeadBench("swin_t", args.queries, 40, frames=args.frames).to(device)
         images = head_features("swin_t", args.batch * args.frames, 384, 640, device, seed=1000 + rank)
+    use_graph = bool(args.graph) and world == 1
     if world > 1:
         model = wrap_ddp(model, device)
-    opt = make_optimizer(model)
+    opt = make_optimizer(model, capturable=use_graph)
     dtypes = {"bf16": torch.bfloat16, "fp16": torch.float16, "none": None}
 
     def barrier():
         if world > 1:
             dist.barrier()
 
-    def run(amp_name, steps, warmup, tag):
+    def run(amp_name, steps, warmup, tag, graph=False):
         amp = dtypes[amp_name]
         scaler = make_scaler(amp)
         t0 = time.perf_counter()
-        for i in range(warmup):
-            train_step(model, opt, images, amp, scaler=scaler)
-            torch.cuda.synchronize()
-            log(f"{tag} warmup {i + 1}/{warmup} done ({time.perf_counter() - t0:.1f}s)")
+        if graph:   # warm-up steps run eagerly inside the capture helper, then the captured step is replayed
+            gstep = GraphStep(model, opt, images, amp, scaler=scaler, warmup=max(warmup, 2))
+            step_fn = gstep
+            log(f"{tag} warmup {warmup} + capture done ({time.perf_counter() - t0:.1f}s)")
+        else:
+            def step_fn():
+                return train_step(model, opt, images, amp, scaler=scaler)
+            for i in range(warmup):
+                step_fn()
+                torch.cuda.synchronize()
+                log(f"{tag} warmup {i + 1}/{warmup} done ({time.perf_counter() - t0:.1f}s)")
         barrier()
         torch.cuda.synchronize()
         start = last = time.perf_counter()
         for i in range(steps):
-            train_step(model, opt, images, amp, scaler=scaler)
+            step_fn()
             if time.perf_counter() - last > 30:
                 log(f"{tag} step {i + 1}/{steps}")
                 last = time.perf_counter()
@@ -556,7 +573,7 @@ def main():
         log(f"{tag}: {steps} steps in {elapsed:.3f}s")
         return elapsed
 
-    elapsed = run(args.amp, args.steps, args.warmup, "timed")
+    elapsed = run(args.amp, args.steps, args.warmup, "timed", graph=use_graph)
     peaks = None
     if world == 1 and not args.no_peaks:
         peaks = measure_peaks(device)
@@ -641,6 +658,7 @@ def main():
         }
         if args.config in (4, 5):
             line.update(head_config_line(args, world, value, knobs))
+        line["config"]["graph_replay"] = use_graph
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

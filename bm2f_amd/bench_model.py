@@ -334,6 +334,23 @@ def wrap_ddp(model, device=None):
     return torch.nn.parallel.DistributedDataParallel(model, **kw)
 
 
+def graph_safe_sum(x):
+    """``x.sum(dtype=float32)`` as dim-wise reductions over rows of at most 1024 elements, repeated until one
+    remains: torch's single-output reduction of a large tensor zeroes its cross-block semaphores with a memset, and
+    on this ROCm a memset captured in a HIP graph is not re-run correctly on replay (tools/graph_memset_check.py),
+    which :class:`GraphStep` relies on.  Eager and replayed steps sum in the same order."""
+    v = x.reshape(-1)
+    first = True
+    while first or v.numel() > 1:
+        n = v.numel()
+        rows = (n + 1023) // 1024
+        if rows * 1024 != n:
+            v = torch.cat([v, v.new_zeros(rows * 1024 - n)])
+        v = v.view(rows, 1024).sum(1, dtype=torch.float32)
+        first = False
+    return v.view(())
+
+
 class _MeanF32(torch.autograd.Function):
     """``x.float().mean()`` without the fp32 copy: the mean accumulates in fp32 straight from the bf16
     masks, and the gradient is the same bf16(g / numel) the cast's backward would produce, written as one
@@ -342,7 +359,7 @@ class _MeanF32(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         ctx.shape, ctx.dtype, ctx.n = x.shape, x.dtype, x.numel()
-        return x.mean(dtype=torch.float32)
+        return graph_safe_sum(x) / x.numel()
 
     @staticmethod
     def backward(ctx, g):
@@ -351,7 +368,7 @@ class _MeanF32(torch.autograd.Function):
 
 
 def _mean_f32(x):
-    return _MeanF32.apply(x) if x.requires_grad else x.float().mean()
+    return _MeanF32.apply(x) if x.requires_grad else graph_safe_sum(x) / x.numel()
 
 
 def surrogate_loss(out):
@@ -360,13 +377,14 @@ def surrogate_loss(out):
     return sum(_mean_f32(h["pred_logits"]) + _mean_f32(h["pred_masks"]) for h in heads)
 
 
-def make_optimizer(model):
+def make_optimizer(model, capturable=False):
     """AdamW (lr 1e-4, weight decay 0.05; train_net.py:185-263).  On a GPU the fused single-kernel form: with
     it GradScaler.step hands found_inf to the kernel instead of reading it on the host (torch's non-fused path
-    syncs on found_inf.item() every fp16 step).  Same update arithmetic."""
+    syncs on found_inf.item() every fp16 step).  Same update arithmetic.  ``capturable``: the step counter on the
+    device, so the step can be captured in a graph (:class:`GraphStep`)."""
     params = list(model.parameters())
     if params and params[0].is_cuda:
-        return torch.optim.AdamW(params, lr=1e-4, weight_decay=0.05, fused=True)
+        return torch.optim.AdamW(params, lr=1e-4, weight_decay=0.05, fused=True, capturable=capturable)
     return torch.optim.AdamW(params, lr=1e-4, weight_decay=0.05, foreach=True)
 
 
@@ -399,3 +417,36 @@ def train_step(model, opt, images, amp_dtype=torch.bfloat16, clip=0.01, scaler=N
     torch.nn.utils.clip_grad_norm_(model.parameters(), clip, foreach=True)
     opt.step()
     return loss.detach()
+
+
+class GraphStep:
+    """The whole training step -- forward, loss, backward, GradScaler unscale / inf check, gradient clipping and
+    the fused AdamW (capturable: its step counter lives on the device) -- captured once as a HIP graph
+    (torch.cuda.CUDAGraph) and replayed.  The per-rank slices of configs 4 and 5 launch a few thousand small
+    kernels per step for two images, more than the host issues in the time the GPU runs them; a replay issues them
+    all at once.  Every input is static (the same feature / image tensors each step), the library's launches go to
+    torch's current stream (the capture stream), and nothing in the step reads a device value on the host (host
+    spatial shapes are tagged up front, GradScaler hands found_inf to the fused optimizer).  Warm-up steps run
+    eagerly on a side stream first (lazy state, MIOpen find-db, workspaces), as torch's whole-network capture
+    recipe prescribes."""
+
+    def __init__(self, model, opt, images, amp_dtype, scaler=None, warmup=3, debug_dump=None):
+        self.model, self.opt, self.images, self.amp, self.scaler = model, opt, images, amp_dtype, scaler
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                train_step(model, opt, images, amp_dtype, scaler=scaler)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        if debug_dump:
+            self.graph.enable_debug_mode()
+        with torch.cuda.graph(self.graph):
+            self.loss = train_step(model, opt, images, amp_dtype, scaler=scaler)
+        if debug_dump:   # the captured graph as a dot file (node types and kernel names; diagnostics)
+            self.graph.debug_dump(debug_dump)
+
+    def __call__(self):
+        self.graph.replay()
+        return self.loss

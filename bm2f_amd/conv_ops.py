@@ -70,7 +70,7 @@ class Conv2dX3(Function):
         want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if k == 3 and WGRAD3 == "tn" and ctx.needs_input_grad[1]:
             dw = _wgrad3_tn(g, x)
-            db = g.sum((0, 2, 3)) if want_b else None
+            db = g.sum((2, 3)).sum(0) if want_b else None   # two reductions with many outputs (graph-safe)
         elif k == 3 and WGRAD3 == "miopen" and (ctx.needs_input_grad[1] or want_b):
             # 3x3 weight gradient on the library (WGRAD3 = "miopen")
             _, dw, db = torch.ops.aten.convolution_backward(

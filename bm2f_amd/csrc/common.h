@@ -46,9 +46,14 @@ enum Option : int {
   kOptMsdaThreads, kOptMsdaTile, kOptMsdaTileW, kOptMsdaHalo, kOptMsdaWinRows, kOptMsdaBwdTiled, kOptMsdaFwdTiled,
   kOptMattnDqAtomic, kOptGemmNtCfg, kOptX3TnNw, kOptX3TnBlocks, kOptX3NtCfg, kOptMsdaFwdQuad, kOptMsdaBwdOverlap, kOptMsdaBwdDet, kOptMsdaFwdPb, kOptMsdaBwdRatio,
   kOptMsdaFwdLds, kOptMsdaFwdTile, kOptMsdaFwdTileW, kOptMsdaFwdCap, kOptMsdaFwdHalo,
-  kOptMattnFwdMinblk, kOptMattnBwdMinblk, kOptCount
+  kOptMattnFwdMinblk, kOptMattnBwdMinblk, kOptMaskDfStage, kOptCount
 };
 int64_t option_raw(Option o);  // -1 when unset
+
+// Zero `bytes` bytes at p on stream st with a kernel, not hipMemsetAsync: on this ROCm a memset captured in a HIP
+// graph is not re-run correctly when the graph is replayed (tools/graph_memset_check.py), and callers capture the
+// library's launches in graphs (bench_model.GraphStep).  Returns a HIP error code.
+hipError_t zero_async(void* p, size_t bytes, hipStream_t st);
 inline int option(Option o, int dflt) {
   const int64_t v = option_raw(o);
   return v < 0 ? dflt : static_cast<int>(v);

@@ -62,6 +62,37 @@ __device__ __forceinline__ f4 mma32(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// gfx950's 16x16x32 forms (twice the K of 16x16x16 per instruction): lane 16g + r holds A[row r][k = 8g + j] and
+// B[k = 8g + j][col r], j = 0..7
+using s8 = short __attribute__((ext_vector_type(8)));
+using h8 = _Float16 __attribute__((ext_vector_type(8)));
+using b8 = __bf16 __attribute__((ext_vector_type(8)));
+template <typename T>
+__device__ __forceinline__ f4 mmak32(s8 a, s8 b, f4 c) {
+  if constexpr (std::is_same<T, _Float16>::value)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(b8, a), __builtin_bit_cast(b8, b), c, 0, 0, 0);
+}
+__device__ __forceinline__ s8 cat8(s4 lo, s4 hi) { return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7); }
+
+// x with bit POS of `word` set replaced by -inf: v_bfe_i32 makes the bit a 0 / all-ones mask and v_bfi_b32 selects
+// (two VALU; a bit test is and + compare + select).  Builtins, not inline asm: the hazard recognizer must see these
+// VALU writes (an MFMA reading a VGPR that the previous instruction wrote needs wait states)
+template <int POS>
+__device__ __forceinline__ float mask_ninf(uint32_t word, float x) {
+  const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(word), POS, 1));
+  return __uint_as_float((m & 0xff800000u) | (~m & __float_as_uint(x)));
+}
+// x, or 0 where bit `pos` of `word` is set
+__device__ __forceinline__ float mask_zero(uint32_t word, uint32_t pos, float x) {
+  const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(word), pos, 1));
+  return __uint_as_float(~m & __float_as_uint(x));
+}
+// raw v_exp_f32 (2^x; -inf -> 0): the scores' exponents are <= 0, where exp2f's denormal range reduction only
+// changes results below 2^-126
+__device__ __forceinline__ float ex2(float x) { return __builtin_amdgcn_exp2f(x); }
+
 template <typename T>
 __device__ __forceinline__ s4 pack4(float a, float b, float c, float d) {
   T t[4] = {Elt<T>::from_f(a), Elt<T>::from_f(b), Elt<T>::from_f(c), Elt<T>::from_f(d)};
@@ -182,7 +213,9 @@ struct KVImage {
   static constexpr int ELEMS = 64 * RS;
 };
 
-template <typename T>
+// CLAMP: rows past the chunk repeat its last row (loads without exec branches, so the compiler's wait counting does
+// not stall the prefetch; the forward masks those keys: p = 0 on a row of the input); else they are zero
+template <typename T, bool CLAMP = false>
 __device__ __forceinline__ void stage_load(const T* __restrict__ src, int64_t row0, int nrows_valid, int stride,
                                            int col0, f4 (&reg)[2]) {
   // 64 rows x 32 elements; 16-bit: 256 x 16 B (one per thread); f32: 512 x 16 B (two per thread)
@@ -193,10 +226,14 @@ __device__ __forceinline__ void stage_load(const T* __restrict__ src, int64_t ro
   for (int it = 0; it < ITERS; ++it) {
     const int idx = threadIdx.x + it * 256;
     const int rr = idx / PARTS, part = idx % PARTS;
-    if (rr < nrows_valid)
-      reg[it] = *reinterpret_cast<const f4*>(src + (row0 + rr) * stride + col0 + part * PER);
-    else
-      reg[it] = f4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (CLAMP) {
+      reg[it] = *reinterpret_cast<const f4*>(src + (row0 + min(rr, nrows_valid - 1)) * stride + col0 + part * PER);
+    } else {
+      if (rr < nrows_valid)
+        reg[it] = *reinterpret_cast<const f4*>(src + (row0 + rr) * stride + col0 + part * PER);
+      else
+        reg[it] = f4{0.f, 0.f, 0.f, 0.f};
+    }
   }
 }
 
@@ -224,8 +261,23 @@ __device__ __forceinline__ void stage_store(T* img, const f4 (&reg)[2]) {
   }
 }
 
+// the four masks of one 16-key tile's C fragment (keys 4g + i of the tile, bits B0 + i of the lane's pre-shifted word)
+template <int B0>
+__device__ __forceinline__ void mask4(f4& s, uint32_t word) {
+  s[0] = mask_ninf<B0>(word, s[0]);
+  s[1] = mask_ninf<B0 + 1>(word, s[1]);
+  s[2] = mask_ninf<B0 + 2>(word, s[2]);
+  s[3] = mask_ninf<B0 + 3>(word, s[3]);
+}
+
+// Per score element: two VALU for the mask (blocked keys and keys past the chunk are both bits of the lane's mask
+// words, folded in when the words are loaded), a max3 share, one fma and v_exp for p = 2^(s sl2 - m), half a pack;
+// the row sums come from the MFMA (16-bit: an all-ones A operand against P^T).  16-bit operands run on the 16x16x32
+// form: S^T tile = one MFMA per 16 keys (K = head dim 32), O^T += V^T P^T one per 32 keys, the key order inside the
+// K = 32 step permuted so that P's C fragments of two key tiles are the B operand as they are (element j < 4: key
+// 4g + j of the first tile, j >= 4: of the second) and V^T's A operand is two transposed reads of those tiles.
 template <typename T, int TPW>
-__global__ void __launch_bounds__(256) mattn_fwd_kernel(
+__global__ void __launch_bounds__(256, TPW <= 2 ? 4 : TPW <= 4 ? 2 : 1) mattn_fwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
     int Lq, int Lk, int H, int qs, int kvs, int nw, float sl2, int chunk_len, T* __restrict__ out,
     float* __restrict__ lse2, float* __restrict__ ws_o, float* __restrict__ ws_ml) {
@@ -240,12 +292,16 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
   const int64_t kvrow0 = static_cast<int64_t>(b) * Lk;
 
-  // query operands (B of S^T = K Q^T): lane holds Q[q = tile*16 + r][d = dc + kw*g + j]
-  s4 qb16[TPW][2];
+  // query operands (B of S^T = K Q^T): 16-bit: lane holds Q[q = tile*16 + r][d = 8g + j]; f32: [d = dc*4 + g]
+  s8 qb16[TPW];
   float qb32[TPW][8];
   f4 o[TPW][2];
+  f4 lsum[TPW];  // 16-bit: P's row sums (every element: query r's)
   float m_run[TPW], l_run[TPW];
   uint32_t mrow_ok[TPW];
+  // 1.0 in the operand format (f16 0x3C00, bf16 0x3F80)
+  constexpr short kOne = std::is_same<T, _Float16>::value ? short(0x3C00) : short(0x3F80);
+  const s8 ones = {kOne, kOne, kOne, kOne, kOne, kOne, kOne, kOne};
 #pragma unroll
   for (int t = 0; t < TPW; ++t) {
     const int qi = (w + 4 * t) * 16 + r;
@@ -253,17 +309,16 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
     mrow_ok[t] = ok;
     const T* qrow = q + (static_cast<int64_t>(b) * Lq + (ok ? qi : 0)) * qs + h * kD;
     if constexpr (k16) {
-#pragma unroll
-      for (int dc = 0; dc < 2; ++dc) {
-        const s4 val = *reinterpret_cast<const s4*>(qrow + dc * 16 + 4 * g);
-        qb16[t][dc] = ok ? val : s4{0, 0, 0, 0};
-      }
+      const s4 lo = *reinterpret_cast<const s4*>(qrow + 8 * g);
+      const s4 hi = *reinterpret_cast<const s4*>(qrow + 8 * g + 4);
+      qb16[t] = ok ? cat8(lo, hi) : s8{0, 0, 0, 0, 0, 0, 0, 0};
     } else {
 #pragma unroll
       for (int dc = 0; dc < 8; ++dc) qb32[t][dc] = ok ? Elt<T>::to_f(qrow[dc * 4 + g]) : 0.f;
     }
     o[t][0] = f4{0.f, 0.f, 0.f, 0.f};
     o[t][1] = f4{0.f, 0.f, 0.f, 0.f};
+    lsum[t] = f4{0.f, 0.f, 0.f, 0.f};
     m_run[t] = -INFINITY;
     l_run[t] = 0.f;
   }
@@ -271,24 +326,22 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
   f4 kreg[2], vreg[2];
   // this lane's mask words of a 64-key block (query row qi of tile t), loaded one block ahead with K / V
   uint32_t mw[TPW][2];
+  // (unconditional loads at clamped addresses: a query row past Lq and a word past the row are overridden when the
+  // words are used)
   auto mload = [&](int kb) {
+    const int w1 = min((kb >> 5) + 1, nw - 1);
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
-      uint32_t a0 = 0xffffffffu, a1 = 0xffffffffu;
-      if (mrow_ok[t]) {
-        const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + (w + 4 * t) * 16 + r) * nw + (kb >> 5);
-        a0 = mr[0];
-        a1 = ((kb >> 5) + 1 < nw) ? mr[1] : 0xffffffffu;
-      }
-      mw[t][0] = a0;
-      mw[t][1] = a1;
+      const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + min((w + 4 * t) * 16 + r, Lq - 1)) * nw;
+      mw[t][0] = mr[kb >> 5];
+      mw[t][1] = mr[w1];
     }
   };
   uint32_t mcur[TPW][2];
   int buf = 0;
   if (key_begin < key_end) {
-    stage_load<T>(k, kvrow0 + key_begin, key_end - key_begin, kvs, h * kD, kreg);
-    stage_load<T>(v, kvrow0 + key_begin, key_end - key_begin, kvs, h * kD, vreg);
+    stage_load<T, true>(k, kvrow0 + key_begin, key_end - key_begin, kvs, h * kD, kreg);
+    stage_load<T, true>(v, kvrow0 + key_begin, key_end - key_begin, kvs, h * kD, vreg);
     mload(key_begin);
     stage_store<T>(Ks[0], kreg);
     stage_store<T>(Vs[0], vreg);
@@ -297,80 +350,88 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
 
   for (int kb0 = key_begin; kb0 < key_end; kb0 += 64) {
     const int next = kb0 + 64;
+    {
+      // keys past the chunk set as blocked, then the words shifted by 4g: key 16 kt + 4g + i of the block is bit
+      // 16 (kt & 1) + i of word kt >> 1 (done here, not at the load, so nothing waits on the prefetch below)
+      const int kv = key_end - kb0;  // >= 1
+      const uint32_t x0 = kv >= 32 ? 0u : (0xffffffffu << (kv & 31));
+      const uint32_t x1 = kv >= 64 ? 0u : (kv <= 32 ? 0xffffffffu : (0xffffffffu << ((kv - 32) & 31)));
+      const uint32_t xw = (kb0 >> 5) + 1 < nw ? 0u : 0xffffffffu;  // no second word: keys past Lk
 #pragma unroll
-    for (int t = 0; t < TPW; ++t) { mcur[t][0] = mw[t][0]; mcur[t][1] = mw[t][1]; }
+      for (int t = 0; t < TPW; ++t) {
+        const uint32_t xr = mrow_ok[t] ? 0u : 0xffffffffu;
+        mcur[t][0] = (mw[t][0] | x0 | xr) >> (4 * g);
+        mcur[t][1] = (mw[t][1] | x1 | xw | xr) >> (4 * g);
+      }
+    }
     if (next < key_end) {  // prefetch the next block into registers
-      stage_load<T>(k, kvrow0 + next, key_end - next, kvs, h * kD, kreg);
-      stage_load<T>(v, kvrow0 + next, key_end - next, kvs, h * kD, vreg);
+      stage_load<T, true>(k, kvrow0 + next, key_end - next, kvs, h * kD, kreg);
+      stage_load<T, true>(v, kvrow0 + next, key_end - next, kvs, h * kD, vreg);
       mload(next);
     }
     const T* Kc = Ks[buf];
     const T* Vc = Vs[buf];
-    const int kvalid = key_end - kb0;  // keys of this block that exist
 #pragma unroll
     for (int t = 0; t < TPW; ++t) {
       if ((w + 4 * t) * 16 >= Lq) continue;  // wave-uniform
-      const uint32_t w0 = mcur[t][0], w1 = mcur[t][1];
       f4 st[4];
 #pragma unroll
       for (int kt = 0; kt < 4; ++kt) {
         f4 acc = {0.f, 0.f, 0.f, 0.f};
         if constexpr (k16) {
-#pragma unroll
-          for (int dc = 0; dc < 2; ++dc) {
-            const s4 a = *reinterpret_cast<const s4*>(Kc + (16 * kt + r) * RS + dc * 16 + 4 * g);
-            acc = mma16<T>(a, qb16[t][dc], acc);
-          }
+          const T* kr = Kc + (16 * kt + r) * RS + 8 * g;
+          acc = mmak32<T>(cat8(*reinterpret_cast<const s4*>(kr), *reinterpret_cast<const s4*>(kr + 4)), qb16[t], acc);
         } else {
 #pragma unroll
           for (int dc = 0; dc < 8; ++dc) acc = mma32(Elt<T>::to_f(Kc[(16 * kt + r) * RS + dc * 4 + g]), qb32[t][dc], acc);
         }
         st[kt] = acc;
       }
-      // mask + scale, block max
+      // blocked -> -inf on the raw scores; the block max of the raw scores (sl2 > 0, checked on the host)
+      mask4<0>(st[0], mcur[t][0]);
+      mask4<16>(st[1], mcur[t][0]);
+      mask4<0>(st[2], mcur[t][1]);
+      mask4<16>(st[3], mcur[t][1]);
       float mx = -INFINITY;
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int off = 16 * kt + 4 * g + i;
-          const uint32_t word = off < 32 ? w0 : w1;
-          const bool blocked = ((word >> (off & 31)) & 1u) || off >= kvalid;
-          const float s = blocked ? -INFINITY : st[kt][i] * sl2;
-          st[kt][i] = s;
-          mx = fmaxf(mx, s);
-        }
-      }
+        for (int i = 0; i < 4; ++i) mx = fmaxf(mx, st[kt][i]);
       mx = wave_max16(mx);
-      const float m_new = fmaxf(m_run[t], mx);
+      const float m_new = fmaxf(m_run[t], mx * sl2);
       const float m_use = m_new == -INFINITY ? 0.f : m_new;
-      const float alpha = exp2f(m_run[t] - m_use);
-      float rs = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float p = exp2f(st[kt][i] - m_use);
-          st[kt][i] = p;
-          rs += p;
-        }
-      }
-      rs = wave_sum16(rs);
-      l_run[t] = l_run[t] * alpha + rs;
+      const float alpha = ex2(m_run[t] - m_use);
       m_run[t] = m_new;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st[kt][i] = ex2(fmaf(st[kt][i], sl2, -m_use));
       o[t][0] *= alpha;
       o[t][1] *= alpha;
       // O^T[d][q] += V^T[d][key] P^T[key][q]
+      if constexpr (k16) {
+        lsum[t] *= alpha;
 #pragma unroll
-      for (int kt = 0; kt < 4; ++kt) {
-        if constexpr (k16) {
-          const s4 pb = pack4<T>(st[kt][0], st[kt][1], st[kt][2], st[kt][3]);
+        for (int pp = 0; pp < 2; ++pp) {
+          const s8 pb = cat8(pack4<T>(st[2 * pp][0], st[2 * pp][1], st[2 * pp][2], st[2 * pp][3]),
+                             pack4<T>(st[2 * pp + 1][0], st[2 * pp + 1][1], st[2 * pp + 1][2], st[2 * pp + 1][3]));
+          lsum[t] = mmak32<T>(ones, pb, lsum[t]);
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt) {
-            const s4 va = tr_read(Vc + (16 * kt + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3));
-            o[t][dt] = mma16<T>(va, pb, o[t][dt]);
+            const T* vr = Vc + (32 * pp + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
+            o[t][dt] = mmak32<T>(cat8(tr_read(vr), tr_read(vr + 16 * RS)), pb, o[t][dt]);
           }
-        } else {
+        }
+      } else {
+        float rs = 0.f;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) rs += st[kt][i];
+        rs = wave_sum16(rs);
+        l_run[t] = l_run[t] * alpha + rs;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
 #pragma unroll
@@ -395,8 +456,9 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
   for (int t = 0; t < TPW; ++t) {
     if (!mrow_ok[t]) continue;
     const int qi = (w + 4 * t) * 16 + r;
+    const float lt = k16 ? lsum[t][0] : l_run[t];
     if (nchunks == 1) {
-      const float inv = l_run[t] > 0.f ? 1.f / l_run[t] : 0.f;
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
       T* orow = out + (static_cast<int64_t>(b) * Lq + qi) * (H * kD) + h * kD;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) {
@@ -407,14 +469,14 @@ __global__ void __launch_bounds__(256) mattn_fwd_kernel(
           *reinterpret_cast<f4*>(orow + dt * 16 + 4 * g) = val;
         }
       }
-      if (g == 0) lse2[static_cast<int64_t>(bh) * Lq + qi] = l_run[t] > 0.f ? m_run[t] + log2f(l_run[t]) : INFINITY;
+      if (g == 0) lse2[static_cast<int64_t>(bh) * Lq + qi] = lt > 0.f ? m_run[t] + log2f(lt) : INFINITY;
     } else {
       const int64_t prow = (static_cast<int64_t>(c) * BH + bh) * Lq + qi;
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt) *reinterpret_cast<f4*>(ws_o + prow * kD + dt * 16 + 4 * g) = o[t][dt];
       if (g == 0) {
         ws_ml[2 * prow] = m_run[t];
-        ws_ml[2 * prow + 1] = l_run[t];
+        ws_ml[2 * prow + 1] = lt;
       }
     }
   }
@@ -476,8 +538,8 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
   constexpr bool k16 = Elt<T>::k16;
   constexpr int RS = KVImage<T>::RS;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // carve: Qs, dOs [Lqp][RS] T | Ks, Vs [64][RS] T | lse, delta [Lqp] f32 | mw [Lqp][2] u32 |
-  //        scr [4][16][17] f32 | dQacc [Lqp][kD] f32
+  // carve: Qs, dOs [Lqp][RS] T | Ks, Vs [64][RS] T | lse, delta [Lqp] f32 | mw [2][Lqp] u32 (word 0 / 1 of the block,
+  //        keys past the chunk set) | scr [4][16][17] f32 | dQacc [Lqp][kD] f32
   T* Qs = reinterpret_cast<T*>(smem);
   T* dOs = Qs + Lqp * RS;
   T* Ks = dOs + Lqp * RS;
@@ -570,20 +632,18 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
   constexpr int kMaxMwPerThread = 2;   // Lqp <= 512
   f4 kreg[2], vreg[2];
   uint32_t mreg[kMaxMwPerThread][2];
+  // (no exec branches around the loads, so the compiler's wait counting leaves them in flight: rows past the chunk
+  // repeat its last row, those keys being masked; mask words load at clamped addresses and a query past Lq or a word
+  // past the row is overridden where the words are staged)
   auto prefetch = [&](int kb) {
-    stage_load<T>(k, kvrow0 + kb, key_end - kb, kvs, h * kD, kreg);
-    stage_load<T>(v, kvrow0 + kb, key_end - kb, kvs, h * kD, vreg);
+    stage_load<T, true>(k, kvrow0 + kb, key_end - kb, kvs, h * kD, kreg);
+    stage_load<T, true>(v, kvrow0 + kb, key_end - kb, kvs, h * kD, vreg);
+    const int w1 = min((kb >> 5) + 1, nw - 1);
 #pragma unroll
     for (int u = 0; u < kMaxMwPerThread; ++u) {
-      const int qi = threadIdx.x + 256 * u;
-      uint32_t a0 = 0xffffffffu, a1 = 0xffffffffu;
-      if (qi < Lq) {
-        const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + qi) * nw + (kb >> 5);
-        a0 = mr[0];
-        a1 = ((kb >> 5) + 1 < nw) ? mr[1] : 0xffffffffu;
-      }
-      mreg[u][0] = a0;
-      mreg[u][1] = a1;
+      const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + min(static_cast<int>(threadIdx.x) + 256 * u, Lq - 1)) * nw;
+      mreg[u][0] = mr[kb >> 5];
+      mreg[u][1] = mr[w1];
     }
   };
   if (key_begin < key_end) prefetch(key_begin);
@@ -591,29 +651,34 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
     __syncthreads();  // previous block's images fully consumed (and the prologue staged)
     stage_store<T>(Ks, kreg);
     stage_store<T>(Vs, vreg);
+    const int kvalid = key_end - kb0;
+    {
+      const uint32_t x0 = kvalid >= 32 ? 0u : (0xffffffffu << (kvalid & 31));
+      const uint32_t x1 = kvalid >= 64 ? 0u : (kvalid <= 32 ? 0xffffffffu : (0xffffffffu << ((kvalid - 32) & 31)));
+      const uint32_t xw = (kb0 >> 5) + 1 < nw ? 0u : 0xffffffffu;  // no second word: keys past Lk
 #pragma unroll
-    for (int u = 0; u < kMaxMwPerThread; ++u) {
-      const int qi = threadIdx.x + 256 * u;
-      if (qi < Lqp) {
-        mw[2 * qi] = mreg[u][0];
-        mw[2 * qi + 1] = mreg[u][1];
+      for (int u = 0; u < kMaxMwPerThread; ++u) {
+        const int qi = threadIdx.x + 256 * u;
+        if (qi < Lqp) {
+          const uint32_t xr = qi < Lq ? 0u : 0xffffffffu;
+          mw[qi] = mreg[u][0] | x0 | xr;
+          mw[Lqp + qi] = mreg[u][1] | x1 | xw | xr;
+        }
       }
     }
     __syncthreads();
     if (kb0 + 64 < key_end) prefetch(kb0 + 64);   // in flight during this block's MFMAs
-    const int kvalid = key_end - kb0;
     const int koff = 16 * w + r;  // this lane's key (column) within the block
     if (16 * w >= kvalid) continue;  // whole tile beyond the chunk (wave-uniform); barriers are at loop top
 
-    // per-key-tile operands: K, V as B[k = d][col = key]
-    s4 kb16[2], vb16[2];
+    // per-key-tile operands: K, V as B[k = d][col = key] (16-bit: d = 8g + j, one 16x16x32 over the head dim)
+    s8 kb16, vb16;
     float kb32[8], vb32[8];
     if constexpr (k16) {
-#pragma unroll
-      for (int dc = 0; dc < 2; ++dc) {
-        kb16[dc] = *reinterpret_cast<const s4*>(Ks + koff * RS + dc * 16 + 4 * g);
-        vb16[dc] = *reinterpret_cast<const s4*>(Vs + koff * RS + dc * 16 + 4 * g);
-      }
+      const T* kr = Ks + koff * RS + 8 * g;
+      const T* vr = Vs + koff * RS + 8 * g;
+      kb16 = cat8(*reinterpret_cast<const s4*>(kr), *reinterpret_cast<const s4*>(kr + 4));
+      vb16 = cat8(*reinterpret_cast<const s4*>(vr), *reinterpret_cast<const s4*>(vr + 4));
     } else {
 #pragma unroll
       for (int dc = 0; dc < 8; ++dc) {
@@ -623,20 +688,40 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
     }
     f4 dkacc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
     f4 dvacc[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-    const int word_sel = koff >> 5, bit = koff & 31;
+    const uint32_t* mwsel = mw + (koff >> 5) * Lqp;  // wave-uniform word of the block
+    const uint32_t bit = koff & 31;
     const bool key_ok = koff < kvalid;
 
-    // one 16-query tile against this wave's 16 keys; dQ^T contributions accumulate into dqt
-    auto tile = [&](const int qt, f4* dqt) {
+    // dV^T += dO^T P ; dK^T += Q^T dS (A[row d][k = q]).  16-bit: two query tiles per 16x16x32 (K = 32 queries,
+    // element j < 4 of a lane's fragments from the first tile's query 4g + j, j >= 4 from the second's), one tile on
+    // 16x16x16 for an odd tail
+    auto dvdk2 = [&](int qa, s4 pa, s4 sa, int qb, s4 pb, s4 sb) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int ra = (qa * 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
+        const int rb = (qb * 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
+        dvacc[dt] = mmak32<T>(cat8(tr_read(dOs + ra), tr_read(dOs + rb)), cat8(pa, pb), dvacc[dt]);
+        dkacc[dt] = mmak32<T>(cat8(tr_read(Qs + ra), tr_read(Qs + rb)), cat8(sa, sb), dkacc[dt]);
+      }
+    };
+    auto dvdk1 = [&](int qa, s4 pa, s4 sa) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int ro = (qa * 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
+        dvacc[dt] = mma16<T>(tr_read(dOs + ro), pa, dvacc[dt]);
+        dkacc[dt] = mma16<T>(tr_read(Qs + ro), sa, dkacc[dt]);
+      }
+    };
+
+    // one 16-query tile against this wave's 16 keys; dQ^T contributions accumulate into dqt; 16-bit: P and dS
+    // packed into pb / sb for dvdk (f32: dV / dK accumulated here)
+    auto tile = [&](const int qt, f4* dqt, s4& pbo, s4& sbo) {
       f4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
       if constexpr (k16) {
-#pragma unroll
-        for (int dc = 0; dc < 2; ++dc) {
-          const s4 qa = *reinterpret_cast<const s4*>(Qs + (qt * 16 + r) * RS + dc * 16 + 4 * g);
-          const s4 ga = *reinterpret_cast<const s4*>(dOs + (qt * 16 + r) * RS + dc * 16 + 4 * g);
-          s = mma16<T>(qa, kb16[dc], s);
-          dp = mma16<T>(ga, vb16[dc], dp);
-        }
+        const T* qr = Qs + (qt * 16 + r) * RS + 8 * g;
+        const T* gr = dOs + (qt * 16 + r) * RS + 8 * g;
+        s = mmak32<T>(cat8(*reinterpret_cast<const s4*>(qr), *reinterpret_cast<const s4*>(qr + 4)), kb16, s);
+        dp = mmak32<T>(cat8(*reinterpret_cast<const s4*>(gr), *reinterpret_cast<const s4*>(gr + 4)), vb16, dp);
       } else {
 #pragma unroll
         for (int dc = 0; dc < 8; ++dc) {
@@ -644,26 +729,22 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
           dp = mma32(Elt<T>::to_f(dOs[(qt * 16 + r) * RS + dc * 4 + g]), vb32[dc], dp);
         }
       }
-      // C layout: [q = qt*16 + 4g + i][key = koff]
+      // C layout: [q = qt*16 + 4g + i][key = koff]; the four queries' mask words, LSE and delta in one 16-B read each
+      const int q0 = qt * 16 + 4 * g;
+      const uint4 mq = *reinterpret_cast<const uint4*>(mwsel + q0);
+      const f4 lq = *reinterpret_cast<const f4*>(lse_s + q0);
+      const f4 dq4 = *reinterpret_cast<const f4*>(del_s + q0);
+      const uint32_t mqa[4] = {mq.x, mq.y, mq.z, mq.w};
       f4 p, ds;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int qi = qt * 16 + 4 * g + i;
-        const bool blocked = !key_ok || ((mw[2 * qi + word_sel] >> bit) & 1u);
-        const float pv = blocked ? 0.f : exp2f(s[i] * sl2 - lse_s[qi]);
+        const float pv = mask_zero(mqa[i], bit, ex2(fmaf(s[i], sl2, -lq[i])));
         p[i] = pv;
-        ds[i] = pv * (dp[i] - del_s[qi]);
+        ds[i] = pv * (dp[i] - dq4[i]);
       }
-      // dV^T += dO^T P ; dK^T += Q^T dS      (A[row d][k = q])
       if constexpr (k16) {
-        const s4 pb = pack4<T>(p[0], p[1], p[2], p[3]);
-        const s4 sb = pack4<T>(ds[0], ds[1], ds[2], ds[3]);
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) {
-          const int ro = (qt * 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
-          dvacc[dt] = mma16<T>(tr_read(dOs + ro), pb, dvacc[dt]);
-          dkacc[dt] = mma16<T>(tr_read(Qs + ro), sb, dkacc[dt]);
-        }
+        pbo = pack4<T>(p[0], p[1], p[2], p[3]);
+        sbo = pack4<T>(ds[0], ds[1], ds[2], ds[3]);
       } else {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -699,15 +780,28 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
         }
       }
     };
+    s4 ppend = {0, 0, 0, 0}, spend = {0, 0, 0, 0};  // 16-bit: an even tile's P / dS waiting for its pair
+    auto tile_done = [&](int qt, s4 pb, s4 sb) {
+      if constexpr (k16) {
+        if (qt & 1) dvdk2(qt - 1, ppend, spend, qt, pb, sb);
+        else { ppend = pb; spend = sb; }
+      }
+    };
     if constexpr (NTR > 0) {
       // dQ stays in registers across every key block of the chunk (Lqp <= 16 * NTR)
 #pragma unroll
       for (int qt = 0; qt < NTR; ++qt)
-        if (qt < NT) tile(qt, dqacc[qt]);
+        if (qt < NT) {
+          s4 pb, sb;
+          tile(qt, dqacc[qt], pb, sb);
+          tile_done(qt, pb, sb);
+        }
     } else {
       for (int qt = 0; qt < NT; ++qt) {
         f4 dqt[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}};
-        tile(qt, dqt);
+        s4 pb, sb;
+        tile(qt, dqt, pb, sb);
+        tile_done(qt, pb, sb);
         // lane holds dQ^T[d = dt*16 + 4g + i][q = qt*16 + r]
         if constexpr (NTR < 0) {
 #pragma unroll
@@ -722,6 +816,9 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
             for (int i = 0; i < 4; ++i) atomicAdd(&dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i], dqt[dt][i]);
         }
       }
+    }
+    if constexpr (k16) {
+      if (NT & 1) dvdk1(NT - 1, ppend, spend);
     }
     // write dK, dV for this key tile: lane holds [d = dt*16 + 4g + i][key = koff]
     if (key_ok) {
@@ -839,6 +936,8 @@ int mattn_fwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   if (B <= 0 || Lq <= 0 || Lk <= 0 || H <= 0) return m2f::fail(M2F_EINVAL, "%s: non-positive size", fn);
   if (Lq > 512) return m2f::fail(M2F_EUNSUPPORTED, "%s: %d queries (max 512)", fn, Lq);
   if (nw < (Lk + 31) / 32) return m2f::fail(M2F_EINVAL, "%s: mask words %d < %d", fn, nw, (Lk + 31) / 32);
+  // the kernel takes the block max on the unscaled scores
+  if (!(scale > 0.f) || !std::isfinite(scale)) return m2f::fail(M2F_EINVAL, "%s: scale %g (need finite > 0)", fn, scale);
   const int vec = Elt<T>::k16 ? 8 : 4;
   if (qs % 4 || kvs % vec || !m2f::aligned(q, 8) || !m2f::aligned(k, 16) || !m2f::aligned(v, 16) ||
       !m2f::aligned(out, 16))

@@ -474,3 +474,32 @@ extern "C" int m2f_gather_probe(const float* table, int rows, int64_t n, float* 
                                                                           static_cast<uint32_t>(rows), n, out);
   return m2f::check_launch(fn);
 }
+
+// ------------------------------------------------------------------------------------------------
+// m2f::zero_async: a grid-stride fill with 16-byte stores (byte stores for an unaligned head / tail)
+// ------------------------------------------------------------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) zero16_kernel(uint4* __restrict__ p, size_t n16) {
+  const uint4 z = {0u, 0u, 0u, 0u};
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += static_cast<size_t>(gridDim.x) * 256) p[i] = z;
+}
+__global__ void __launch_bounds__(256) zero1_kernel(unsigned char* __restrict__ p, size_t n) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += static_cast<size_t>(gridDim.x) * 256) p[i] = 0;
+}
+}  // namespace
+
+namespace m2f {
+hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
+  if (bytes == 0) return hipSuccess;
+  unsigned char* b = static_cast<unsigned char*>(p);
+  const size_t head = std::min(bytes, (16 - (reinterpret_cast<uintptr_t>(b) & 15)) & 15);
+  const size_t n16 = (bytes - head) / 16, tail = bytes - head - n16 * 16;
+  if (head) zero1_kernel<<<1, 256, 0, st>>>(b, head);
+  if (n16) {
+    const size_t blocks = std::min<size_t>((n16 + 255) / 256, 4096);
+    zero16_kernel<<<static_cast<unsigned>(blocks), 256, 0, st>>>(reinterpret_cast<uint4*>(b + head), n16);
+  }
+  if (tail) zero1_kernel<<<1, 256, 0, st>>>(b + head + n16 * 16, tail);
+  return hipGetLastError();
+}
+}  // namespace m2f

@@ -408,31 +408,42 @@ struct DfHeads {
   const void* g[kDfMaxHeads];
 };
 
-template <typename T, typename O>   // O: the features' dtype (T, or fp32 when autocast made T a copy)
+// KS: k-steps (16 queries each) per LDS stage.  KS = 4 (the default) stages 64 G rows per barrier: 32 MFMAs per
+// wave between barriers instead of 8, the A fragments of a whole stage prefetched one stage ahead.
+template <typename T, typename O, int KS = 4>   // O: the features' dtype (T, or fp32 when autocast made T a copy)
 __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T* __restrict__ Et, int H, int Q,
                                                          int QP, int64_t N, int ncol, O* __restrict__ df) {
   using E = MhElt<T>;
-  constexpr int C = 256;
+  constexpr int C = 256, KR = 16 * KS;                        // G rows per stage
   constexpr int EPP = 16 / static_cast<int>(sizeof(O));       // output elements per 16-byte piece
-  __shared__ __attribute__((aligned(16))) T sg[2][16 * kDfPitch];
+  constexpr int GP = KR * kDfCols / 8 / 256;                  // 16-byte G pieces per thread per stage
+  __shared__ __attribute__((aligned(16))) T sg[2][KR * kDfPitch];
   __shared__ __attribute__((aligned(16))) O so[4][32][32 + EPP];
   const int cc = blockIdx.x % ncol, b = blockIdx.x / ncol;
   const int64_t n0 = static_cast<int64_t>(cc) * kDfCols;
   const int cw = static_cast<int>(min<int64_t>(kDfCols, N - n0));
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, li = lane & 31, lh = lane >> 5;
-  const int KP = H * QP, nsteps = KP / 16, spq = QP / 16;
-  // staging: thread -> (k row tid >> 4, 8 columns (tid & 15) * 8) of the step's 16 x 128 G slab
-  const int sr = tid >> 4, scol = (tid & 15) * 8;
+  const int KP = H * QP, nsteps = KP / 16, nstages = (nsteps + KS - 1) / KS;
+  // staging: piece i of a thread -> (stage row (tid >> 4) + 16 i, 8 columns (tid & 15) * 8) of the stage's KR x 128
+  // G slab; row k of the K axis is query k % QP of head k / QP (zero past KP and past Q)
+  const int scol = (tid & 15) * 8;
   const bool cok = scol < cw;
-  auto gload = [&](int st) -> s8 {
-    s8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int h = st / spq, q = (st - h * spq) * 16 + sr;
-    if (cok && q < Q && st < nsteps)
-      v = *reinterpret_cast<const s8*>(static_cast<const T*>(heads.g[h]) + (static_cast<int64_t>(b) * Q + q) * N +
-                                       n0 + scol);
-    return v;
+  const float iqp = 1.f / static_cast<float>(QP);
+  auto gload = [&](int stg, s8 (&v)[GP]) {
+#pragma unroll
+    for (int i = 0; i < GP; ++i) {
+      v[i] = s8{0, 0, 0, 0, 0, 0, 0, 0};
+      const int k = stg * KR + (tid >> 4) + 16 * i;
+      const int h = static_cast<int>((static_cast<float>(k) + 0.5f) * iqp), q = k - h * QP;   // k < 2^16: exact
+      if (cok && k < KP && q < Q)
+        v[i] = *reinterpret_cast<const s8*>(static_cast<const T*>(heads.g[h]) + (static_cast<int64_t>(b) * Q + q) * N +
+                                            n0 + scol);
+    }
   };
-  auto gstore = [&](int buf, s8 v) { *reinterpret_cast<s8*>(&sg[buf][sr * kDfPitch + scol]) = v; };
+  auto gstore = [&](int buf, const s8 (&v)[GP]) {
+#pragma unroll
+    for (int i = 0; i < GP; ++i) *reinterpret_cast<s8*>(&sg[buf][((tid >> 4) + 16 * i) * kDfPitch + scol]) = v[i];
+  };
   const T* et = Et + (static_cast<int64_t>(b) * C + 64 * w + li) * KP + lh * 8;
   f16v acc[2][4];
 #pragma unroll
@@ -442,37 +453,45 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[j][t][e] = 0.f;
   const int gq = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-  // A fragments of step st (clamped to the last step past the end: loaded, never used)
-  auto aload = [&](int st, s8 (&af)[2]) {
-    const int sc = min(st, nsteps - 1);
+  // A fragments of a stage's KS k-steps (a step past the end clamped to the last: loaded, multiplied by zero rows)
+  auto aload = [&](int stg, s8 (&af)[KS][2]) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) af[j] = *reinterpret_cast<const s8*>(et + static_cast<int64_t>(32 * j) * KP + sc * 16);
+    for (int s = 0; s < KS; ++s) {
+      const int sc = min(stg * KS + s, nsteps - 1);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) af[s][j] = *reinterpret_cast<const s8*>(et + static_cast<int64_t>(32 * j) * KP + sc * 16);
+    }
   };
-  s8 r0 = gload(0), r1 = gload(1);
-  s8 a_cur[2], a_n1[2], a_n2[2];
+  s8 gr[GP], a_cur[KS][2], a_nxt[KS][2];
+  gload(0, gr);
   aload(0, a_cur);
-  aload(1, a_n1);
-  gstore(0, r0);
+  gstore(0, gr);
   __syncthreads();
-  for (int st = 0; st < nsteps; ++st) {
-    const int buf = st & 1;
-    const s8 r2 = gload(st + 2);  // steps st + 1 (r1) and st + 2 (r2) in flight
-    aload(st + 2, a_n2);          // A fragments two steps ahead
-    s8 af[2] = {a_cur[0], a_cur[1]};
-    a_cur[0] = a_n1[0]; a_cur[1] = a_n1[1];
-    a_n1[0] = a_n2[0]; a_n1[1] = a_n2[1];
+  for (int stg = 0; stg < nstages; ++stg) {
+    const int buf = stg & 1;
+    const bool more = stg + 1 < nstages;
+    if (more) {  // the next stage's G rows and A fragments in flight during this stage's MFMAs
+      gload(stg + 1, gr);
+      aload(stg + 1, a_nxt);
+    }
     const T* base = &sg[buf][0];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int col = 32 * t + 16 * (gq & 1) + 4 * pp;
-      const s4 lo = tr_read(base + (8 * lh + qq) * kDfPitch + col);
-      const s4 hi = tr_read(base + (8 * lh + 4 + qq) * kDfPitch + col);
-      const s8 bf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    for (int s = 0; s < KS; ++s) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[j][t] = E::mma(af[j], bf, acc[j][t]);
+      for (int t = 0; t < 4; ++t) {
+        const int col = 32 * t + 16 * (gq & 1) + 4 * pp;
+        const s4 lo = tr_read(base + (16 * s + 8 * lh + qq) * kDfPitch + col);
+        const s4 hi = tr_read(base + (16 * s + 8 * lh + 4 + qq) * kDfPitch + col);
+        const s8 bf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[j][t] = E::mma(a_cur[s][j], bf, acc[j][t]);
+      }
     }
-    gstore(buf ^ 1, r1);
-    r1 = r2;
+    if (more) {
+      gstore(buf ^ 1, gr);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) { a_cur[s][0] = a_nxt[s][0]; a_cur[s][1] = a_nxt[s][1]; }
+    }
     __syncthreads();
   }
   // epilogue: per 32x32 tile through the wave's LDS image, 16-byte stores (one rounding to O)
@@ -647,9 +666,12 @@ extern "C" int m2f_mask_heads_bwd_feats(int dtype, const void* const* grad_masks
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (out_dtype != dtype && out_dtype != M2F_F32) return m2f::fail(M2F_EUNSUPPORTED, "%s: out dtype %d", fn, out_dtype);
   const unsigned g = static_cast<unsigned>(nblk);
-#define M2F_DF(T, O) \
-  mask_df_kernel<T, O><<<g, 256, 0, st>>>(h, static_cast<const T*>(embed_t), heads, num_queries, padded_queries, n, ncol, \
-                                          static_cast<O*>(grad_feats))
+  const bool ks4 = m2f::option(m2f::kOptMaskDfStage, 4) >= 4;  // k-steps per LDS stage: 4 (default) or 1
+#define M2F_DF(T, O)                                                                                                    \
+  (ks4 ? mask_df_kernel<T, O, 4><<<g, 256, 0, st>>>(h, static_cast<const T*>(embed_t), heads, num_queries,             \
+                                                    padded_queries, n, ncol, static_cast<O*>(grad_feats))              \
+       : mask_df_kernel<T, O, 1><<<g, 256, 0, st>>>(h, static_cast<const T*>(embed_t), heads, num_queries,             \
+                                                    padded_queries, n, ncol, static_cast<O*>(grad_feats)))
   if (dtype == M2F_BF16) {
     if (out_dtype == M2F_F32) M2F_DF(__bf16, float); else M2F_DF(__bf16, __bf16);
   } else {

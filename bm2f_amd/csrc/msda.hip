@@ -42,7 +42,7 @@ constexpr const char* kOptionNames[m2f::kOptCount] = {
     "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
     "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap",
     "msda_bwd_det", "msda_fwd_pb", "msda_bwd_ratio", "msda_fwd_lds", "msda_fwd_tile", "msda_fwd_tile_w",
-    "msda_fwd_cap", "msda_fwd_halo", "mattn_fwd_minblk", "mattn_bwd_minblk"};
+    "msda_fwd_cap", "msda_fwd_halo", "mattn_fwd_minblk", "mattn_bwd_minblk", "mask_df_stage"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -321,9 +321,10 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // grad_value is a scatter: every (query, sample, corner) adds w_c * a * g[query] (32 channels) to one
 // pixel row.  Here it becomes a gather inside the workgroup:
 //   phase 0  one lane per (query, level) derives that level's P samples ONCE (softmax and ref + offset /
-//            (W, H) on the fused path, or the given loc / attn) into a 12-byte descriptor {h, w, a} per
-//            sample in LDS (h = loc_y * H - 0.5 ...; h = w = -2 when the sample lies outside (-1, H) x
-//            (-1, W)), stages the tile's grad_output rows (this head) in LDS and takes the bounding box of
+//            (W, H) on the fused path, or the given loc / attn) into a 16-byte descriptor {ly, lx, a, floors}
+//            per sample in LDS (h = loc_y * H - 0.5 = floor + ly ..., the two floors + 2 packed in 16 bits each;
+//            floors -2 and fractions 0 when the sample lies outside (-1, H) x (-1, W): every corner outside),
+//            stages the tile's grad_output rows (this head) in LDS and takes the bounding box of
 //            the touched corners per level (every global load of the phase issued first).  The window = that
 //            box clipped to the tile +- halo.
 //   phase 1  counting sort of the samples by the window cell of their 2x2 corner block (the window grid
@@ -334,8 +335,8 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 //            forms the per-corner channel dots with g and writes grad_loc / grad_attn (or d offset / d logit)
 //            once per point (quad transpose-reduce).  Flagged samples add their 4 corner rows with atomics.
 //   phase 3  a 4-lane group per window pixel reads the 4 slot ranges whose cells cover it ((y,x) ->
-//            corner 1 of cell (y,x), corner 2 of (y,x-1), corner 3 of (y-1,x), corner 4 of (y-1,x-1)),
-//            accumulating w_c * a * g[query] in fp32 from the LDS descriptors and g rows (8 channels per
+//            corner 1 of cell (y,x), corner 2 of (y,x-1), corner 3 of (y-1,x), corner 4 of (y-1,x-1); the
+//            row-major cell order makes them two contiguous ranges), accumulating w_c * a * g[query] in fp32 from the LDS descriptors and g rows (8 channels per
 //            lane); the wave's 16 rows are transposed through LDS, 8 at a time, so that each atomic
 //            instruction adds two whole 128-B rows to HBM.
 //   Phases 2 and 3 read nothing the other writes: their units are dealt from one counter, interleaved
@@ -349,10 +350,13 @@ __global__ void __launch_bounds__(256) msda_bwd_f32_vec(
 // in pixel units (the level scale cancels) and d logit = a * (d attn - sum_k a_k d attn_k) (softmax
 // backward over the pair's L*P logits).
 // ------------------------------------------------------------------------------------------------
-constexpr int kWalkLanes = 4;   // phase-3 lanes per window pixel (8 channels each)
+#ifndef M2F_WALK_LANES
+#define M2F_WALK_LANES 4        // phase-3 lanes per window pixel (2: an experiment build, tools/lib)
+#endif
+constexpr int kWalkLanes = M2F_WALK_LANES;   // phase-3 lanes per window pixel (32 / kWalkLanes channels each)
 constexpr int kMaxBwdWaves = 16;
 constexpr int kSortSamples = 6144;  // samples per workgroup the counting sort holds in registers (max_qt * L * P)
-static_assert(3 * kSortSamples < 65536, "phase 3's slots hold the descriptor float index 3 * sid in 16 bits");
+static_assert(kSortSamples < 65536, "phase 3's slots hold the sample index in 16 bits");
 constexpr int kStageFloats = 8 * 32 + 8;  // per wave: 8 rows x 32 channels + 8 row offsets (a flush half)
 
 struct TileState {
@@ -488,15 +492,15 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int rs = M * D;  // value row stride (elements); N*S*M*D < 2^31 is checked on the host
   const int nsamp_max = geo.max_qt * LP;
-  // LDS carve-up (16-byte aligned pieces): g rows [max_qt][32] | desc [max_qt * LP][3] | stage [waves][264]
-  //   | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32 | slots [max_qt * LP + 4] u32 | qmap [max_qt] i32
+  // LDS carve-up (16-byte aligned pieces): g rows [max_qt][32] | desc [max_qt * LP][4] | stage [waves][264]
+  //   | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32 | slots [max_qt * LP + 8] u32 | qmap [max_qt] i32
   float* gsh = reinterpret_cast<float*>(lds_raw);
   float* desc = gsh + geo.max_qt * D;
-  float* stage = desc + ((nsamp_max * 3 + 3) & ~3);
+  float* stage = desc + nsamp_max * 4;
   int* cstart = reinterpret_cast<int*>(stage + kBwdWaves * kStageFloats);
   unsigned* oow = reinterpret_cast<unsigned*>(cstart + ((geo.max_rows + 1 + 3) & ~3));
   unsigned* slots = reinterpret_cast<unsigned*>(oow + (((nsamp_max + 31) / 32 + 3) & ~3));
-  int* qmap = reinterpret_cast<int*>(slots + nsamp_max + 4);  // pyramid position of each tile query
+  int* qmap = reinterpret_cast<int*>(slots + nsamp_max + 8);  // pyramid position of each tile query
   float fxscale = 0.f;  // DET: 2^k, grad_value contributions leave the workgroup as round(v * 2^k) in int64
   bool fixed = false;
   if constexpr (DET) {
@@ -651,18 +655,18 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         for (int p = 0; p < P; ++p) { lx[p] = in.xy[p].x; ly[p] = in.xy[p].y; av[p] = in.x[p]; }
       }
       if (!act) return;
-      float* dq = desc + (qi * LP + l * P) * 3;
+      float* dq = desc + (qi * LP + l * P) * 4;
 #pragma unroll
       for (int p = 0; p < P; ++p) {
         float h = ly[p] * H - 0.5f, w = lx[p] * W - 0.5f;
         const bool ok = h > -1.f && w > -1.f && h < static_cast<float>(H) && w < static_cast<float>(W);
         h = ok ? h : -2.f;
         w = ok ? w : -2.f;
-        dq[3 * p] = h;
-        dq[3 * p + 1] = w;
-        dq[3 * p + 2] = av[p];
+        const float fh = floorf(h), fw = floorf(w);
+        const int h0 = static_cast<int>(fh), w0 = static_cast<int>(fw);
+        *reinterpret_cast<f4*>(dq + 4 * p) =
+            f4{h - fh, w - fw, av[p], __uint_as_float(static_cast<unsigned>(h0 + 2) | (static_cast<unsigned>(w0 + 2) << 16))};
         if (ok) {
-          const int h0 = static_cast<int>(floorf(h)), w0 = static_cast<int>(floorf(w));
 #pragma unroll
           for (int ll = 0; ll < LT; ++ll)
             if (ll == l) {
@@ -766,10 +770,11 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       const int sid = tid + r * kBwdThreads;
       cell[r] = -1;
       if (sid < nsamp) {
-        const float h = desc[3 * sid], w = desc[3 * sid + 1];
-        if (h > -1.f) {  // ok sample
+        const unsigned pk = __float_as_uint(desc[4 * sid + 3]);
+        const int h0 = static_cast<int>(pk & 0xffffu) - 2, w0 = static_cast<int>(pk >> 16) - 2;
+        if (h0 != -2) {  // ok sample
           const int l = (sid % LP) / P;
-          const int c = window_cell(ts, l, static_cast<int>(floorf(h)), static_cast<int>(floorf(w)), ts.H[l], ts.W[l]);
+          const int c = window_cell(ts, l, h0, w0, ts.H[l], ts.W[l]);
           if (c >= 0) {
             cell[r] = c;
             rank[r] = atomicAdd(cstart + c, 1);
@@ -801,10 +806,10 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kSortPerThread; ++r)
-      if (cell[r] >= 0) {  // slot = desc float index << 16 | g row byte offset: phase 3 decodes it in 3 VALU
+      if (cell[r] >= 0) {  // slot = sample index << 16 | g row byte offset: phase 3 decodes it in 3 VALU
         const int sid = tid + r * kBwdThreads, qs = sid / LP;
         slots[cstart[cell[r]] + rank[r]] =
-            (static_cast<unsigned>(3 * sid) << 16) | static_cast<unsigned>(4 * g_chunk_off(qs, 0));
+            (static_cast<unsigned>(sid) << 16) | static_cast<unsigned>(4 * g_chunk_off(qs, 0));
       }
   }
   __syncthreads();
@@ -832,7 +837,8 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
   // after a barrier.
   {
     const int rows_total = ts.roff[LT];
-    const int U2 = (Qt + 15) / 16, U3 = (rows_total + 15) / 16;
+    constexpr int LPR = kWalkLanes, CPL = D / LPR, RPW = 64 / LPR;  // phase 3: lanes per row, channels per lane, rows per wave
+    const int U2 = (Qt + 15) / 16, U3 = (rows_total + RPW - 1) / RPW;
     const int ratio = max(geo.ratio23, 1);
     // phase 2, quad form: a quad of lanes takes one query, lane j owning channels 4j..4j+3 and 16+4j..16+4j+3
     // (one load address per corner row: the second half is the immediate offset).  Per level, lane j derives
@@ -852,7 +858,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       const int64_t nq = static_cast<int64_t>(n) * S + q;
       const f4 gA = *reinterpret_cast<const f4*>(gsh + g_chunk_off(qi, j));
       const f4 gB = *reinterpret_cast<const f4*>(gsh + g_chunk_off(qi, 4 + j));
-      const float* dq = desc + qi * LP * 3;
+      const float* dq = desc + qi * LP * 4;
       const int sid0 = qi * LP, sh = sid0 & 31;
       const unsigned w0f = oow[sid0 >> 5], w1f = oow[min((sid0 + LP - 1) >> 5, (nsamp_max + 31) / 32 - 1)];
       const unsigned qfar = (sh ? (w0f >> sh) | (w1f << (32 - sh)) : w0f) & ((1u << LP) - 1u);
@@ -863,10 +869,12 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         const int H = geo.H[l], W = geo.W[l];
         const int lbase = ((n * S + geo.start[l]) * M + m) * D * 4;
         // this lane's point (l, j)
-        const float* dk = dq + 3 * (l * P + j);
-        const float h = dk[0], w = dk[1], a = dk[2];
-        // not-ok samples carry h = w = -2 (every corner outside, ok false)
-        const QuadPoint k = quad_point(h, w, H, W, lbase, rsb);
+        const f4 dk = *reinterpret_cast<const f4*>(dq + 4 * (l * P + j));
+        const float a = dk[2];
+        // not-ok samples carry floors -2 (every corner outside, ok false)
+        const unsigned pk = __float_as_uint(dk[3]);
+        const QuadPoint k = quad_point_fl(static_cast<int>(pk & 0xffffu) - 2, static_cast<int>(pk >> 16) - 2, dk[0], dk[1],
+                                          H, W, lbase, rsb);
         const bool ok = k.ok;
         const float ly = k.ly, lx = k.lx, hy = 1.f - ly, hx = 1.f - lx;
         const int o1 = k.o1, o2 = k.o2, o3 = k.o3, o4 = k.o4;
@@ -978,7 +986,6 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       }
     };
     // phase 3: per window pixel, the 4 covering slot ranges; one row-contiguous atomic add per row
-    constexpr int LPR = kWalkLanes, CPL = D / LPR, RPW = 64 / LPR;  // lanes per row, channels per lane, rows per wave
     const int jl = lane % LPR, rw = lane / LPR;
     float* wst = stage + wid * kStageFloats;               // this wave's flush half: 8 rows x 32 channels
     int* woff = reinterpret_cast<int*>(wst + 8 * 32);      // and their grad_value element offsets
@@ -1001,21 +1008,24 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
         ey = static_cast<int>((static_cast<float>(rr) + 0.5f) * ts.iww[l]);
         ex = rr - ey * ww;  // window coordinates; cells are offset by (1, 1)
         const int cw = ww + 1, cbase = ts.coff[l] + (ey + 1) * cw + ex + 1;
-        // corner 1 of cell (y, x), corner 2 of (y, x-1), corner 3 of (y-1, x), corner 4 of (y-1, x-1)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const int cell = cbase - ((c & 2) ? cw : 0) - (c & 1);
-          const int s0 = cstart[cell], s1 = cstart[cell + 1];
-          any |= s1 > s0;
-          // a record: the sample's descriptor {h, w, a} and its query's g row; the corner coefficient from the
-          // fractions ((1 - ly) a or ly a, times (1 - lx) or lx, the (1 - t) factors as fmas)
-          auto rec = [&](unsigned p) {
-            const float* dk = desc + (p >> 16);
-            const float h = dk[0], w = dk[1], a = dk[2];
-            const float ly = h - floorf(h), lx = w - floorf(w);
-            const float A = (c & 2) ? ly * a : fmaf(-ly, a, a);
+        // corner 1 of cell (y, x), corner 2 of (y, x-1), corner 3 of (y-1, x), corner 4 of (y-1, x-1).  Cells are
+        // numbered row-major, so the slot ranges of (y, x-1) and (y, x) are one contiguous range, as are those of
+        // (y-1, x-1) and (y-1, x): two walks, the six range bounds read up front
+        const int* cs = cstart + cbase;
+        const int b0 = cs[-1], b1 = cs[0], b2 = cs[1];
+        const int u0 = cs[-cw - 1], u1 = cs[-cw], u2 = cs[-cw + 1];
+        any = b2 > b0 || u2 > u0;
+        // HI: the row above (corners 3 / 4: ly a, else (1 - ly) a); a record below `mid` comes from the cell at x-1
+        // (corners 2 / 4: times lx, else (1 - lx)); the (1 - t) factors as fmas
+        auto walk = [&](auto hi_c, int s0, int mid, int s1) {
+          constexpr bool HI = decltype(hi_c)::value;
+          // a record: the sample's descriptor {ly, lx, a, -} (one 16-byte read) and its query's g row
+          auto rec = [&](unsigned p, int idx) {
+            const f4 dk = *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(desc) + ((p >> 12) & 0xffff0u));
+            const float ly = dk[0], lx = dk[1], a = dk[2];
+            const float A = HI ? ly * a : fmaf(-ly, a, a);
             const f4* g = reinterpret_cast<const f4*>(gbytes + ((p & 0xffffu) | jlb));
-            const float cf = (c & 1) ? A * lx : fmaf(-A, lx, A);
+            const float cf = idx < mid ? A * lx : fmaf(-A, lx, A);
 #pragma unroll
             for (int k = 0; k < CPL / 4; ++k) {  // fma chains (pairs of channels pack into v_pk_fma_f32)
               const f4 v = g[k];
@@ -1023,8 +1033,8 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
               for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(cf, v[e], acc[4 * k + e]);
             }
           };
-          // two records per step, the next pair's slots read one step ahead (unclamped: a read past the cell's
-          // range, or past the array into its 4-entry pad, is never used), so a step waits on one LDS round trip
+          // two records per step, the next pair's slots read one step ahead (unclamped: a read past the range, or
+          // past the array into its 8-entry pad, is never used), so a step waits on one LDS round trip
           const unsigned* sp = slots + s0;
           unsigned npa = sp[0], npb = sp[1];
           int i = s0;
@@ -1032,20 +1042,22 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
             const unsigned pa = npa, pb = npb;
             npa = sp[2];
             npb = sp[3];
-            rec(pa);
-            rec(pb);
+            rec(pa, i);
+            rec(pb, i + 1);
           }
-          if (i < s1) rec(npa);
-        }
+          if (i < s1) rec(npa, i);
+        };
+        walk(std::false_type{}, b0, b1, b2);
+        walk(std::true_type{}, u0, u1, u2);
       }
       if (any) {
         const int y = ts.wy0[l] + ey, x = ts.wx0[l] + ex;
         off = ((n * S + ts.start[l] + y * ts.W[l] + x) * M + m) * D;
       }
-      // transpose the wave's 16 rows through LDS, 8 rows at a time, so that each atomic instruction adds two whole
+      // transpose the wave's RPW rows through LDS, 8 rows at a time, so that each atomic instruction adds two whole
       // 128-B rows, one dword per lane (the L2 takes atomics per 64-B request)
 #pragma unroll
-      for (int half = 0; half < 2; ++half) {
+      for (int half = 0; half < RPW / 8; ++half) {
         if ((rw >> 3) == half) {
 #pragma unroll
           for (int k = 0; k < CPL / 4; ++k)
@@ -1828,9 +1840,9 @@ int fwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
 // Tile geometry for the tiled backward; false when the configuration does not qualify (then the
 // caller uses the untiled kernels).  Lq == S: the queries are the flattened pyramid.
 // Options (m2f_set_option):
-//   msda_threads (512): workgroup size, 512 (two workgroups per CU) or 1024 (one);
+//   msda_threads (1024; 512 in the deterministic mode): workgroup size, 512 (two workgroups per CU) or 1024 (one);
 //   msda_tile / msda_tile_w (12 / 12 at 512 threads, 16 / 16 at 1024): tile on the finest level;
-//   msda_halo (8): window halo;  msda_win_rows (cells per workgroup; the halo shrinks until the
+//   msda_halo (8 at 512 threads, 12 at 1024): window halo;  msda_win_rows (cells per workgroup; the halo shrinks until the
 //   window fits).  Geometry only: every setting computes the same gradients (tests sweep them).
 bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds, int& threads) {
   if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
@@ -1846,6 +1858,8 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     // phase 2 forms corner offsets (y0 * W + x0) * rs with 24-bit multiplies (__umul24): a level of 2^24 or
     // more pixels would silently wrap, so such shapes take the untiled kernels
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] >= (int64_t{1} << 24)) return false;
+    // the descriptors pack each floor + 2 (-2 .. H - 1) in 16 bits
+    if (geo.H[l] > 65533 || geo.W[l] > 65533) return false;
     geo.start[l] = static_cast<int>(total);
     geo.invW[l] = 1.f / static_cast<float>(geo.W[l]);
     geo.invH[l] = 1.f / static_cast<float>(geo.H[l]);
@@ -1853,36 +1867,48 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   if (total != d.S) return false;
-  threads = m2f::option(m2f::kOptMsdaThreads, 512) >= 1024 ? 1024 : 512;
+  // 1024 threads with 16x16 tiles and a halo of 12 (one workgroup per CU): at config 2 1.707 ms with near-init
+  // sampling against 1.697 for 512 threads / 12x12 / halo 8 (two per CU), and 2.43 against 4.51 ms with N(0, 4 px)
+  // offsets, where the larger tiles flush fewer window rows per owned row and the halo keeps samples out of the
+  // direct atomics (profiles/r04_i*_mb.txt).  The deterministic mode keeps 512 / 12x12 / 8 (2.74 vs 3.55 ms).
+  const bool det = m2f::option(m2f::kOptMsdaBwdDet, 0) != 0;
+  const int first = m2f::option(m2f::kOptMsdaThreads, det ? 512 : 1024) >= 1024 ? 1024 : 512;
   geo.ratio23 = std::max(1, m2f::option(m2f::kOptMsdaBwdRatio, 1));
-  // 512 threads: 12x12 tiles (78 KB of LDS, two workgroups per CU) measured 2.44 ms at config 2 against 2.45
-  // (8x16), 2.52 (16x8) and 2.65 for 1024 threads with 16x16 tiles (tools/msda_bench.py, r2k)
-  const int tile_h = std::max(1, m2f::option(m2f::kOptMsdaTile, threads == 1024 ? 16 : 12));
-  const int tile_w = std::max(1, m2f::option(m2f::kOptMsdaTileW, tile_h));
-  geo.nty = (geo.H[fi] + tile_h - 1) / tile_h;
-  geo.ntx = (geo.W[fi] + tile_w - 1) / tile_w;
-  geo.max_halo = std::max(0, m2f::option(m2f::kOptMsdaHalo, 8));
-  // cells of the largest window any workgroup can choose (tile + 2 halo + 1 per axis, clipped to the level),
-  // unless a smaller budget is asked for; it must hold every level's share of one tile at halo 0 (tiles
-  // span at most ceil(n / nt) pixels per axis, tile_lo) plus the extra cell row / column
-  int own = 0, qt = 0, full = 0;
-  for (int l = 0; l < d.L; ++l) {
-    const int th = (geo.H[l] + geo.nty - 1) / geo.nty, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx;
-    own += (std::min(geo.H[l], th + 1) + 1) * (std::min(geo.W[l], tw + 1) + 1);  // clipped like `full`
-    full += (std::min(geo.H[l], th + 2 * geo.max_halo) + 1) * (std::min(geo.W[l], tw + 2 * geo.max_halo) + 1);
-    qt += th * tw;
+  const TileGeom base = geo;
+  // a default 1024-thread geometry whose LDS does not fit (e.g. four levels: 16 samples per query) falls back to
+  // the 512-thread one; an explicit msda_threads does not
+  for (int attempt = 0; attempt < 2; ++attempt) {
+    if (attempt == 1 && (first == 512 || m2f::option_raw(m2f::kOptMsdaThreads) >= 0)) break;
+    threads = attempt == 0 ? first : 512;
+    geo = base;
+    const int tile_h = std::max(1, m2f::option(m2f::kOptMsdaTile, threads == 1024 ? 16 : 12));
+    const int tile_w = std::max(1, m2f::option(m2f::kOptMsdaTileW, tile_h));
+    geo.nty = (geo.H[fi] + tile_h - 1) / tile_h;
+    geo.ntx = (geo.W[fi] + tile_w - 1) / tile_w;
+    geo.max_halo = std::max(0, m2f::option(m2f::kOptMsdaHalo, threads == 1024 ? 12 : 8));
+    // cells of the largest window any workgroup can choose (tile + 2 halo + 1 per axis, clipped to the level),
+    // unless a smaller budget is asked for; it must hold every level's share of one tile at halo 0 (tiles
+    // span at most ceil(n / nt) pixels per axis, tile_lo) plus the extra cell row / column
+    int own = 0, qt = 0, full = 0;
+    for (int l = 0; l < d.L; ++l) {
+      const int th = (geo.H[l] + geo.nty - 1) / geo.nty, tw = (geo.W[l] + geo.ntx - 1) / geo.ntx;
+      own += (std::min(geo.H[l], th + 1) + 1) * (std::min(geo.W[l], tw + 1) + 1);  // clipped like `full`
+      full += (std::min(geo.H[l], th + 2 * geo.max_halo) + 1) * (std::min(geo.W[l], tw + 2 * geo.max_halo) + 1);
+      qt += th * tw;
+    }
+    geo.max_rows = m2f::option(m2f::kOptMsdaWinRows, full);
+    geo.max_qt = qt;
+    const int lp = d.L * d.P;
+    // phase 3's 32-bit slots hold the g-row byte offset 128 * qs (qs < qt) in their low 16 bits: qt <= 512
+    if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff || qt > 512) continue;
+    if (static_cast<int64_t>(qt) * lp > kSortSamples) continue;
+    const size_t ns = static_cast<size_t>(qt) * lp;
+    lds = (static_cast<size_t>(qt) * 32 + ns * 4 + (threads / 64) * kStageFloats) * 4 +
+          ((static_cast<size_t>(geo.max_rows) + 1 + 3) & ~static_cast<size_t>(3)) * 4 +
+          (((ns + 31) / 32 + 3) & ~static_cast<size_t>(3)) * 4 + (ns + 8) * 4 + static_cast<size_t>(qt) * 4;
+    if (lds <= 156 * 1024) return true;
   }
-  geo.max_rows = m2f::option(m2f::kOptMsdaWinRows, full);
-  geo.max_qt = qt;
-  const int lp = d.L * d.P;
-  // phase 3's 32-bit slots hold the g-row byte offset 128 * qs (qs < qt) in their low 16 bits: qt <= 512
-  if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff || qt > 512) return false;
-  if (static_cast<int64_t>(qt) * lp > kSortSamples) return false;
-  const size_t ns = static_cast<size_t>(qt) * lp;
-  lds = (static_cast<size_t>(qt) * 32 + ((ns * 3 + 3) & ~static_cast<size_t>(3)) + (threads / 64) * kStageFloats) * 4 +
-        ((static_cast<size_t>(geo.max_rows) + 1 + 3) & ~static_cast<size_t>(3)) * 4 + (((ns + 31) / 32 + 3) & ~static_cast<size_t>(3)) * 4 +
-        (ns + 4) * 4 + static_cast<size_t>(qt) * 4;
-  return lds <= 156 * 1024;
+  return false;
 }
 
 // Deterministic-mode buffers (msda_bwd_det): the int64 accumulator of grad_value and the scale words.
@@ -1956,7 +1982,7 @@ int bwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
   if (rc) return rc;
   if (!gout || !gv || !gl || !ga) return m2f::fail(M2F_EINVAL, "%s: null gradient pointer", fn);
   const size_t gv_bytes = static_cast<size_t>(d.N) * d.S * d.M * d.D * sizeof(T);
-  hipError_t e = hipMemsetAsync(gv, 0, gv_bytes, st);
+  hipError_t e = m2f::zero_async(gv, gv_bytes, st);
   if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
   bool done = false;
   if constexpr (std::is_same<T, float>::value) {
@@ -2264,7 +2290,7 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t nval = static_cast<int64_t>(d.N) * d.S * d.M * d.D;
   const size_t gv_bytes = static_cast<size_t>(nval) * sizeof(float);
-  hipError_t e = hipMemsetAsync(grad_value, 0, gv_bytes, st);
+  hipError_t e = m2f::zero_async(grad_value, gv_bytes, st);
   if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
   const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
   DetBufs det;
@@ -2275,7 +2301,7 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
                        "(m2f_msda_fused_bwd_workspace)", fn, static_cast<long long>(need));
     det.acc = static_cast<unsigned long long*>(workspace);
     det.scale = reinterpret_cast<unsigned*>(det.acc + nval);
-    e = hipMemsetAsync(workspace, 0, static_cast<size_t>(need), st);
+    e = m2f::zero_async(workspace, static_cast<size_t>(need), st);
     if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset workspace: %s", fn, hipGetErrorString(e));
     const int64_t n4 = static_cast<int64_t>(d.N) * d.Lq * d.M * d.D / 4;  // grad_output (N, Lq, M*32) fp32
     msda_det_scale_kernel<<<2048, 256, 0, st>>>(reinterpret_cast<const float4*>(grad_output), n4, det.scale);
@@ -2303,7 +2329,7 @@ extern "C" int m2f_diag_msda_bwd_stamps_f32(const float* value, const float* loc
   if (num_levels != 3 || !make_tile_geom(d, host_spatial_shapes, geo, lds, threads))
     return m2f::fail(M2F_EUNSUPPORTED, "diag");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  (void)hipMemsetAsync(grad_value, 0, static_cast<size_t>(d.N) * d.S * d.M * 32 * 4, st);
+  (void)m2f::zero_async(grad_value, static_cast<size_t>(d.N) * d.S * d.M * 32 * 4, st);
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
 #define M2F_DIAG_LAUNCH(TPB, NF)                                                                                  \
   do {                                                                                                           \

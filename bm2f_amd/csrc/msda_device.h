@@ -198,6 +198,33 @@ __device__ __forceinline__ QuadPoint quad_point(float h, float w, int H, int W, 
   return k;
 }
 
+// quad_point from a point's floors and fractions (h = fh + ly, w = fw + lx; fh = fw = -2 and ly = lx = 0 for a point
+// outside, as quad_point moves it): the same offsets, weights and flags as quad_point(h, w, ...)
+__device__ __forceinline__ QuadPoint quad_point_fl(int fh, int fw, float ly, float lx, int H, int W, int lbase, int rsb) {
+  QuadPoint k;
+  k.ok = fh != -2;
+  const float hy = 1.f - ly, hx = 1.f - lx;
+  const bool vy0 = fh >= 0, vy1 = fh < H - 1, vx0 = fw >= 0, vx1 = fw < W - 1;
+  const int y0 = static_cast<int>(__builtin_amdgcn_fmed3f(static_cast<float>(fh), 0.f, static_cast<float>(H - 1)));
+  const int x0 = static_cast<int>(__builtin_amdgcn_fmed3f(static_cast<float>(fw), 0.f, static_cast<float>(W - 1)));
+  k.o1 = mad_u24(mad_u24(y0, W, x0), rsb, lbase);
+  const int dx = (vx0 && vx1) ? rsb : 0, dy = (vy0 && vy1) ? W * rsb : 0;
+  k.o2 = k.o1 + dx;
+  k.o3 = k.o1 + dy;
+  k.o4 = k.o3 + dx;
+  k.c1 = vy0 && vx0;
+  k.c2 = vy0 && vx1;
+  k.c3 = vy1 && vx0;
+  k.c4 = vy1 && vx1;
+  k.w1 = k.c1 ? hy * hx : 0.f;
+  k.w2 = k.c2 ? hy * lx : 0.f;
+  k.w3 = k.c3 ? ly * hx : 0.f;
+  k.w4 = k.c4 ? ly * lx : 0.f;
+  k.ly = ly;
+  k.lx = lx;
+  return k;
+}
+
 __device__ __forceinline__ float pick4(const f4& v, int c) {
   return c == 0 ? v.x : (c == 1 ? v.y : (c == 2 ? v.z : v.w));
 }

@@ -246,8 +246,8 @@ extern "C" int m2f_add_layernorm_bwd_f32(const float* grad_y, const float* a, co
                      static_cast<long long>(need));
   float* part = static_cast<float*>(workspace);
   if (rows == 0) {
-    if (grad_gamma) (void)hipMemsetAsync(grad_gamma, 0, C * sizeof(float), st);
-    if (grad_beta) (void)hipMemsetAsync(grad_beta, 0, C * sizeof(float), st);
+    if (grad_gamma) (void)m2f::zero_async(grad_gamma, C * sizeof(float), st);
+    if (grad_beta) (void)m2f::zero_async(grad_beta, C * sizeof(float), st);
     return m2f::check_launch(fn);
   }
   const int nv = (C / 4 + 63) / 64;

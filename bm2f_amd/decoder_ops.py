@@ -402,6 +402,20 @@ def image_mask_fold(mask_features, mask_features_lp=None):
     return MaskFeatureFold(mask_features, lp.detach().reshape(B, C, H * W), (H, W), lambda df, shape: df.view(shape))
 
 
+def colsum_f32(g2):
+    """``g2.sum(0, dtype=float32)`` for a long (R, C) matrix as two reductions with many outputs each (1024-row
+    blocks, then the block sums): torch reduces a long column to few outputs across workgroups with semaphores it
+    zeroes by a memset, which a HIP graph replay on this ROCm does not re-run correctly (bench_model.GraphStep)."""
+    R, C = g2.shape
+    ch = 1024
+    if R <= ch:
+        return g2.sum(0, dtype=torch.float32)
+    pad = (-R) % ch
+    if pad:
+        g2 = torch.cat([g2, g2.new_zeros(pad, C)])
+    return g2.reshape(-1, ch, C).sum(1, dtype=torch.float32).sum(0)
+
+
 class _TokenLinear(Function):
     """y = x W^T + b for the cross-attention K/V projections over the memory tokens (B * HW_l rows, up to
     262,144 at 1024^2 bs16; reference: nn.MultiheadAttention's in_proj, mask2former_transformer_decoder.py
@@ -435,7 +449,7 @@ class _TokenLinear(Function):
             else:
                 gw = g2.t() @ x2
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = g2.sum(0, dtype=torch.float32).to(w.dtype)
+            gb = colsum_f32(g2).to(w.dtype)
         return gx, gw, gb
 
 

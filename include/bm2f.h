@@ -312,7 +312,8 @@ int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, 
  * msda_halo, msda_win_rows, msda_bwd_tiled, msda_fwd_tiled, msda_fwd_quad, msda_fwd_pb, msda_bwd_overlap,
  * msda_bwd_ratio, msda_bwd_det, msda_fwd_lds, msda_fwd_tile, msda_fwd_tile_w, msda_fwd_cap, msda_fwd_halo (MSDA
  * partitions, variants, LDS windows, deterministic mode), mattn_dq_atomic, mattn_fwd_minblk, mattn_bwd_minblk
- * (masked-attention dQ variant, key blocks per workgroup at least), gemm_nt_cfg, x3_tn_nw, x3_tn_blocks,
+ * (masked-attention dQ variant, key blocks per workgroup at least), mask_df_stage (mask-einsum feature
+ * gradient: k-steps per LDS stage, 4 or 1), gemm_nt_cfg, x3_tn_nw, x3_tn_blocks,
  * x3_nt_cfg (GEMM tilings).  Every option changes
  * the partition or kernel variant only; results agree to fp32 rounding (summation order may differ between
  * variants).  Process-wide; not synchronised with launches in flight on other threads.  Unknown names return

@@ -1,6 +1,10 @@
 import os
 import sys
 
+# HIP graph replays need the runtime's graph packet capture off on this ROCm (bm2f_amd/__init__.py); set before any
+# test initialises the device
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

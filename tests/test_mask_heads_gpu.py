@@ -133,10 +133,19 @@ def test_mask_heads_bwd_embed(device, dt, B, Q, N):
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("H,B,Q,N,out", [(10, 2, 100, 4096, "f32"), (10, 2, 100, 4096, "same"), (1, 1, 7, 200, "f32"),
-                                         (3, 2, 37, 1000, "same"), (16, 1, 20, 520, "f32")])
-def test_mask_heads_bwd_feats(device, dt, H, B, Q, N, out):
+                                         (3, 2, 37, 1000, "same"), (16, 1, 20, 520, "f32"), (10, 1, 200, 1040, "f32"),
+                                         (2, 1, 256, 264, "same")])
+@pytest.mark.parametrize("stage", [4, 1])
+def test_mask_heads_bwd_feats(device, dt, H, B, Q, N, out, stage):
     """d feats = sum_h E_h^T G_h over the heads' gradient buffers in place: fp32 output within fp32
-    accumulation error of the fp64 sum, dtype output within one ulp of it rounded once."""
+    accumulation error of the fp64 sum, dtype output within one ulp of it rounded once; 64 (the default) or 16 G
+    rows per LDS stage (stages spanning head boundaries, partial last stages)."""
+    from bm2f_amd import _native
+    with _native.options(mask_df_stage=stage):
+        _bwd_feats_case(device, dt, H, B, Q, N, out)
+
+
+def _bwd_feats_case(device, dt, H, B, Q, N, out):
     from bm2f_amd import decoder_ops
     gen = torch.Generator(device=device).manual_seed(H * 1000 + N)
     es = [torch.randn(B, Q, 256, device=device, generator=gen).to(DT[dt]) for _ in range(H)]

@@ -186,14 +186,15 @@ def _pyramid_case(shapes, N, M, far_frac, seed):
 @pytest.mark.parametrize("tile,rows,halo", [(16, 2304, 8), (12, 2304, 8), (8, 480, 8), (4, 64, 2), (8, 200, 0),
                                            (6, 2304, 12), (16, 700, 8)])
 @pytest.mark.parametrize("overlap,ratio", [(1, 1), (1, 3), (0, 1)])
-def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, overlap, ratio):
+@pytest.mark.parametrize("threads", [1024, 512])
+def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, overlap, ratio, threads):
     """The tiled backward over tile / cell-budget / halo geometries (m2f_set_option msda_*: geometry only), on a
     non-square pyramid whose tiles do not divide every level evenly, 5 % of the samples thrown far (the
     direct-atomic path), against the C oracle and the untiled kernel; phases 2 and 3 as one interleaved work queue
     (msda_bwd_overlap 1, the default) and one after the other."""
     from bm2f_amd import _native, msda
     with _native.options(msda_tile=tile, msda_win_rows=rows, msda_halo=halo, msda_bwd_overlap=overlap,
-                         msda_bwd_ratio=ratio):
+                         msda_bwd_ratio=ratio, msda_threads=threads):
         _tiled_backward_case(device, tile, rows)
 
 

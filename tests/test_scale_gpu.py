@@ -596,3 +596,43 @@ def test_op_level_forward_lds_bitwise_vs_quad(device, regime):
     ref_out = msda_ref.msda_forward(value.double(), stc, torch.tensor([0, 1024, 5120]), loc.float().double(),
                                     attn.float().double())
     _close(got.cpu(), ref_out)
+
+
+@pytest.mark.parametrize("swin,frames,amp", [("swin_l", None, torch.float16), ("swin_t", 2, torch.bfloat16)])
+def test_graph_step_matches_eager(device, swin, frames, amp):
+    """bench_model.GraphStep (the whole training step captured as a HIP graph and replayed; bench.py --graph, the
+    default for the per-rank configs 4 / 5) against the same steps run eagerly on a copy: with torch's deterministic
+    algorithms, the math attention backend and the MSDA deterministic mode both are bitwise repeatable, so after the two warm-up steps and two
+    replays (the capture itself executes nothing) the losses and every parameter agree exactly.  Small shapes of the config 4 / 5 slices (256^2)."""
+    import copy
+
+    from bm2f_amd import _native
+    from bm2f_amd.bench_model import GraphStep, HeadBench, head_features, make_optimizer, make_scaler, train_step
+    torch.manual_seed(0)
+    n = 2 * (frames or 1)
+    base = HeadBench(swin, 20, 10, frames=frames).to(device)
+    eager = copy.deepcopy(base)
+    feats = head_features(swin, n, 256, 256, device, seed=3)
+    feats_e = {k: v.detach().clone().requires_grad_() for k, v in feats.items()}
+    prev_det, prev_cudnn = torch.are_deterministic_algorithms_enabled(), torch.backends.cudnn.deterministic
+    torch.use_deterministic_algorithms(True, warn_only=True)
+    torch.backends.cudnn.deterministic = True
+    from torch.nn.attention import SDPBackend, sdpa_kernel
+    try:
+        # the math attention backend: torch's flash backward is non-deterministic even here (it warns)
+        with _native.options(msda_bwd_det=1), sdpa_kernel([SDPBackend.MATH]):
+            opt_g, opt_e = make_optimizer(base, capturable=True), make_optimizer(eager, capturable=True)
+            sc_g, sc_e = make_scaler(amp), make_scaler(amp)
+            g = GraphStep(base, opt_g, feats, amp, scaler=sc_g, warmup=2)   # 2 eager warm-up steps (capture runs nothing)
+            losses_e = [train_step(eager, opt_e, feats_e, amp, scaler=sc_e) for _ in range(2)]
+            for _ in range(2):
+                lg = g().clone()
+                losses_e.append(train_step(eager, opt_e, feats_e, amp, scaler=sc_e))
+            torch.cuda.synchronize()
+        assert torch.isfinite(lg)
+        assert torch.equal(lg, losses_e[-1]), (lg.item(), losses_e[-1].item())
+        for (nm, pg), (_, pe) in zip(base.named_parameters(), eager.named_parameters()):
+            assert torch.equal(pg, pe), nm
+    finally:
+        torch.use_deterministic_algorithms(prev_det)
+        torch.backends.cudnn.deterministic = prev_cudnn

@@ -5,7 +5,7 @@
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd "$R" && mkdir -p gpurun_out && export TMPDIR=/tmp
-B="python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-modes --kernel-steps 0"
+B="python3 $R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-modes --no-dropin --no-peaks --kernel-steps 0"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$R/gpurun_out/pmc_fetch" -o fetch -- $B > gpurun_out/pmc_fetch.log 2>&1 && \
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE GRBM_GUI_ACTIVE --output-format csv -d "$R/gpurun_out/pmc_write" -o write -- $B > gpurun_out/pmc_write.log 2>&1 && \
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 \

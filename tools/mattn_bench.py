@@ -42,7 +42,11 @@ def main():
     ap.add_argument("--dq-atomic", action="store_true")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library option (m2f_set_option) for this run, repeatable; e.g. --opt mattn_bwd_minblk=4")
+    ap.add_argument("--lib", default=None, help="another build of libbm2f.so to load (A/B against a baseline build)")
     a = ap.parse_args()
+    if a.lib:
+        _native._LIB_PATH = os.path.abspath(a.lib)
+        print("lib:", os.path.basename(a.lib))
     if a.dq_atomic:
         _native.set_option("mattn_dq_atomic", 1)
     for kv in a.opt:

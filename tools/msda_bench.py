@@ -119,8 +119,11 @@ def main():
     ap.add_argument("--fused", action="store_true", help="the fused front-end kernels (the path the bench step runs)")
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library option (m2f_set_option) for this run, repeatable; e.g. --opt msda_fwd_quad=0")
+    ap.add_argument("--lib", default=None, help="another build of libbm2f.so to load (A/B against a baseline build)")
     a = ap.parse_args()
     from bm2f_amd import _native
+    if a.lib:
+        _native._LIB_PATH = os.path.abspath(a.lib)
     for kv in a.opt:
         k, v_ = kv.split("=")
         _native.set_option(k, int(v_))
@@ -140,7 +143,7 @@ def main():
     tf = 0.0 if a.bwd_only else timeit(fwd, a.iters)
     tb = float("nan") if a.fwd_only else timeit(bwd, a.iters)
     tf = tf or float("nan")
-    print(f"N={a.n} res={r} fused={a.fused} opts={','.join(a.opt) or '-'} stress={a.stress} noise={a.noise} : fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
+    print(f"lib={os.path.basename(a.lib) if a.lib else '-'} N={a.n} res={r} fused={a.fused} opts={','.join(a.opt) or '-'} stress={a.stress} noise={a.noise} : fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
           f"bwd {tb:.3f} ms ({bwd_bytes / tb / 1e6:.0f} GB/s alg)")
 
 
