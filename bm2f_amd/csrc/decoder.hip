@@ -901,7 +901,10 @@ int plan_chunks(int B, int H, int Lk, int* chunk_len, int* nchunks, int minblk =
   return 0;
 }
 int fwd_minblk() { return std::max(1, m2f::option(m2f::kOptMattnFwdMinblk, 2)); }
-int bwd_minblk() { return std::max(1, m2f::option(m2f::kOptMattnBwdMinblk, 2)); }
+// backward: 4 key blocks per chunk at least (every chunk re-stages Q, dO, LSE, delta and writes a dQ partial): at
+// config 2 / Lk = 1,024 0.143 -> 0.063 ms, config 4 / Lk = 4,096 0.124 -> 0.068 ms, equal at Lk = 16,384
+// (profiles/r04_o_mattn_minblk.txt)
+int bwd_minblk() { return std::max(1, m2f::option(m2f::kOptMattnBwdMinblk, 4)); }
 
 size_t bwd_lds_bytes(int Lqp, bool k16, int elt, int dq_copies = 1) {
   const int RS = k16 ? kDP : kD + 1;
