@@ -22,7 +22,7 @@ def build():
     csrc = os.path.join(ROOT, "bm2f_amd", "csrc")
     cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "-shared", "--offload-arch=gfx950", "-DM2F_DIAG",
            "-munsafe-fp-atomics", "-I" + os.path.join(ROOT, "include"), "-I" + csrc, os.path.join(csrc, "msda.hip"),
-           "-o", LIB]
+           os.path.join(csrc, "eltwise.hip"), "-o", LIB]   # eltwise.hip: m2f::zero_async
     subprocess.run(cmd, check=True)
 
 
