@@ -396,12 +396,15 @@ __global__ void __launch_bounds__(256) mask_de_reduce_kernel(const float* __rest
 
 // d features = sum over heads h of E_h^T G_h, one pass over the heads' G (no concatenation):
 // df[b, c, n] = sum_{h, q} Et[b, c, h * QP + q] G_h[b, q, n], Et the embeds transposed and zero-padded to QP
-// (a multiple of 16) queries per head.  Block = (image, 128 columns of n), 4 waves, wave w: channels
+// (a multiple of 16) queries per head, stored in the MFMA A-fragment order (bm2f.h).  Block = (image, 128 columns of n), 4 waves, wave w: channels
 // 64 w .. 64 w + 63 (two 32-tiles) x the four 32-column tiles.  Per k-step (16 queries of one head) the G
 // rows are staged in LDS (rows padded to 320 B: the transposed ds_read_b64_tr_b16 of the B operand is
 // conflict-free), double-buffered with the next two steps' global loads in registers; the A fragments
-// (Et rows, L2-resident) load straight from global memory two steps ahead (loaded at their step they left
-// every step waiting out an L2 round trip: 1.32 -> see DESIGN.md §3).  fp32 accumulation, one rounding to T.
+// (Et, L2-resident, 1 KB per wave load in fragment order) load straight from global memory one stage ahead.
+// fp32 accumulation, one rounding to T.
+#ifndef M2F_DF_DIAG
+#define M2F_DF_DIAG 0
+#endif
 constexpr int kDfCols = 128, kDfPitch = kDfCols + 32, kDfMaxHeads = 16;
 
 struct DfHeads {
@@ -419,6 +422,9 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
   constexpr int GP = KR * kDfCols / 8 / 256;                  // 16-byte G pieces per thread per stage
   __shared__ __attribute__((aligned(16))) T sg[2][KR * kDfPitch];
   __shared__ __attribute__((aligned(16))) O so[4][32][32 + EPP];
+  // the heads' G pointers: a per-lane index into the kernel arguments is a global load the G load then waits on
+  // (every stage paid two memory round trips); from LDS it is a ds_read
+  __shared__ const T* sgp[kDfMaxHeads];
   const int cc = blockIdx.x % ncol, b = blockIdx.x / ncol;
   const int64_t n0 = static_cast<int64_t>(cc) * kDfCols;
   const int cw = static_cast<int>(min<int64_t>(kDfCols, N - n0));
@@ -436,15 +442,16 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
       const int k = stg * KR + (tid >> 4) + 16 * i;
       const int h = static_cast<int>((static_cast<float>(k) + 0.5f) * iqp), q = k - h * QP;   // k < 2^16: exact
       if (cok && k < KP && q < Q)
-        v[i] = *reinterpret_cast<const s8*>(static_cast<const T*>(heads.g[h]) + (static_cast<int64_t>(b) * Q + q) * N +
-                                            n0 + scol);
+        v[i] = *reinterpret_cast<const s8*>(sgp[h] + (static_cast<int64_t>(b) * Q + q) * N + n0 + scol);
     }
   };
   auto gstore = [&](int buf, const s8 (&v)[GP]) {
 #pragma unroll
     for (int i = 0; i < GP; ++i) *reinterpret_cast<s8*>(&sg[buf][((tid >> 4) + 16 * i) * kDfPitch + scol]) = v[i];
   };
-  const T* et = Et + (static_cast<int64_t>(b) * C + 64 * w + li) * KP + lh * 8;
+  // Et in fragment order: the 16-byte A piece of lane l for (32-channel group, k-step) at
+  // ((b * 8 + group) * nsteps + step) * 512 + 8 l -- each A load instruction reads 1 KB contiguous
+  const T* et = Et + (static_cast<int64_t>(b) * 8 + 2 * w) * nsteps * 512 + lane * 8;
   f16v acc[2][4];
 #pragma unroll
   for (int j = 0; j < 2; ++j)
@@ -459,10 +466,12 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
     for (int s = 0; s < KS; ++s) {
       const int sc = min(stg * KS + s, nsteps - 1);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) af[s][j] = *reinterpret_cast<const s8*>(et + static_cast<int64_t>(32 * j) * KP + sc * 16);
+      for (int j = 0; j < 2; ++j) af[s][j] = *reinterpret_cast<const s8*>(et + (static_cast<int64_t>(j) * nsteps + sc) * 512);
     }
   };
   s8 gr[GP], a_cur[KS][2], a_nxt[KS][2];
+  if (tid < H) sgp[tid] = static_cast<const T*>(heads.g[tid]);
+  __syncthreads();
   gload(0, gr);
   aload(0, a_cur);
   gstore(0, gr);
@@ -471,8 +480,12 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
     const int buf = stg & 1;
     const bool more = stg + 1 < nstages;
     if (more) {  // the next stage's G rows and A fragments in flight during this stage's MFMAs
+#if M2F_DF_DIAG != 2
       gload(stg + 1, gr);
+#endif
+#if M2F_DF_DIAG != 1
       aload(stg + 1, a_nxt);
+#endif
     }
     const T* base = &sg[buf][0];
 #pragma unroll

@@ -258,7 +258,8 @@ def mask_heads_bwd_feats(es, gs, out_dtype):
     QP = (Q + 15) // 16 * 16
     et = torch.zeros((B, H, QP, C), dtype=es[0].dtype, device=es[0].device)
     et[:, :, :Q] = torch.stack(es, 1)
-    et = et.permute(0, 3, 1, 2).reshape(B, C, H * QP).contiguous()
+    # (b, k = (step, half, e), c = (group, lane)) -> MFMA fragment order (b, group, step, half, lane, e) (bm2f.h)
+    et = et.view(B, H * QP // 16, 2, 8, C // 32, 32).permute(0, 4, 1, 2, 5, 3).contiguous()
     ptrs = (ctypes.c_void_p * H)(*[g.data_ptr() for g in gs])
     df = torch.empty((B, C, N), dtype=out_dtype, device=gs[0].device)
     _native.call("m2f_mask_heads_bwd_feats", _code(gs[0].dtype), ctypes.cast(ptrs, ctypes.c_void_p), H, et.data_ptr(),

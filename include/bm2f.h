@@ -164,8 +164,10 @@ int m2f_mask_row_fix(uint32_t* bits, int rows, int nwords, int keys, void* strea
  *   Needs n % 16 == 0, Q <= 256.
  * m2f_mask_heads_bwd_feats: grad_feats (B, 256, n) = out_dtype( sum_h embed_h^T . grad_masks_h ) over `heads`
  *   heads' gradients (an array of device pointers, each (B, Q, n), no concatenation); embed_t is the
- *   heads' embeds transposed, (B, 256, heads * padded_queries) with zero rows past Q in each head's
- *   padded_queries (a multiple of 16) slots.  out_dtype = dtype, or M2F_F32 when the features are fp32
+ *   heads' embeds transposed, Et[b][c][k] = embed_{k / padded_queries}[b][k % padded_queries][c] for k < heads *
+ *   padded_queries (zero past Q in each head's padded_queries slots, a multiple of 16), stored in MFMA
+ *   fragment order: element (b, c, k) at ((((b * 8 + c / 32) * (K / 16) + k / 16) * 2 + (k / 8) % 2) * 32 +
+ *   c % 32) * 8 + k % 8, K = heads * padded_queries.  out_dtype = dtype, or M2F_F32 when the features are fp32
  *   (autocast's copy): one rounding either way.  heads <= 16, n % 8 == 0. */
 int m2f_mask_heads_bwd_workspace(int batch, int num_queries, int64_t n, int64_t* workspace_bytes);
 int m2f_mask_heads_bwd_embed(int dtype, const void* grad_masks, const void* feats, int batch, int num_queries,
