@@ -396,15 +396,13 @@ __global__ void __launch_bounds__(256) mask_de_reduce_kernel(const float* __rest
 
 // d features = sum over heads h of E_h^T G_h, one pass over the heads' G (no concatenation):
 // df[b, c, n] = sum_{h, q} Et[b, c, h * QP + q] G_h[b, q, n], Et the embeds transposed and zero-padded to QP
-// (a multiple of 16) queries per head, stored in the MFMA A-fragment order (bm2f.h).  Block = (image, 128 columns of n), 4 waves, wave w: channels
-// 64 w .. 64 w + 63 (two 32-tiles) x the four 32-column tiles.  Per k-step (16 queries of one head) the G
-// rows are staged in LDS (rows padded to 320 B: the transposed ds_read_b64_tr_b16 of the B operand is
-// conflict-free), double-buffered with the next two steps' global loads in registers; the A fragments
-// (Et, L2-resident, 1 KB per wave load in fragment order) load straight from global memory one stage ahead.
-// fp32 accumulation, one rounding to T.
-#ifndef M2F_DF_DIAG
-#define M2F_DF_DIAG 0
-#endif
+// (a multiple of 16) queries per head, stored in the MFMA A-fragment order (bm2f.h).  Block = (image, 128
+// columns of n), 4 waves, wave w: channels 64 w .. 64 w + 63 (two 32-tiles) x the four 32-column tiles.  Per
+// k-step (16 queries of one head) the G rows are staged in LDS (rows padded to 320 B: the transposed
+// ds_read_b64_tr_b16 of the B operand is conflict-free), double-buffered with the next stage's global loads in
+// registers; the A fragments (Et, L2-resident, one contiguous KB per wave load in fragment order) load straight
+// from global memory one stage ahead.  fp32 accumulation, one rounding to T.  Config 2: 0.95 ms; with the G
+// loads removed (a timing-only build) 0.71 ms, so the G latency left exposed is about a quarter of the time.
 constexpr int kDfCols = 128, kDfPitch = kDfCols + 32, kDfMaxHeads = 16;
 
 struct DfHeads {
@@ -480,12 +478,8 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
     const int buf = stg & 1;
     const bool more = stg + 1 < nstages;
     if (more) {  // the next stage's G rows and A fragments in flight during this stage's MFMAs
-#if M2F_DF_DIAG != 2
       gload(stg + 1, gr);
-#endif
-#if M2F_DF_DIAG != 1
       aload(stg + 1, a_nxt);
-#endif
     }
     const T* base = &sg[buf][0];
 #pragma unroll
