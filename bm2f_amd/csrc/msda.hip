@@ -568,8 +568,10 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
     // FUSED: a quad of lanes per query (lane l < LT handles level l), so the softmax over the pair's L*P
     // logits is shared: each lane exps its level's P logits, the quad max is a DPP reduction (exact), and
     // the sum is carried from lane to lane in logit order (the sequential sum the forward forms)
-    constexpr int TPQ = FUSED ? 4 : LT;  // tasks per query
-    static_assert(!FUSED || LT <= 4, "one quad lane per level");
+    // a quad of lanes per query either way (the op-level path with LT lanes per query ran 3-4 % slower: its
+    // queries straddled quads and the level boxes took LT full-wave reductions)
+    constexpr int TPQ = 4;  // tasks per query
+    static_assert(LT <= 4, "one quad lane per level");
     const int ntask = Qt * TPQ;
     struct TaskIn {
       float x[P];      // logits (FUSED) or attention weights
@@ -695,7 +697,7 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       *reinterpret_cast<f4*>(gsh + g_chunk_off(qi, j)) = ld4(gout + pair * D + 4 * j);
     }
     // per-level boxes over the wave, then over the workgroup
-    if constexpr (TPQ == 4) {
+    {
       // a lane only ever touches its own level (tid & 3: the task stride is a multiple of 4), so the lanes of
       // one level (lane & 3 equal) reduce it over xor 4..32, and lane l < LT publishes level l
       const int ol = (lane & 3) < LT ? (lane & 3) : LT - 1;
@@ -711,20 +713,6 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
       if (lane < LT && a1 >= 0) {
         atomicMin(&ts.bb[lane][0], a0); atomicMax(&ts.bb[lane][1], a1);
         atomicMin(&ts.bb[lane][2], a2); atomicMax(&ts.bb[lane][3], a3);
-      }
-    } else {
-#pragma unroll
-      for (int l = 0; l < LT; ++l) {
-        int a0 = bmin_y[l], a1 = bmax_y[l], a2 = bmin_x[l], a3 = bmax_x[l];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          a0 = min(a0, __shfl_xor(a0, o)); a1 = max(a1, __shfl_xor(a1, o));
-          a2 = min(a2, __shfl_xor(a2, o)); a3 = max(a3, __shfl_xor(a3, o));
-        }
-        if (lane == 0 && a1 >= 0) {
-          atomicMin(&ts.bb[l][0], a0); atomicMax(&ts.bb[l][1], a1);
-          atomicMin(&ts.bb[l][2], a2); atomicMax(&ts.bb[l][3], a3);
-        }
       }
     }
   }
