@@ -36,10 +36,6 @@ import subprocess
 import sys
 import time
 
-# before any HIP call: the runtime's graph packet capture replays captured memsets wrongly on this ROCm
-# (bm2f_amd/__init__.py); the graph-replayed configs need it off
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
-
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -495,6 +491,11 @@ def load_traffic():
 
 def main():
     args = parse_args()
+    # before any HIP call (bm2f_amd/__init__.py): the runtime's graph packet capture replays captured memsets
+    # wrongly on this ROCm.  A graph-replayed run keeps it (faster replays) and checks after the capture that the
+    # step holds no memset node (GraphStep.nodes), falling back to eager steps if it does; others turn it off.
+    graph_run = bool(args.graph) and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "1" if graph_run else "0")
     maybe_launch(args)
     knobs = knob_env()
     if knobs and not args.allow_knobs:
@@ -549,9 +550,16 @@ def main():
         t0 = time.perf_counter()
         if graph:   # warm-up steps run eagerly inside the capture helper, then the captured step is replayed
             gstep = GraphStep(model, opt, images, amp, scaler=scaler, warmup=max(warmup, 2))
-            step_fn = gstep
-            log(f"{tag} warmup {warmup} + capture done ({time.perf_counter() - t0:.1f}s)")
-        else:
+            graph_info["nodes"] = gstep.nodes
+            log(f"{tag} warmup {warmup} + capture done ({time.perf_counter() - t0:.1f}s), nodes {gstep.nodes}")
+            if gstep.nodes.get("memset") and os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
+                log(f"{tag}: the captured step holds memset nodes, which packet capture replays wrongly: eager steps")
+                graph_info["fallback"] = "memset nodes under packet capture: eager steps"
+                graph = False
+                del gstep
+            else:
+                step_fn = gstep
+        if not graph:
             def step_fn():
                 return train_step(model, opt, images, amp, scaler=scaler)
             for i in range(warmup):
@@ -576,7 +584,9 @@ def main():
         log(f"{tag}: {steps} steps in {elapsed:.3f}s")
         return elapsed
 
+    graph_info = {}
     elapsed = run(args.amp, args.steps, args.warmup, "timed", graph=use_graph)
+    use_graph = use_graph and "fallback" not in graph_info
     peaks = None
     if world == 1 and not args.no_peaks:
         peaks = measure_peaks(device)
@@ -662,6 +672,8 @@ def main():
         if args.config in (4, 5):
             line.update(head_config_line(args, world, value, knobs))
         line["config"]["graph_replay"] = use_graph
+        if graph_info:
+            line["config"]["graph"] = dict(graph_info, packet_capture=os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE"))
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

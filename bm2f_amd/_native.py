@@ -66,6 +66,8 @@ _SIGNATURES = {
     "m2f_set_option": [ctypes.c_char_p, _l],
     "m2f_get_option": [ctypes.c_char_p, _p],
     "m2f_transpose_f32": [_p, _l, _l, _p, _l, _l, _i, _i, _i, _p],
+    "m2f_colsum_workspace": [_l, _i, _p],
+    "m2f_colsum": [_i, _p, _l, _i, _p, _l, _p, _p],
     "m2f_group_norm_workspace": [_i, _i, _i, _l, _p],
     "m2f_group_norm_fwd_f32": [_p, _p, _p, _i, _i, _i, _l, _f, _i, _p, _p, _p, _p, _l, _p],
     "m2f_group_norm_bwd_f32": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _l, _i, _p, _p, _p, _p, _l, _p],

@@ -419,6 +419,31 @@ def train_step(model, opt, images, amp_dtype=torch.bfloat16, clip=0.01, scaler=N
     return loss.detach()
 
 
+_NODE_TYPES = {0: "kernel", 1: "memcpy", 2: "memset", 3: "host", 4: "graph", 5: "empty", 6: "wait_event",
+               7: "event_record", 10: "mem_alloc", 11: "mem_free"}
+
+
+def graph_node_counts(graph):
+    """Node kinds of a captured torch.cuda.CUDAGraph (kept with keep_graph=True), through the HIP runtime's
+    hipGraphGetNodes / hipGraphNodeGetType."""
+    hip = ctypes.CDLL("libamdhip64.so")
+    g = ctypes.c_void_p(graph.raw_cuda_graph())
+    n = ctypes.c_size_t(0)
+    if hip.hipGraphGetNodes(g, None, ctypes.byref(n)) != 0:
+        raise RuntimeError("hipGraphGetNodes failed")
+    nodes = (ctypes.c_void_p * n.value)()
+    if hip.hipGraphGetNodes(g, nodes, ctypes.byref(n)) != 0:
+        raise RuntimeError("hipGraphGetNodes failed")
+    counts = {}
+    t = ctypes.c_int(0)
+    for i in range(n.value):
+        if hip.hipGraphNodeGetType(ctypes.c_void_p(nodes[i]), ctypes.byref(t)) != 0:
+            raise RuntimeError("hipGraphNodeGetType failed")
+        k = _NODE_TYPES.get(t.value, str(t.value))
+        counts[k] = counts.get(k, 0) + 1
+    return counts
+
+
 class GraphStep:
     """The whole training step -- forward, loss, backward, GradScaler unscale / inf check, gradient clipping and
     the fused AdamW (capturable: its step counter lives on the device) -- captured once as a HIP graph
@@ -430,22 +455,30 @@ class GraphStep:
     eagerly on a side stream first (lazy state, MIOpen find-db, workspaces), as torch's whole-network capture
     recipe prescribes."""
 
-    def __init__(self, model, opt, images, amp_dtype, scaler=None, warmup=3, debug_dump=None):
+    def __init__(self, model, opt, images, amp_dtype, scaler=None, warmup=3, debug_dump=None, sdpa_math=False):
+        from torch.nn.attention import SDPBackend, sdpa_kernel
+        import contextlib
         self.model, self.opt, self.images, self.amp, self.scaler = model, opt, images, amp_dtype, scaler
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            for _ in range(warmup):
-                train_step(model, opt, images, amp_dtype, scaler=scaler)
-        torch.cuda.current_stream().wait_stream(side)
-        torch.cuda.synchronize()
-        self.graph = torch.cuda.CUDAGraph()
-        if debug_dump:
-            self.graph.enable_debug_mode()
-        with torch.cuda.graph(self.graph):
-            self.loss = train_step(model, opt, images, amp_dtype, scaler=scaler)
+        # sdpa_math: the decoder's self-attention on the math backend (bitwise-repeatable; tests)
+        ctx = sdpa_kernel([SDPBackend.MATH]) if sdpa_math else contextlib.nullcontext()
+        with ctx:
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(warmup):
+                    train_step(model, opt, images, amp_dtype, scaler=scaler)
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            self.graph = torch.cuda.CUDAGraph(keep_graph=True)
+            if debug_dump:
+                self.graph.enable_debug_mode()
+            with torch.cuda.graph(self.graph):
+                self.loss = train_step(model, opt, images, amp_dtype, scaler=scaler)
         if debug_dump:   # the captured graph as a dot file (node types and kernel names; diagnostics)
             self.graph.debug_dump(debug_dump)
+        # node kinds (kernel / memcpy / memset ...): a memset node replays wrongly under the runtime's packet capture
+        self.nodes = graph_node_counts(self.graph)
+        self.graph.instantiate()
 
     def __call__(self):
         self.graph.replay()

@@ -360,6 +360,75 @@ extern "C" int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, 
 }
 
 // ---------------------------------------------------------------------------------------------------
+// Column sums in fp32 of a row-major (rows, cols) matrix: out[c] = sum_r src[r][c] -- the bias / broadcast-add
+// gradients over the decoder's memory tokens and the level embeddings.  Row chunks write fp32 partials, then one
+// thread per column adds them in chunk order: the same result every call, and no memset (torch's reduction of a
+// long column to few outputs zeroes cross-block semaphores with one, which the runtime's graph packet capture
+// replays wrongly).
+namespace {
+
+constexpr int kColsumRows = 256;   // rows per chunk (at most 1024 chunks)
+
+int64_t colsum_chunks(int64_t rows) {
+  int64_t n = (rows + kColsumRows - 1) / kColsumRows;
+  return std::max<int64_t>(1, std::min<int64_t>(n, 1024));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ src, int64_t rows, int cols,
+                                                          int64_t rows_per, float* __restrict__ part) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int64_t r0 = blockIdx.y * rows_per, r1 = std::min<int64_t>(rows, r0 + rows_per);
+  float s = 0.f;
+  if (c < cols)
+    for (int64_t r = r0 + w; r < r1; r += 4) s += static_cast<float>(src[r * cols + c]);
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < cols) part[blockIdx.y * static_cast<int64_t>(cols) + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+}
+
+__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ part, int chunks, int cols,
+                                                           float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < chunks; ++k) s += part[static_cast<int64_t>(k) * cols + c];
+  out[c] = s;
+}
+
+}  // namespace
+
+extern "C" int m2f_colsum_workspace(int64_t rows, int cols, int64_t* workspace_floats) {
+  if (rows < 0 || cols <= 0 || !workspace_floats) return m2f::fail(M2F_EINVAL, "m2f_colsum_workspace: bad arguments");
+  *workspace_floats = colsum_chunks(rows) * cols;
+  return m2f::ok();
+}
+
+extern "C" int m2f_colsum(int dtype, const void* src, int64_t rows, int cols, float* workspace,
+                          int64_t workspace_floats, float* out, void* stream) {
+  const char* fn = "m2f_colsum";
+  if (!src || !workspace || !out || rows < 0 || cols <= 0) return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  const int64_t chunks = colsum_chunks(rows);
+  if (workspace_floats < chunks * cols)
+    return m2f::fail(M2F_EINVAL, "%s: workspace %lld < %lld floats", fn, static_cast<long long>(workspace_floats),
+                     static_cast<long long>(chunks * cols));
+  if (cols > 65535 * 64) return m2f::fail(M2F_EUNSUPPORTED, "%s: %d columns", fn, cols);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int64_t rows_per = std::max<int64_t>(1, (rows + chunks - 1) / chunks);
+  const dim3 grid((cols + 63) / 64, static_cast<unsigned>(chunks));
+  switch (dtype) {
+    case M2F_F32: colsum_part_kernel<float><<<grid, 256, 0, st>>>(static_cast<const float*>(src), rows, cols, rows_per, workspace); break;
+    case M2F_F16: colsum_part_kernel<_Float16><<<grid, 256, 0, st>>>(static_cast<const _Float16*>(src), rows, cols, rows_per, workspace); break;
+    case M2F_BF16: colsum_part_kernel<__bf16><<<grid, 256, 0, st>>>(static_cast<const __bf16*>(src), rows, cols, rows_per, workspace); break;
+    default: return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  }
+  colsum_final_kernel<<<(cols + 255) / 256, 256, 0, st>>>(workspace, static_cast<int>(chunks), cols, out);
+  return m2f::check_launch(fn);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // Achievable-HBM probe ("measure achievable peaks with a stream kernel"): out = in over
 // n16 16-byte vectors.  mode 0: one pass, each thread copies 4 vectors a block-width apart (plain loads and
 // stores, ~n16 / 1024 workgroups); mode 1: a fixed grid of 8 workgroups per CU striding over the buffer with

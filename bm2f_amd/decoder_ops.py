@@ -404,17 +404,76 @@ def image_mask_fold(mask_features, mask_features_lp=None):
 
 
 def colsum_f32(g2):
-    """``g2.sum(0, dtype=float32)`` for a long (R, C) matrix as two reductions with many outputs each (1024-row
-    blocks, then the block sums): torch reduces a long column to few outputs across workgroups with semaphores it
-    zeroes by a memset, which a HIP graph replay on this ROCm does not re-run correctly (bench_model.GraphStep)."""
+    """``g2.sum(0, dtype=float32)`` of a (R, C) matrix on the library's column-sum kernel (m2f_colsum: 256-row
+    fp32 partials added in a fixed order): torch reduces a long column to few outputs across workgroups with
+    semaphores it zeroes by a memset, which the runtime's HIP graph packet capture replays wrongly
+    (bench_model.GraphStep)."""
+    if g2.dim() != 2:
+        raise RuntimeError(f"colsum_f32 needs a matrix, got shape {tuple(g2.shape)}")
+    g2 = g2.contiguous()
     R, C = g2.shape
-    ch = 1024
-    if R <= ch:
-        return g2.sum(0, dtype=torch.float32)
-    pad = (-R) % ch
-    if pad:
-        g2 = torch.cat([g2, g2.new_zeros(pad, C)])
-    return g2.reshape(-1, ch, C).sum(1, dtype=torch.float32).sum(0)
+    out = torch.empty(C, dtype=torch.float32, device=g2.device)
+    if R == 0:
+        return out.zero_()
+    wf = ctypes.c_int64(0)
+    _native.call("m2f_colsum_workspace", R, C, ctypes.byref(wf))
+    ws = torch.empty(wf.value, dtype=torch.float32, device=g2.device)
+    _native.call("m2f_colsum", _code(g2.dtype), g2.data_ptr(), R, C, ws.data_ptr(), wf, out.data_ptr(), _stream(g2))
+    return out
+
+
+class _RowBias(Function):
+    """x + b with b (C,) broadcast over the leading dims of a channels-last x (..., C): the level-embedding adds
+    (mask2former_transformer_decoder.py:376, msdeformattn.py:75).  Same forward (torch's add and its type
+    promotion); d b is the column sum on m2f_colsum instead of autograd's reduction."""
+
+    @staticmethod
+    def forward(ctx, x, b):
+        ctx.meta = (x.dtype, b.dtype, b.shape)
+        return x + b
+
+    @staticmethod
+    def backward(ctx, g):
+        xd, bd, bshape = ctx.meta
+        gb = colsum_f32(g.reshape(-1, g.shape[-1])).to(bd).view(bshape) if ctx.needs_input_grad[1] else None
+        return (g.to(xd) if ctx.needs_input_grad[0] else None), gb
+
+
+class _ChanBias(Function):
+    """x + b[None, :, None] for x (N, C, L) (the video decoder's level-embedding add,
+    video_mask2former_transformer_decoder.py:388): d b sums L in two short stages (64-element pieces, then the
+    pieces: every output of both reductions is one workgroup's, so torch zeroes no semaphore with a memset),
+    then the N rows on m2f_colsum."""
+
+    @staticmethod
+    def forward(ctx, x, b):
+        ctx.meta = (x.dtype, b.dtype, b.shape)
+        return x + b[None, :, None]
+
+    @staticmethod
+    def backward(ctx, g):
+        xd, bd, bshape = ctx.meta
+        gb = None
+        if ctx.needs_input_grad[1]:
+            N, C, L = g.shape
+            k = next((k for k in (64, 32, 16, 8, 4, 2) if L % k == 0), 1)
+            part = g.reshape(N, C, L // k, k).sum(3, dtype=torch.float32).sum(2)
+            gb = colsum_f32(part).to(bd).view(bshape)
+        return (g.to(xd) if ctx.needs_input_grad[0] else None), gb
+
+
+def chan_bias_add(x, b):
+    """x (N, C, L) + b (C,) broadcast over N and L (:class:`_ChanBias`); plain add off the GPU."""
+    if not x.is_cuda or b.dim() != 1 or x.dim() != 3 or x.shape[1] != b.shape[0]:
+        return x + b[None, :, None]
+    return _ChanBias.apply(x, b)
+
+
+def row_bias_add(x, b):
+    """x (..., C) + b (C,), b's gradient through m2f_colsum (:class:`_RowBias`); plain x + b off the GPU."""
+    if not x.is_cuda or b.dim() != 1 or x.shape[-1] != b.shape[0]:
+        return x + b
+    return _RowBias.apply(x, b)
 
 
 class _TokenLinear(Function):

@@ -23,6 +23,7 @@ from torch.nn.init import normal_
 
 from .msda import MSDeformAttn, attach_host_shapes
 from . import conv_ops, linear_ops
+from .decoder_ops import row_bias_add
 from .norm_ops import add_layernorm, group_norm_act
 from .position_encoding import PositionEmbeddingSine
 from .registry import SEM_SEG_HEADS_REGISTRY, Conv2d, ShapeSpec, c2_xavier_fill, configurable, get_norm, register
@@ -185,7 +186,7 @@ class MSDeformAttnTransformerEncoderOnly(nn.Module):
             # copy; the layers broadcast it, and its gradient is (1, S, C) instead of (N, S, C) per layer
             pos_embeds = [p[:1] for p in pos_embeds]
         lvl_pos_embed_flatten = torch.cat(
-            [p.flatten(2).transpose(1, 2) + self.level_embed[lvl].view(1, 1, -1) for lvl, p in enumerate(pos_embeds)],
+            [row_bias_add(p.flatten(2).transpose(1, 2), self.level_embed[lvl]) for lvl, p in enumerate(pos_embeds)],
             1)
         spatial_shapes, level_start_index = self._shapes(host_shapes, src_flatten.device)
         memory = self.encoder(src_flatten, spatial_shapes, level_start_index, None, lvl_pos_embed_flatten, None,

@@ -255,7 +255,7 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
                 p = pe[:1].flatten(2).transpose(1, 2).contiguous().expand(pe.shape[0], -1, -1)
             else:
                 p = pe.flatten(2).transpose(1, 2)
-            s = self.input_proj[i](x[i]).flatten(2).transpose(1, 2) + self.level_embed.weight[i][None, None, :]
+            s = decoder_ops.row_bias_add(self.input_proj[i](x[i]).flatten(2).transpose(1, 2), self.level_embed.weight[i])
             src.append(s)
             pos.append(p)
             key.append(s + p)

@@ -53,7 +53,7 @@ class VideoMultiScaleMaskedTransformerDecoder(MultiScaleMaskedTransformerDecoder
             h, w = x[i].shape[-2:]
             size_list.append((h, w))
             p = self.pe_layer(x[i].view(bs, t, -1, h, w), None).flatten(3)  # (bs, t, c, hw)
-            s = self.input_proj[i](x[i]).flatten(2) + self.level_embed.weight[i][None, :, None]  # (bt, c, hw)
+            s = decoder_ops.chan_bias_add(self.input_proj[i](x[i]).flatten(2), self.level_embed.weight[i])  # (bt, c, hw)
             c = s.shape[1]
             # (bs, t, c, hw) -> (bs, t*hw, c): frame-major keys, as (T*HW, B, C) in the reference
             p = p.permute(0, 1, 3, 2).reshape(bs, t * h * w, c)

@@ -339,6 +339,14 @@ int m2f_gather_probe(const float* table, int rows, int64_t n, float* out, int ou
 int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, float* out, int64_t out_bs, int64_t out_ld,
                       int B, int R, int Q, void* stream);
 
+/* Column sums out[c] = sum_r src[r][c] in fp32 over a row-major (rows, cols) matrix (dtype f32, f16 or bf16):
+ * fp32 partials per 256-row chunk (workspace from m2f_colsum_workspace), added in chunk order, no memset.
+ * The gradients of the decoder's memory-token projection biases (nn.MultiheadAttention in_proj,
+ * mask2former_transformer_decoder.py:103-108) and of the level embeddings (:376, msdeformattn.py:75). */
+int m2f_colsum_workspace(int64_t rows, int cols, int64_t* workspace_floats);
+int m2f_colsum(int dtype, const void* src, int64_t rows, int cols, float* workspace, int64_t workspace_floats,
+               float* out, void* stream);
+
 /* GroupNorm (+ ReLU when relu != 0) over fp32 NCHW x (N, C, H*W = HW), G groups, affine gamma/beta (may
  * be null): the pixel decoder's GN layers (msdeformattn.py:216-219, :269-281; nn.GroupNorm(32, C)
  * semantics, biased variance, eps).  fwd writes y and the per-(n, g) mean / rstd (N*G floats each) the
