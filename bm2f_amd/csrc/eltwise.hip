@@ -361,41 +361,81 @@ extern "C" int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, 
 
 // ---------------------------------------------------------------------------------------------------
 // Column sums in fp32 of a row-major (rows, cols) matrix: out[c] = sum_r src[r][c] -- the bias / broadcast-add
-// gradients over the decoder's memory tokens and the level embeddings.  Row chunks write fp32 partials, then one
-// thread per column adds them in chunk order: the same result every call, and no memset (torch's reduction of a
+// gradients over the decoder's memory tokens and the level embeddings.  1024-row chunks write fp32 partials
+// (16-byte row vectors, row lanes added in order through LDS), then a second kernel adds the chunks in order: the same result every call, and no memset (torch's reduction of a
 // long column to few outputs zeroes cross-block semaphores with one, which the runtime's graph packet capture
 // replays wrongly).
 namespace {
 
-constexpr int kColsumRows = 256;   // rows per chunk (at most 1024 chunks)
+constexpr int kColsumRows = 1024;   // rows per chunk (at most 512 chunks)
 
 int64_t colsum_chunks(int64_t rows) {
   int64_t n = (rows + kColsumRows - 1) / kColsumRows;
-  return std::max<int64_t>(1, std::min<int64_t>(n, 1024));
+  return std::max<int64_t>(1, std::min<int64_t>(n, 512));
 }
 
-template <typename T>
+template <typename T, int V>
+__device__ __forceinline__ void load_cols(const T* p, float (&v)[V]) {
+  if constexpr (V == 8 && sizeof(T) == 2) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    const T* e = reinterpret_cast<const T*>(&u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = static_cast<float>(e[i]);
+  } else if constexpr (V == 8) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (int i = 0; i < V; ++i) v[i] = static_cast<float>(p[i]);
+  }
+}
+
+// block: 64 columns x one chunk of rows; thread: V consecutive columns (V = 8: one 16- or 32-byte vector per row,
+// rows 16-byte aligned) of every (256 V / 64)-th row, then the row lanes are added in order through LDS
+template <typename T, int V>
 __global__ void __launch_bounds__(256) colsum_part_kernel(const T* __restrict__ src, int64_t rows, int cols,
                                                           int64_t rows_per, float* __restrict__ part) {
+  constexpr int TPR = 64 / V, RL = 256 / TPR;   // threads per row, row lanes
+  __shared__ float red[RL][65];
+  const int cg = threadIdx.x % TPR, rl = threadIdx.x / TPR;
+  const int c0 = blockIdx.x * 64 + cg * V;
+  const int64_t r0 = blockIdx.y * rows_per, r1 = std::min<int64_t>(rows, r0 + rows_per);
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = 0.f;
+  if (c0 < cols) {
+    const T* p = src + c0;
+#pragma unroll 4
+    for (int64_t r = r0 + rl; r < r1; r += RL) {
+      float v[V];
+      load_cols<T, V>(p + r * cols, v);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] += v[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) red[rl][cg * V + i] = acc[i];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int c = blockIdx.x * 64 + threadIdx.x;
+    float s = 0.f;
+    for (int k = 0; k < RL; ++k) s += red[k][threadIdx.x];
+    if (c < cols) part[blockIdx.y * static_cast<int64_t>(cols) + c] = s;
+  }
+}
+
+// block: 64 columns; wave w adds chunks w, w + 4, ..., then the four waves in order
+__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ part, int chunks, int cols,
+                                                           float* __restrict__ out) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
-  const int64_t r0 = blockIdx.y * rows_per, r1 = std::min<int64_t>(rows, r0 + rows_per);
   float s = 0.f;
   if (c < cols)
-    for (int64_t r = r0 + w; r < r1; r += 4) s += static_cast<float>(src[r * cols + c]);
+    for (int k = w; k < chunks; k += 4) s += part[static_cast<int64_t>(k) * cols + c];
   red[w][lane] = s;
   __syncthreads();
-  if (w == 0 && c < cols) part[blockIdx.y * static_cast<int64_t>(cols) + c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-}
-
-__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ part, int chunks, int cols,
-                                                           float* __restrict__ out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float s = 0.f;
-  for (int k = 0; k < chunks; ++k) s += part[static_cast<int64_t>(k) * cols + c];
-  out[c] = s;
+  if (w == 0 && c < cols) out[c] = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
 }
 
 }  // namespace
@@ -418,13 +458,20 @@ extern "C" int m2f_colsum(int dtype, const void* src, int64_t rows, int cols, fl
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int64_t rows_per = std::max<int64_t>(1, (rows + chunks - 1) / chunks);
   const dim3 grid((cols + 63) / 64, static_cast<unsigned>(chunks));
+  // 8-column vectors when every row starts 16-byte aligned and cols % 8 == 0, else one column per thread
+  const int esz = dtype == M2F_F32 ? 4 : 2;
+  const bool vec = cols % 8 == 0 && m2f::aligned(src, 16) && (static_cast<int64_t>(cols) * esz) % 16 == 0;
+#define M2F_COLSUM(T)                                                                                                   \
+  (vec ? colsum_part_kernel<T, 8><<<grid, 256, 0, st>>>(static_cast<const T*>(src), rows, cols, rows_per, workspace)   \
+       : colsum_part_kernel<T, 1><<<grid, 256, 0, st>>>(static_cast<const T*>(src), rows, cols, rows_per, workspace))
   switch (dtype) {
-    case M2F_F32: colsum_part_kernel<float><<<grid, 256, 0, st>>>(static_cast<const float*>(src), rows, cols, rows_per, workspace); break;
-    case M2F_F16: colsum_part_kernel<_Float16><<<grid, 256, 0, st>>>(static_cast<const _Float16*>(src), rows, cols, rows_per, workspace); break;
-    case M2F_BF16: colsum_part_kernel<__bf16><<<grid, 256, 0, st>>>(static_cast<const __bf16*>(src), rows, cols, rows_per, workspace); break;
+    case M2F_F32: M2F_COLSUM(float); break;
+    case M2F_F16: M2F_COLSUM(_Float16); break;
+    case M2F_BF16: M2F_COLSUM(__bf16); break;
     default: return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
   }
-  colsum_final_kernel<<<(cols + 255) / 256, 256, 0, st>>>(workspace, static_cast<int>(chunks), cols, out);
+#undef M2F_COLSUM
+  colsum_final_kernel<<<(cols + 63) / 64, 256, 0, st>>>(workspace, static_cast<int>(chunks), cols, out);
   return m2f::check_launch(fn);
 }
 

@@ -404,7 +404,7 @@ def image_mask_fold(mask_features, mask_features_lp=None):
 
 
 def colsum_f32(g2):
-    """``g2.sum(0, dtype=float32)`` of a (R, C) matrix on the library's column-sum kernel (m2f_colsum: 256-row
+    """``g2.sum(0, dtype=float32)`` of a (R, C) matrix on the library's column-sum kernel (m2f_colsum: 1024-row
     fp32 partials added in a fixed order): torch reduces a long column to few outputs across workgroups with
     semaphores it zeroes by a memset, which the runtime's HIP graph packet capture replays wrongly
     (bench_model.GraphStep)."""

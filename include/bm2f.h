@@ -340,7 +340,7 @@ int m2f_transpose_f32(const float* in, int64_t in_bs, int64_t in_ld, float* out,
                       int B, int R, int Q, void* stream);
 
 /* Column sums out[c] = sum_r src[r][c] in fp32 over a row-major (rows, cols) matrix (dtype f32, f16 or bf16):
- * fp32 partials per 256-row chunk (workspace from m2f_colsum_workspace), added in chunk order, no memset.
+ * fp32 partials per 1024-row chunk (workspace from m2f_colsum_workspace), added in chunk order, no memset.
  * The gradients of the decoder's memory-token projection biases (nn.MultiheadAttention in_proj,
  * mask2former_transformer_decoder.py:103-108) and of the level embeddings (:376, msdeformattn.py:75). */
 int m2f_colsum_workspace(int64_t rows, int cols, int64_t* workspace_floats);
