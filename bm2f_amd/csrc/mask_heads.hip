@@ -519,9 +519,9 @@ __global__ void __launch_bounds__(256, 2) mask_df_kernel(DfHeads heads, const T*
       for (int u = 0; u < 32 * 32 / EPP / 64; ++u) {
         const int piece = lane + 64 * u, row = piece / (32 / EPP), ce = (piece % (32 / EPP)) * EPP;
         const int col = 32 * t + ce;
-        if (col < cw)
-          *reinterpret_cast<s8*>(out + static_cast<int64_t>(64 * w + 32 * j + row) * N + col) =
-              *reinterpret_cast<const s8*>(&so[w][row][ce]);
+        if (col < cw)   // nontemporal: the gradient is not read again here (1-2 % in tools/mask_df_bench.py)
+          __builtin_nontemporal_store(*reinterpret_cast<const s8*>(&so[w][row][ce]),
+                                      reinterpret_cast<s8*>(out + static_cast<int64_t>(64 * w + 32 * j + row) * N + col));
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
