@@ -890,10 +890,10 @@ __global__ void __launch_bounds__(256) mattn_dq_reduce_kernel(const float* __res
 // ----------------------------------------------------------------------------------------------
 // Key chunks per (b, head): aim for >= ~1024 workgroups, but no chunk shorter than minblk key blocks (each
 // workgroup stages its queries and writes a partial once: short chunks are all prologue and epilogue).
-int plan_chunks(int B, int H, int Lk, int* chunk_len, int* nchunks, int minblk = 2) {
+int plan_chunks(int B, int H, int Lk, int* chunk_len, int* nchunks, int minblk = 2, int target = 1024) {
   const int BH = B * H;
   const int nblocks = (Lk + 63) / 64;
-  int per = (nblocks * BH + 1023) / 1024;
+  int per = (nblocks * BH + target - 1) / target;
   per = per < minblk ? minblk : per;
   if (per > nblocks) per = nblocks;
   *chunk_len = per * 64;
@@ -901,6 +901,10 @@ int plan_chunks(int B, int H, int Lk, int* chunk_len, int* nchunks, int minblk =
   return 0;
 }
 int fwd_minblk() { return std::max(1, m2f::option(m2f::kOptMattnFwdMinblk, 2)); }
+// forward workgroup target: 512 when there are few (b, head) pairs -- config 4 (B = 2, Q = 200) at Lk = 16,384
+// 0.065 -> 0.050 ms with half the chunks; config 2's 128 pairs keep 1024 (512 cost it 0.117 -> 0.126 ms,
+// profiles/r04_v_mattn_target.txt)
+int fwd_target(int B, int H) { return B * H < 64 ? 512 : 1024; }
 // backward: 4 key blocks per chunk at least (every chunk re-stages Q, dO, LSE, delta and writes a dQ partial): at
 // config 2 / Lk = 1,024 0.143 -> 0.063 ms, config 4 / Lk = 4,096 0.124 -> 0.068 ms, equal at Lk = 16,384
 // (profiles/r04_o_mattn_minblk.txt)
@@ -946,7 +950,7 @@ int mattn_fwd_impl(const char* fn, const void* q, const void* k, const void* v, 
       !m2f::aligned(out, 16))
     return m2f::fail(M2F_EINVAL, "%s: misaligned operand or stride", fn);
   int chunk, nch;
-  plan_chunks(B, H, Lk, &chunk, &nch, fwd_minblk());
+  plan_chunks(B, H, Lk, &chunk, &nch, fwd_minblk(), fwd_target(B, H));
   const size_t need = nch > 1 ? sizeof(float) * static_cast<size_t>(nch) * B * H * Lq * (kD + 2) : 0;
   if (ws_bytes < need || (need && !ws)) return m2f::fail(M2F_EINVAL, "%s: workspace %zu < %zu", fn, ws_bytes, need);
   float* ws_o = ws;
@@ -1048,7 +1052,7 @@ extern "C" int m2f_attn_mask_bits(const void* logits, int dtype, int batch, int 
 extern "C" int m2f_masked_attn_plan(int batch, int num_queries, int num_keys, int num_heads, int* chunk_len,
                                     int* num_chunks, int64_t* fwd_workspace_bytes, int64_t* bwd_workspace_bytes) {
   int cl, nc, clb, ncb;
-  plan_chunks(batch, num_heads, num_keys, &cl, &nc, fwd_minblk());
+  plan_chunks(batch, num_heads, num_keys, &cl, &nc, fwd_minblk(), fwd_target(batch, num_heads));
   plan_chunks(batch, num_heads, num_keys, &clb, &ncb, bwd_minblk());
   if (chunk_len) *chunk_len = cl;
   if (num_chunks) *num_chunks = nc;
