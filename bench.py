@@ -45,6 +45,7 @@ METRIC = "images/sec fwd+bwd, R50 100-query 1024² bs16, at 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_PEAK_TF = 2500.0      # dense bf16/f16 MFMA
 F32_PEAK_TF = 157.3        # f32 MFMA (= f32 vector)
+LDS_B128_PEAK_GBS = 150000.0   # ds_read_b64/b128 with every CU streaming at 2.4 GHz (MI355X_MICROARCH.md §LDS)
 
 
 def log(msg):
@@ -238,9 +239,19 @@ def roofline_entry(fam, k, bound):
             ent["mfma_tflops"] = round(k["flops"] / t / 1e12, 1)
             ent["note"] = MFMA_NOTE[fam]
         if k.get("gather_bytes"):
-            ent["gather_gbs"] = round(k["gather_bytes"] / t / 1e9, 1)
-            ent["gather_note"] = ("corner-row gathers (4 x 128 B per sample) through L1 / L2: the bound that binds "
-                                  "(compare achievable.l2_gather_gbs)")
+            rate = round(k["gather_bytes"] / t / 1e9, 1)
+            if fam == "msda_fwd":   # the LDS-window forward reads its corner rows from LDS (ds_read_b128)
+                ent["lds_gather_gbs"] = rate
+                ent["lds_peak_gbs"] = LDS_B128_PEAK_GBS
+                ent["frac_lds"] = round(rate / LDS_B128_PEAK_GBS, 4)
+                ent["gather_note"] = ("corner rows (4 x 128 B per sample) read from the LDS windows by ds_read_b128, "
+                                      "vs the chip's ds_read_b128 rate (MI355X_MICROARCH.md §LDS); not the binding "
+                                      "limit: the kernel is VALU-issue bound (profiles/r04_pmc_fl1_*)")
+            else:                   # the backward's phase 2 gathers corner rows through L1 / L2
+                ent["gather_gbs"] = rate
+                ent["gather_note"] = ("phase-2 corner-row gathers (4 x 128 B per sample) through L1 / L2, vs the "
+                                      "measured gather probe (achievable.l2_gather_gbs); one of the units the "
+                                      "kernel's phases use in turn, not the single binding limit")
         return ent
     if fam.startswith("x3"):
         ach = 6 * k["flops"] / t / 1e12

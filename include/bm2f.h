@@ -62,11 +62,14 @@ int m2f_abi_version(void);
  *   attn_weight      (N, Lq, M, L, P)
  *   output           (N, Lq, M*D)
  * host_spatial_shapes: optional host copy of spatial_shapes (L*2 int64, may be NULL).  When given
- * and Lq == S (encoder self-attention over the flattened pyramid) the backward groups queries by
- * spatial tile and accumulates grad_value in LDS windows; results agree with the untiled path up to
- * the order of fp32 additions.  That path takes each level's start as the prefix sum of the host
- * shapes: the caller guarantees spatial_shapes == host_spatial_shapes and level_start_index == their
- * prefix sums (the Python layer checks both once per tensor, bm2f_amd/msda.py attach_host_shapes).
+ * and Lq == S (encoder self-attention over the flattened pyramid) the forward reads each level's
+ * touched box from LDS windows (bit-identical to the untiled forward) and the backward groups queries
+ * by spatial tile and accumulates grad_value in LDS windows (results agree with the untiled path up to
+ * the order of fp32 additions).  Both tiled paths take each level's start as the prefix sum of the host
+ * shapes and do NOT read spatial_shapes / level_start_index: the caller guarantees spatial_shapes ==
+ * host_spatial_shapes and level_start_index == their prefix sums (the Python layer checks both once per
+ * tensor, bm2f_amd/msda.py attach_host_shapes / _check_level_starts).  Pass NULL to have the kernels
+ * read the device arrays as they are.
  * ------------------------------------------------------------------------------------------- */
 int m2f_msda_fwd_f32(const float* value, const int64_t* spatial_shapes, const int64_t* level_start_index,
                      const float* sampling_loc, const float* attn_weight,

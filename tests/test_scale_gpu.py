@@ -15,6 +15,7 @@
 * DDP over RCCL (backend "nccl") with the custom autograd nodes, world size 1, against the unwrapped model.
 """
 import contextlib
+import os
 
 import numpy as np
 import pytest
@@ -25,6 +26,7 @@ from oracle import msda_ref
 from oracle.decoder_ref import ref_masked_attention, unpack_bits
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 SHAPES_1024 = [(32, 32), (64, 64), (128, 128)]
 
@@ -441,6 +443,89 @@ def test_config5_video_decoder_full_size_vs_torch_ops(device):
     assert rel(gm0, gm1) < 1e-2
 
 
+def test_pixdec_config2_full_size_vs_reference_math(device):
+    """MSDeformAttnPixelDecoder.forward_features at config 2's per-image shape (R50 channels 256 / 512 / 1024 / 2048
+    at strides 4..32 of a 1024^2 image, N = 2; encoder on the 32^2 / 64^2 / 128^2 pyramid, 6 layers, FFN 1024, FPN
+    to 256^2), forward + backward, on the fp32 HIP path (x3 GEMMs / convs, fused MSDA, add+LN, GroupNorm, FPN
+    upsample-add) against oracle/pixdec_ref.py -- the reference's forward_features (msdeformattn.py:314-358)
+    restated with plain torch ops and ms_deform_attn_core_pytorch, pinned on CPU by pixdec.npz -- run on the GPU in
+    fp64.  Outputs, the four input gradients and every parameter gradient (82 tensors).
+
+    Bars: every tensor within 1e-3 relative in norm (||a - b|| / ||b||) and within 1e-3 of its max (max |a - b| /
+    max |b|), or, for the max-normalised bar, within three times the same distance of the reference math run in fp32
+    (the reference's own fp32 arithmetic) when that is larger: at this size a few hundred ReLU pre-activations and
+    sampling coordinates sit within fp32 rounding of 0 / of a pixel-centre line, so ANY fp32 evaluation flips some
+    of them against fp64, and each flip moves one term of a weight-gradient sum over 43,008 tokens (or of a
+    2304-term conv input-gradient sum) (measured and logged in
+    gpurun_out/pixdec_full_size.log).  Parameters: the reference init plus N(0, 0.02) on the sampling-offset and
+    attention-weight projections, so samples interpolate and the attention is query-dependent."""
+    from module_cases import PIXDEC_SHAPES
+    from oracle import pixdec_ref
+    from bm2f_amd.pixel_decoder import MSDeformAttnPixelDecoder
+    from bm2f_amd.registry import ShapeSpec
+    torch.manual_seed(0)
+    shape = {k: ShapeSpec(channels=c, stride=s) for k, (c, s) in PIXDEC_SHAPES.items()}
+    m = MSDeformAttnPixelDecoder(shape, transformer_dropout=0.0, transformer_nheads=8, transformer_dim_feedforward=1024,
+                                 transformer_enc_layers=6, conv_dim=256, mask_dim=256, norm="GN",
+                                 transformer_in_features=["res3", "res4", "res5"], common_stride=4).to(device).train()
+    gcpu = torch.Generator().manual_seed(21)
+    with torch.no_grad():
+        for lyr in m.transformer.encoder.layers:
+            for lin in (lyr.self_attn.sampling_offsets, lyr.self_attn.attention_weights):
+                lin.weight.add_((torch.randn(lin.weight.shape, generator=gcpu) * 0.02).to(device))
+    g = torch.Generator(device=device).manual_seed(22)
+    feats0 = {k: torch.randn(2, c, 1024 // s, 1024 // s, device=device, generator=g) for k, (c, s) in PIXDEC_SHAPES.items()}
+    # HIP path, fp32
+    feats = {k: v.clone().requires_grad_() for k, v in feats0.items()}
+    mf, o0, ms = m.forward_features(feats)
+    outs = [mf, o0] + list(ms)
+    seeds = [torch.randn(o.shape, device=device, generator=g) for o in outs]
+    torch.autograd.backward(outs, seeds)
+    got = {"out_mask_features": mf, "out_out0": o0, **{f"out_ms{i}": t for i, t in enumerate(ms)}}
+    got.update({f"ingrad_{k}": v.grad for k, v in feats.items()})
+    got.update({f"pgrad_{n}": p.grad for n, p in m.named_parameters()})
+    got = {k: v.detach().double() for k, v in got.items()}
+    del mf, o0, ms, outs, feats
+    m.zero_grad(set_to_none=True)
+
+    def run_ref(dtype):
+        f = {k: v.to(dtype).requires_grad_() for k, v in feats0.items()}
+        P = pixdec_ref.params_like(m, dtype)
+        mf_, o0_, ms_ = pixdec_ref.forward_features(m, P, f, dtype)
+        outs_ = [mf_, o0_] + list(ms_)
+        torch.autograd.backward(outs_, [s.to(dtype) for s in seeds])
+        r = {"out_mask_features": mf_, "out_out0": o0_, **{f"out_ms{i}": t for i, t in enumerate(ms_)}}
+        r.update({f"ingrad_{k}": v.grad for k, v in f.items()})
+        r.update({f"pgrad_{n}": p.grad for n, p in P.items()})
+        return {k: v.detach().double() for k, v in r.items()}
+
+    want = run_ref(torch.float64)
+    ref32 = run_ref(torch.float32)
+    assert set(got) == set(want) and len(got) == 5 + 4 + len(list(m.parameters()))
+
+    def errs(a, b):
+        return ((a - b).abs().max() / b.abs().max().clamp_min(1e-300)).item(), \
+               ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+    lines, bad = [], []
+    for k in sorted(want):
+        assert got[k].shape == want[k].shape, k
+        e_max, e_norm = errs(got[k], want[k])
+        r_max, r_norm = errs(ref32[k], want[k])
+        bar = max(1e-3, 3 * r_max)
+        ok = e_norm < 1e-3 and e_max < bar
+        lines.append(f"{k:70s} hip max {e_max:.2e} norm {e_norm:.2e} | ref-fp32 max {r_max:.2e} norm {r_norm:.2e}"
+                     f" | bar {bar:.1e} {'ok' if ok else 'FAIL'}")
+        if not ok:
+            bad.append(k)
+    n_tight = sum(1 for k in want if errs(got[k], want[k])[0] < 1e-3)
+    lines.append(f"{len(want)} tensors; {n_tight} within 1e-3 of their max; failures: {bad}")
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "pixdec_full_size.log"), "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+    assert not bad, "\n".join(ln for ln in lines if "FAIL" in ln)
+
+
 def test_config4_decoder_full_size_vs_torch_ops(device):
     """The image decoder at config 4's full per-rank size (2 images, Q=200, K=80, mask features 256x256, pyramid
     32^2 / 64^2 / 128^2) in fp32 on the HIP ops against the same module on the torch restatements of the decoder
@@ -596,6 +681,26 @@ def test_op_level_forward_lds_bitwise_vs_quad(device, regime):
     ref_out = msda_ref.msda_forward(value.double(), stc, torch.tensor([0, 1024, 5120]), loc.float().double(),
                                     attn.float().double())
     _close(got.cpu(), ref_out)
+
+
+@pytest.mark.parametrize("swin,frames,amp", [("swin_l", 0, "fp16"), ("swin_t", 2, "bf16")])
+def test_graph_step_packet_capture(device, swin, frames, amp):
+    """The graph-vs-eager check with the runtime's graph packet capture ON, as bench.py's graph runs of configs 4 / 5
+    use it: DEBUG_CLR_GRAPH_PACKET_CAPTURE is read once when HIP initialises, so the check runs in a fresh child
+    process (tests/graph_child.py) with the variable set before any device call; four replays, losses and every
+    parameter bitwise equal to the eager copy.  The child's log goes to gpurun_out/graph_packet_capture_*.log."""
+    import subprocess
+    import sys
+    env = dict(os.environ, DEBUG_CLR_GRAPH_PACKET_CAPTURE="1")
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "graph_child.py"), "--swin", swin, "--frames", str(frames),
+           "--amp", amp, "--replays", "4"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+    log_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(log_dir, exist_ok=True)
+    with open(os.path.join(log_dir, f"graph_packet_capture_{swin}_{amp}.log"), "w") as f:
+        f.write(r.stdout + "\n--- stderr ---\n" + r.stderr[-4000:])
+    assert r.returncode == 0 and "GRAPH_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+    assert "packet capture env: '1'" in r.stdout
 
 
 @pytest.mark.parametrize("swin,frames,amp", [("swin_l", None, torch.float16), ("swin_t", 2, torch.bfloat16)])
