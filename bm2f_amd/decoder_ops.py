@@ -457,10 +457,11 @@ class _ChanBias(Function):
         if ctx.needs_input_grad[1]:
             N, C, L = g.shape
             k = next((k for k in (64, 32, 16, 8, 4, 2) if L % k == 0), 1)
+            gs = g
             if k == 1 and L > 64:   # odd L: zero-pad it to a multiple of 64 so the second stage stays short
-                g = F.pad(g, (0, (-L) % 64))
-                k, L = 64, g.shape[2]
-            part = g.reshape(N, C, L // k, k).sum(3, dtype=torch.float32).sum(2)
+                gs = F.pad(g, (0, (-L) % 64))
+                k, L = 64, gs.shape[2]
+            part = gs.reshape(N, C, L // k, k).sum(3, dtype=torch.float32).sum(2)
             gb = colsum_f32(part).to(bd).view(bshape)
         return (g.to(xd) if ctx.needs_input_grad[0] else None), gb
 

@@ -451,13 +451,16 @@ def test_pixdec_config2_full_size_vs_reference_math(device):
     restated with plain torch ops and ms_deform_attn_core_pytorch, pinned on CPU by pixdec.npz -- run on the GPU in
     fp64.  Outputs, the four input gradients and every parameter gradient (82 tensors).
 
-    Bars: every tensor within 1e-3 relative in norm (||a - b|| / ||b||) and within 1e-3 of its max (max |a - b| /
-    max |b|), or, for the max-normalised bar, within three times the same distance of the reference math run in fp32
-    (the reference's own fp32 arithmetic) when that is larger: at this size a few hundred ReLU pre-activations and
-    sampling coordinates sit within fp32 rounding of 0 / of a pixel-centre line, so ANY fp32 evaluation flips some
-    of them against fp64, and each flip moves one term of a weight-gradient sum over 43,008 tokens (or of a
-    2304-term conv input-gradient sum) (measured and logged in
-    gpurun_out/pixdec_full_size.log).  Parameters: the reference init plus N(0, 0.02) on the sampling-offset and
+    Bars, both metrics (max-normalised max |a - b| / max |b| and in norm ||a - b|| / ||b||): outputs within 1e-5
+    of their max; every tensor within 1e-3, or within twice the distance from fp64 of the same reference math run
+    in fp32 (the reference's own fp32 arithmetic) when that is larger.  At this size the gradients' fp32 noise
+    floor is above 1e-3: the reference math in fp32 is up to 7.9e-3 (max) / 3.1e-3 (norm) from fp64 on the
+    sampling-offset gradients and ~1e-3 on the others (a few hundred ReLU pre-activations and sampling coordinates
+    sit within fp32 rounding of 0 / of a pixel-centre line, so any fp32 evaluation flips some of them against
+    fp64, and the six post-norm layers' backward amplifies rounding), while the HIP path's errors are at or below
+    the reference fp32 ones in both metrics on 92 of the 126 tensors, and above 1e-3 never more than 1.7x them
+    (round-5 measurement, logged in
+    gpurun_out/pixdec_full_size.log, committed as profiles/r05_pixdec_full_size*.txt).  Parameters: the reference init plus N(0, 0.02) on the sampling-offset and
     attention-weight projections, so samples interpolate and the attention is query-dependent."""
     from module_cases import PIXDEC_SHAPES
     from oracle import pixdec_ref
@@ -512,10 +515,12 @@ def test_pixdec_config2_full_size_vs_reference_math(device):
         assert got[k].shape == want[k].shape, k
         e_max, e_norm = errs(got[k], want[k])
         r_max, r_norm = errs(ref32[k], want[k])
-        bar = max(1e-3, 3 * r_max)
-        ok = e_norm < 1e-3 and e_max < bar
+        bar, bar_n = max(1e-3, 2 * r_max), max(1e-3, 2 * r_norm)
+        ok = e_max <= bar and e_norm <= bar_n
+        if k.startswith("out_"):
+            ok = ok and e_max < 1e-5
         lines.append(f"{k:70s} hip max {e_max:.2e} norm {e_norm:.2e} | ref-fp32 max {r_max:.2e} norm {r_norm:.2e}"
-                     f" | bar {bar:.1e} {'ok' if ok else 'FAIL'}")
+                     f" | bars {bar:.1e} / {bar_n:.1e} {'ok' if ok else 'FAIL'}")
         if not ok:
             bad.append(k)
     n_tight = sum(1 for k in want if errs(got[k], want[k])[0] < 1e-3)

@@ -103,26 +103,83 @@ def phases(model, opt, images, amp, scaler, steps):
     return tot
 
 
+MARK = "FillFunctor<short>"   # phase-boundary marker kernels (an int16 fill): nothing else in the step fills int16
+
+
+def marked_step(model, opt, images, amp, scaler, marker):
+    """train_step with an int16 fill launched at each phase boundary (forward: in program order; backward: from
+    tensor hooks, which run as autograd reaches them), so the kernel timeline splits into the phases."""
+    opt.zero_grad(set_to_none=True)
+    marker()
+    with torch.autocast("cuda", dtype=amp):
+        x = (images - model.pixel_mean) / model.pixel_std
+        feats = model.backbone(x)
+        marker()
+        mf, _, ms = model.pixel_decoder.forward_features(feats)
+        marker()
+        out = model.predictor(ms, mf)
+        marker()
+        loss = surrogate_loss(out)
+        marker()
+    def hook(g):
+        marker()   # returns None: the gradient is left as it is
+    mf.register_hook(hook)
+    feats["res5"].register_hook(hook)
+    scaler.scale(loss).backward()
+    marker()
+    scaler.unscale_(opt)
+    torch.nn.utils.clip_grad_norm_(model.parameters(), 0.01, foreach=True)
+    marker()
+    scaler.step(opt)
+    scaler.update()
+    marker()
+
+
+PHASES = ["backbone_fwd", "pixdec_fwd", "decoder_fwd", "loss", "decoder_bwd", "pixdec_bwd", "backbone_bwd",
+          "unscale+clip", "opt+scaler"]
+
+
 def profile(model, opt, images, amp, scaler, steps):
     from torch.profiler import ProfilerActivity, profile as tprof
+    buf = torch.zeros(1, dtype=torch.int16, device=images.device)
     with tprof(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
         for _ in range(steps):
-            train_step(model, opt, images, amp, scaler=scaler)
+            marked_step(model, opt, images, amp, scaler, lambda: buf.fill_(1) and None)
         torch.cuda.synchronize()
     kern = collections.defaultdict(lambda: [0.0, 0])
-    glue = collections.defaultdict(lambda: [0.0, 0, ""])
-    for e in prof.events():
-        for k in getattr(e, "kernels", []):
-            us = k.duration if hasattr(k, "duration") else k.time_range.elapsed_us()
-            kern[k.name][0] += us / 1e3 / steps
-            kern[k.name][1] += 1
-            if family(k.name).startswith("torch glue") or family(k.name).startswith("runtime"):
-                shp = tuple(tuple(s) for s in (e.input_shapes or []) if s)
-                key = (e.name, shp)
-                glue[key][0] += us / 1e3 / steps
-                glue[key][1] += 1
-                glue[key][2] = short(k.name, 80)
-    return kern, glue
+    glue = collections.defaultdict(lambda: [0.0, 0, "", collections.Counter()])
+    from torch.autograd import DeviceType
+    evs = prof.profiler.kineto_results.events()
+    ops = {}   # correlation id -> (cpu op name, input shapes)
+    for e in evs:
+        if e.device_type() == DeviceType.CPU and e.linked_correlation_id() == 0:
+            ops[e.correlation_id()] = (e.name(), tuple(tuple(x) for x in (e.shapes() or []) if x))
+    launches = []   # (gpu start, name, ms, cpu op, shapes)
+    for e in evs:
+        if e.device_type() == DeviceType.CUDA and e.duration_ns() > 0:
+            op, shp = ops.get(e.linked_correlation_id(), ("?", ()))
+            launches.append((e.start_ns(), e.name(), e.duration_ns() / 1e6, op, shp))
+    launches.sort(key=lambda t: t[0])
+    grid = collections.defaultdict(float)   # (phase, family) -> ms per step
+    phase = -1
+    for _, name, ms, op, shp in launches:
+        if MARK in name:
+            phase = (phase + 1) % (len(PHASES) + 1)
+            continue
+        if phase < 0 or phase >= len(PHASES):
+            continue
+        ph = PHASES[phase]
+        fam = family(name)
+        grid[(ph, fam)] += ms / steps
+        kern[name][0] += ms / steps
+        kern[name][1] += 1
+        if fam.startswith("torch glue") or fam.startswith("runtime"):
+            key = (op, shp)
+            glue[key][0] += ms / steps
+            glue[key][1] += 1
+            glue[key][2] = short(name, 80)
+            glue[key][3][ph] += 1
+    return kern, glue, grid
 
 
 def scan_sites(model, opt, images, amp, scaler):
@@ -176,7 +233,7 @@ def main():
     torch.cuda.synchronize()
     ph = phases(model, opt, images, amp, scaler, a.steps)
     print("phases", json.dumps({k: round(v, 2) for k, v in ph.items()}), flush=True)
-    kern, glue = profile(model, opt, images, amp, scaler, a.prof_steps)
+    kern, glue, grid = profile(model, opt, images, amp, scaler, a.prof_steps)
     sites = {} if a.no_sites else scan_sites(model, opt, images, amp, scaler)
     fams = collections.defaultdict(float)
     for n, (ms, _) in kern.items():
@@ -186,14 +243,16 @@ def main():
     res = {"step_ms_events": round(step_ms, 2), "kernel_ms_per_step": round(kern_ms, 2),
            "phases_ms": {k: round(v, 2) for k, v in ph.items()},
            "families_ms": {k: round(v, 2) for k, v in sorted(fams.items(), key=lambda x: -x[1])},
+           "phase_family_ms": {ph: {f: round(v, 3) for (p2, f), v in sorted(grid.items()) if p2 == ph}
+                               for ph in PHASES},
            "kernels": [{"name": short(n, 160), "family": family(n), "ms_per_step": round(ms, 3),
                         "calls_per_step": c / a.prof_steps}
                        for n, (ms, c) in sorted(kern.items(), key=lambda x: -x[1][0])[:80]],
            "glue": []}
-    for (op, shp), (ms, c, kn) in sorted(glue.items(), key=lambda x: -x[1][0])[:60]:
+    for (op, shp), (ms, c, kn, phs) in sorted(glue.items(), key=lambda x: -x[1][0])[:60]:
         st = sites.get((op, shp)) or collections.Counter()
         res["glue"].append({"op": op, "shapes": [list(s) for s in shp], "ms_per_step": round(ms, 3),
-                            "calls_per_step": c / a.prof_steps, "kernel": kn,
+                            "calls_per_step": c / a.prof_steps, "kernel": kn, "phases": dict(phs),
                             "sites": [f"{n}x {s}" for s, n in st.most_common(4)]})
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out + ".json", "w") as f:
@@ -204,10 +263,17 @@ def main():
     lines += [f"| {k} | {v:.2f} |" for k, v in ph.items()]
     lines += ["", "## Kernel families (torch.profiler, ms per step)", "", "| family | ms | share |", "|---|---|---|"]
     lines += [f"| {k} | {v:.2f} | {100 * v / kern_ms:.1f} % |" for k, v in res["families_ms"].items()]
-    lines += ["", "## Torch glue by call site (ms per step)", "", "| ms | calls | op | shapes | site |",
-              "|---|---|---|---|---|"]
+    fl = list(res["families_ms"])
+    abbrev = {f: f.split(" (")[0] for f in fl}
+    lines += ["", "## Phase x family (kernel ms per step)", "",
+              "| phase | " + " | ".join(abbrev[f] for f in fl) + " | total |", "|---" * (len(fl) + 2) + "|"]
+    for ph in PHASES:
+        row = [grid.get((ph, f), 0.0) for f in fl]
+        lines.append(f"| {ph} | " + " | ".join(f"{v:.2f}" for v in row) + f" | {sum(row):.2f} |")
+    lines += ["", "## Torch glue by call site (ms per step)", "", "| ms | calls | phase | op | shapes | site |",
+              "|---|---|---|---|---|---|"]
     for gl in res["glue"][:40]:
-        lines.append(f"| {gl['ms_per_step']:.3f} | {gl['calls_per_step']:g} | {gl['op']} | "
+        lines.append(f"| {gl['ms_per_step']:.3f} | {gl['calls_per_step']:g} | {','.join(gl['phases'])} | {gl['op']} | "
                      f"{' '.join('x'.join(map(str, s)) for s in gl['shapes'][:3])} | {'; '.join(gl['sites'][:2])} |")
     lines += ["", "## Top kernels (ms per step)", "", "| ms | calls | family | kernel |", "|---|---|---|---|"]
     lines += [f"| {k['ms_per_step']:.3f} | {k['calls_per_step']:g} | {k['family'].split(' (')[0]} | "
