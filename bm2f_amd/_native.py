@@ -50,6 +50,7 @@ _SIGNATURES = {
     "m2f_gemm_f32x3_nt": [_p, _l, _p, _l, _i, _p, _i, _p, _l, _p, _l, _i, _i, _i, _p, _l, _p],
     "m2f_gemm_f32x3_nt_add": [_p, _l, _p, _l, _i, _p, _i, _p, _l, _p, _p, _l, _p, _l, _i, _i, _i, _p, _l, _p],
     "m2f_gemm_f32x3_nt_bits": [_p, _l, _p, _l, _i, _p, _i, _p, _p, _l, _p, _l, _i, _i, _i, _p, _l, _p],
+    "m2f_gemm_f32x3_nt_rowadd": [_p, _l, _p, _l, _i, _p, _l, _i, _p, _l, _i, _i, _i, _p, _l, _p],
     "m2f_gemm_f32x3_tn_workspace": [_i, _i, _i, _p],
     "m2f_gemm_f32x3_tn": [_p, _l, _p, _l, _p, _l, _p, _i, _i, _i, _p, _l, _p],
     "m2f_conv_f32x3_workspace": [_i, _i, _i, _i, _i, _i, _p],
@@ -59,6 +60,8 @@ _SIGNATURES = {
     "m2f_relu_bwd_sum": [_p, _i, _p, _p, _l, _i, _p],
     "m2f_upsample2x_add_fwd_f32": [_p, _l, _l, _l, _l, _p, _p, _i, _i, _i, _i, _p],
     "m2f_upsample2x_bwd_f32": [_p, _p, _i, _i, _i, _i, _p],
+    "m2f_upsample2x_add_fwd_nhwc_f32": [_p, _l, _p, _p, _i, _i, _i, _i, _p],
+    "m2f_upsample2x_bwd_nhwc_f32": [_p, _p, _i, _i, _i, _i, _p],
     "m2f_maxpool3s2_fwd": [_p, _p, _p, _l, _i, _i, _i, _p],
     "m2f_maxpool3s2_bwd": [_p, _p, _p, _l, _i, _i, _i, _p],
     "m2f_stream_copy": [_p, _p, _l, _i, _p],

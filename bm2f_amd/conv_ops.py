@@ -169,13 +169,21 @@ class Upsample2xAdd(Function):
     @staticmethod
     def forward(ctx, src, lateral):
         lat = lateral.contiguous()
-        # the strided read of a transposed (N, HW, C) view costs a cache line per lane and tap (2.6 ms at
-        # bs16 128->256); one transposing copy first makes every tap read coalesced (1.0 ms with the copy)
-        src = src.contiguous()
         N, C, h, w = src.shape
         out = torch.empty_like(lat)
-        _native.call("m2f_upsample2x_add_fwd_f32", src.data_ptr(), *(ctypes.c_int64(s) for s in src.stride()),
-                     lat.data_ptr(), out.data_ptr(), N, C, h, w, _stream(lat))
+        ctx.nhwc = _nhwc_view(src) and C % 64 == 0 and w <= 256 and w % 2 == 0
+        if ctx.nhwc:
+            # the encoder's (N, HW, C) map read channel-contiguous and transposed in LDS: no transposing copy, and
+            # the gradient comes back channels-last like the decoder's gradient of the same map (one fast sum)
+            sN = src.stride(0) if N > 1 else h * w * C   # a size-1 batch dimension's stride is arbitrary
+            _native.call("m2f_upsample2x_add_fwd_nhwc_f32", src.data_ptr(), ctypes.c_int64(sN), lat.data_ptr(),
+                         out.data_ptr(), N, C, h, w, _stream(lat))
+        else:
+            # the strided read of a transposed (N, HW, C) view costs a cache line per lane and tap (2.6 ms at
+            # bs16 128->256); one transposing copy first makes every tap read coalesced (1.0 ms with the copy)
+            src = src.contiguous()
+            _native.call("m2f_upsample2x_add_fwd_f32", src.data_ptr(), *(ctypes.c_int64(s) for s in src.stride()),
+                         lat.data_ptr(), out.data_ptr(), N, C, h, w, _stream(lat))
         ctx.src_shape = src.shape
         return out
 
@@ -185,9 +193,22 @@ class Upsample2xAdd(Function):
         N, C, h, w = ctx.src_shape
         gsrc = None
         if ctx.needs_input_grad[0]:
-            gsrc = torch.empty(N, C, h, w, device=g.device, dtype=torch.float32)
-            _native.call("m2f_upsample2x_bwd_f32", g.data_ptr(), gsrc.data_ptr(), N, C, h, w, _stream(g))
+            if ctx.nhwc:
+                gsrc = torch.empty(N, h, w, C, device=g.device, dtype=torch.float32).permute(0, 3, 1, 2)
+                _native.call("m2f_upsample2x_bwd_nhwc_f32", g.data_ptr(), gsrc.data_ptr(), N, C, h, w, _stream(g))
+            else:
+                gsrc = torch.empty(N, C, h, w, device=g.device, dtype=torch.float32)
+                _native.call("m2f_upsample2x_bwd_f32", g.data_ptr(), gsrc.data_ptr(), N, C, h, w, _stream(g))
         return gsrc, (g if ctx.needs_input_grad[1] else None)
+
+
+def _nhwc_view(t):
+    """t (N, C, h, w) is a channels-last view: (h, w, C) contiguous per image, the batch stride a multiple of 4 at
+    least h*w*C (the encoder's level slices of (N, S, C))."""
+    N, C, h, w = t.shape
+    sN = t.stride(0)
+    return (t.stride()[1:] == (1, w * C, C) and (N == 1 or (sN >= h * w * C and sN % 4 == 0))
+            and t.data_ptr() % 16 == 0)
 
 
 def upsample_add(src, lateral):

@@ -105,7 +105,7 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
                                                        const __bf16* __restrict__ Bs, int NP,
                                                        const float* __restrict__ bias,
                                                        const float* __restrict__ mask, int64_t ldm,
-                                                       const float* D1, const float* D2, int64_t ldd,
+                                                       const float* D1, const float* D2, int64_t ldd, int dper,
                                                        uint32_t* bits, float* C, int64_t ldc, int M, int N, int K) {
   constexpr int NT = 64 * NW, BM = 32 * NW, TJ = BN / 32;
   constexpr int PIECES = 3 * BN * 2;             // 16-byte pieces of one B chunk
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
         }
         if constexpr ((EPI & kAdd) != 0) {
           // (A.B + bias) + D1 + D2, left to right: the sum autograd would form, one rounding per add
-          v = v + *reinterpret_cast<const f4*>(D1 + static_cast<int64_t>(row) * ldd + col);
+          v = v + *reinterpret_cast<const f4*>(D1 + static_cast<int64_t>(dper ? row % dper : row) * ldd + col);
           if (D2) v = v + *reinterpret_cast<const f4*>(D2 + static_cast<int64_t>(row) * ldd + col);
         }
         *reinterpret_cast<f4*>(C + static_cast<int64_t>(row) * ldc + col) = v;
@@ -275,7 +275,7 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
           float x = v[t];
           if constexpr ((EPI & kMask) != 0) x = mask[static_cast<int64_t>(row) * ldm + col + t] > 0.f ? x : 0.f;
           if constexpr ((EPI & kAdd) != 0) {
-            x += D1[static_cast<int64_t>(row) * ldd + col + t];
+            x += D1[static_cast<int64_t>(dper ? row % dper : row) * ldd + col + t];
             if (D2) x += D2[static_cast<int64_t>(row) * ldd + col + t];
           }
           C[static_cast<int64_t>(row) * ldc + col + t] = x;
@@ -290,17 +290,17 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
 
 template <int BN, int NW>
 int launch_nt(int epi, const float* A, int64_t lda, const __bf16* Bs, int NP, const float* bias, const float* mask,
-              int64_t ldm, const float* D1, const float* D2, int64_t ldd, uint32_t* bits, float* C, int64_t ldc, int M,
-              int N, int K, hipStream_t st) {
+              int64_t ldm, const float* D1, const float* D2, int64_t ldd, int dper, uint32_t* bits, float* C,
+              int64_t ldc, int M, int N, int K, hipStream_t st) {
   constexpr int BM = 32 * NW;
   const int64_t nwg = static_cast<int64_t>((M + BM - 1) / BM) * ((N + BN - 1) / BN);
   if (nwg > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "m2f_gemm_f32x3_nt: too many tiles");
   const dim3 grid(static_cast<unsigned>(nwg)), block(64 * NW);
 #define M2F_X3NT(E)                                                                                            \
   (K % kBK == 0 ? x3_nt_kernel<BN, NW, E, true><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, \
-                                                                       bits, C, ldc, M, N, K)                     \
+                                                                       dper, bits, C, ldc, M, N, K)               \
                 : x3_nt_kernel<BN, NW, E, false><<<grid, block, 0, st>>>(A, lda, Bs, NP, bias, mask, ldm, D1, D2,     \
-                                                                        ldd, bits, C, ldc, M, N, K))
+                                                                        ldd, dper, bits, C, ldc, M, N, K))
   switch (epi) {
     case kNone: M2F_X3NT(kNone); break;
     case kBias: M2F_X3NT(kBias); break;
@@ -623,8 +623,9 @@ namespace {
 int nt_impl(const char* fn, const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* bias,
             int relu, const float* mask, int64_t ldm, const float* D1, const float* D2, int64_t ldd, uint32_t* bits_out,
             const uint32_t* bits_in, int64_t ldbits, float* C, int64_t ldc, int M, int N, int K, void* workspace,
-            int64_t workspace_bytes, void* stream) {
+            int64_t workspace_bytes, void* stream, int dper = 0) {
   if (M < 0 || N <= 0 || K <= 0) return m2f::fail(M2F_EINVAL, "%s: M %d N %d K %d", fn, M, N, K);
+  if (dper < 0 || (dper && !D1)) return m2f::fail(M2F_EINVAL, "%s: row period %d needs D1", fn, dper);
   if (!A || !B || !C) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
   if (K % 4 || lda % 4 || lda < K || ldb < (b_kn ? N : K) || ldc < N || !m2f::aligned(A, 16))
     return m2f::fail(M2F_EINVAL, "%s: K, lda must be multiples of 4 (lda >= K), A 16-byte aligned", fn);
@@ -660,10 +661,10 @@ int nt_impl(const char* fn, const float* A, int64_t lda, const float* B, int64_t
   int cfg = (N % 128 != 0 && N % 96 == 0) ? 1 : 3;
   cfg = m2f::option(m2f::kOptX3NtCfg, cfg);
   switch (cfg) {
-    case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, bits, C, ldc, M, N, K, st);
-    case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, bits, C, ldc, M, N, K, st);
-    case 2: return launch_nt<256, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, bits, C, ldc, M, N, K, st);
-    case 3: return launch_nt<128, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, bits, C, ldc, M, N, K, st);
+    case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
+    case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
+    case 2: return launch_nt<256, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
+    case 3: return launch_nt<128, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
     default: return m2f::fail(M2F_EINVAL, "%s: config %d", fn, cfg);
   }
 }
@@ -683,6 +684,14 @@ extern "C" int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B
                                      void* workspace, int64_t workspace_bytes, void* stream) {
   return nt_impl("m2f_gemm_f32x3_nt_add", A, lda, B, ldb, b_kn, bias, relu, mask, ldm, D1, D2, ldd, nullptr, nullptr,
                  0, C, ldc, M, N, K, workspace, workspace_bytes, stream);
+}
+
+extern "C" int m2f_gemm_f32x3_nt_rowadd(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn,
+                                        const float* R, int64_t ldr, int period, float* C, int64_t ldc, int M, int N,
+                                        int K, void* workspace, int64_t workspace_bytes, void* stream) {
+  if (!R || period <= 0) return m2f::fail(M2F_EINVAL, "m2f_gemm_f32x3_nt_rowadd: R and a positive period needed");
+  return nt_impl("m2f_gemm_f32x3_nt_rowadd", A, lda, B, ldb, b_kn, nullptr, 0, nullptr, 0, R, nullptr, ldr, nullptr,
+                 nullptr, 0, C, ldc, M, N, K, workspace, workspace_bytes, stream, period);
 }
 
 extern "C" int m2f_gemm_f32x3_nt_bits(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn,

@@ -194,6 +194,106 @@ __global__ void __launch_bounds__(256) up2x_bwd2(const float* __restrict__ g, fl
   dst[1] = acc_b;
 }
 
+// ---- channels-last source (the encoder's (N, HW, C) map seen as (N, C, h, w)): both directions LDS-tiled --------
+// A block owns one output row oy (forward) / source row y (backward) of one image and kUpCT channels.  The channel
+// axis is the unit-stride one of the (N, h, w, C) side and the x axis that of the NCHW side, so each side is read
+// or written coalesced and the transpose happens in LDS (pitch kUpCT + 1 floats: the x-strided reads of one
+// channel fall on distinct banks two apart).  Same taps, products and summation order as the NCHW kernels.
+constexpr int kUpCT = 64;
+constexpr int kUpPitch = kUpCT + 1;
+constexpr int kUpMaxW = 256;   // LDS: forward 2 * w * kUpPitch floats, backward w * kUpPitch
+
+__global__ void __launch_bounds__(256) up2x_add_fwd_nhwc(const float* __restrict__ src, int64_t sN,
+                                                         const float* __restrict__ lat, float* __restrict__ out, int C,
+                                                         int h, int w) {
+  extern __shared__ float tile[];   // [2][w][kUpPitch]: source rows i0, i1 of this channel tile
+  const int nct = C / kUpCT, H2 = 2 * h, W2 = 2 * w;
+  const int ct = blockIdx.x % nct;
+  const int r = blockIdx.x / nct;
+  const int oy = r % H2, n = r / H2;
+  const Tap ty = tap2x(oy, h);
+  const int c4n = kUpCT / 4;
+  for (int idx = threadIdx.x; idx < 2 * w * c4n; idx += blockDim.x) {
+    const int sel = idx / (w * c4n), rem = idx - sel * w * c4n;
+    const int x = rem / c4n, c4 = rem - x * c4n;
+    const int iy = sel ? ty.i1 : ty.i0;
+    const f4 v = *reinterpret_cast<const f4*>(src + n * sN + (static_cast<int64_t>(iy) * w + x) * C + ct * kUpCT + 4 * c4);
+    float* d = tile + (sel * w + x) * kUpPitch + 4 * c4;
+    d[0] = v[0]; d[1] = v[1]; d[2] = v[2]; d[3] = v[3];
+  }
+  __syncthreads();
+  const int qv = W2 / 4;
+  for (int it = threadIdx.x; it < kUpCT * qv; it += blockDim.x) {
+    const int c = it / qv, q = it - c * qv, ox0 = 4 * q;
+    const int64_t o = ((static_cast<int64_t>(n) * C + ct * kUpCT + c) * H2 + oy) * W2 + ox0;
+    f4 v = *reinterpret_cast<const f4*>(lat + o);
+    const float* r0 = tile + c;
+    const float* r1 = tile + w * kUpPitch + c;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const Tap tx = tap2x(ox0 + e, w);
+      const float val = ty.l0 * (tx.l0 * r0[tx.i0 * kUpPitch] + tx.l1 * r0[tx.i1 * kUpPitch]) +
+                        ty.l1 * (tx.l0 * r1[tx.i0 * kUpPitch] + tx.l1 * r1[tx.i1 * kUpPitch]);
+      v[e] = v[e] + val;
+    }
+    *reinterpret_cast<f4*>(out + o) = v;
+  }
+}
+
+// grad_src (N, h, w, C) from grad_out (N, C, 2h, 2w): up2x_bwd2's sums per (channel, source pixel pair), staged
+// in LDS and stored channel-contiguous
+__global__ void __launch_bounds__(256) up2x_bwd_nhwc(const float* __restrict__ g, float* __restrict__ gsrc, int C,
+                                                     int h, int w) {
+  extern __shared__ float tile[];   // [w][kUpPitch]
+  const int nct = C / kUpCT, H2 = 2 * h, W2 = 2 * w, wp = w / 2;
+  const int ct = blockIdx.x % nct;
+  const int r = blockIdx.x / nct;
+  const int y = r % h, n = r / h;
+  for (int it = threadIdx.x; it < kUpCT * wp; it += blockDim.x) {
+    const int c = it / wp, k = it - c * wp, x0 = 2 * k;
+    const float* gp = g + (static_cast<int64_t>(n) * C + ct * kUpCT + c) * H2 * W2;
+    float wa[6], wb[6];
+#pragma unroll
+    for (int cc = 0; cc < 6; ++cc) {
+      const int ox = 4 * k - 1 + cc;
+      const bool ok = ox >= 0 && ox < W2;
+      wa[cc] = ok && cc < 4 ? wgt2x(ox, x0, w) : 0.f;
+      wb[cc] = ok && cc >= 2 ? wgt2x(ox, x0 + 1, w) : 0.f;
+    }
+    float acc_a = 0.f, acc_b = 0.f;
+#pragma unroll
+    for (int dy = -1; dy <= 2; ++dy) {
+      const int oy = 2 * y + dy;
+      if (oy < 0 || oy >= H2) continue;
+      const float wy = wgt2x(oy, y, h);
+      if (wy == 0.f) continue;
+      const float* row = gp + static_cast<int64_t>(oy) * W2;
+      const f4 mid = *reinterpret_cast<const f4*>(row + 4 * k);
+      const float v[6] = {4 * k - 1 >= 0 ? row[4 * k - 1] : 0.f, mid[0], mid[1], mid[2], mid[3],
+                          4 * k + 4 < W2 ? row[4 * k + 4] : 0.f};
+      float ra = 0.f, rb = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < 4; ++cc) {
+        const int oxa = 4 * k - 1 + cc, oxb = 4 * k + 1 + cc;
+        if (oxa >= 0 && oxa < W2) ra += wa[cc] * v[cc];
+        if (oxb >= 0 && oxb < W2) rb += wb[cc + 2] * v[cc + 2];
+      }
+      acc_a += wy * ra;
+      acc_b += wy * rb;
+    }
+    tile[x0 * kUpPitch + c] = acc_a;
+    tile[(x0 + 1) * kUpPitch + c] = acc_b;
+  }
+  __syncthreads();
+  const int c4n = kUpCT / 4;
+  for (int idx = threadIdx.x; idx < w * c4n; idx += blockDim.x) {
+    const int x = idx / c4n, c4 = idx - x * c4n;
+    const float* s = tile + x * kUpPitch + 4 * c4;
+    *reinterpret_cast<f4*>(gsrc + ((static_cast<int64_t>(n) * h + y) * w + x) * C + ct * kUpCT + 4 * c4) =
+        f4{s[0], s[1], s[2], s[3]};
+  }
+}
+
 }  // namespace
 
 extern "C" int m2f_upsample2x_add_fwd_f32(const float* src, int64_t sN, int64_t sC, int64_t sY, int64_t sX,
@@ -228,5 +328,43 @@ extern "C" int m2f_upsample2x_bwd_f32(const float* grad_out, float* grad_src, in
     return m2f::check_launch(fn);
   }
   up2x_bwd<<<m2f::ceil_div(n_in, 256), 256, 0, static_cast<hipStream_t>(stream)>>>(grad_out, grad_src, h, w, n_in);
+  return m2f::check_launch(fn);
+}
+
+// channels-last coarse map: src (N, h, w, C) with batch stride sN elements (>= h*w*C; the encoder's (N, S, C) output
+// holds the level as a slice), lateral / out NCHW
+extern "C" int m2f_upsample2x_add_fwd_nhwc_f32(const float* src, int64_t sN, const float* lateral, float* out, int N,
+                                               int C, int h, int w, void* stream) {
+  const char* fn = "m2f_upsample2x_add_fwd_nhwc_f32";
+  if (!src || !lateral || !out) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (N < 0 || C <= 0 || h <= 0 || w <= 0) return m2f::fail(M2F_EINVAL, "%s: bad sizes", fn);
+  if (C % kUpCT || w > kUpMaxW || sN % 4 || sN < static_cast<int64_t>(h) * w * C || !m2f::aligned(src, 16) ||
+      !m2f::aligned(lateral, 16) || !m2f::aligned(out, 16))
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs C %% %d == 0, w <= %d, sN %% 4 == 0, sN >= h*w*C and 16-byte aligned "
+                     "buffers", fn, kUpCT, kUpMaxW);
+  const int64_t nblk = static_cast<int64_t>(N) * 2 * h * (C / kUpCT);
+  if (nblk == 0) return m2f::ok();
+  if (nblk > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many blocks", fn);
+  const size_t lds = static_cast<size_t>(2) * w * kUpPitch * sizeof(float);
+  up2x_add_fwd_nhwc<<<static_cast<unsigned>(nblk), 256, lds, static_cast<hipStream_t>(stream)>>>(src, sN, lateral, out,
+                                                                                                 C, h, w);
+  return m2f::check_launch(fn);
+}
+
+// grad of the coarse map in channels-last layout: grad_src (N, h, w, C) contiguous from grad_out (N, C, 2h, 2w)
+extern "C" int m2f_upsample2x_bwd_nhwc_f32(const float* grad_out, float* grad_src, int N, int C, int h, int w,
+                                           void* stream) {
+  const char* fn = "m2f_upsample2x_bwd_nhwc_f32";
+  if (!grad_out || !grad_src) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
+  if (N < 0 || C <= 0 || h <= 0 || w <= 0) return m2f::fail(M2F_EINVAL, "%s: bad sizes", fn);
+  if (C % kUpCT || w % 2 || w > kUpMaxW || !m2f::aligned(grad_out, 16) || !m2f::aligned(grad_src, 16))
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs C %% %d == 0, even w <= %d and 16-byte aligned buffers", fn, kUpCT,
+                     kUpMaxW);
+  const int64_t nblk = static_cast<int64_t>(N) * h * (C / kUpCT);
+  if (nblk == 0) return m2f::ok();
+  if (nblk > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many blocks", fn);
+  const size_t lds = static_cast<size_t>(w) * kUpPitch * sizeof(float);
+  up2x_bwd_nhwc<<<static_cast<unsigned>(nblk), 256, lds, static_cast<hipStream_t>(stream)>>>(grad_out, grad_src, C, h,
+                                                                                             w);
   return m2f::check_launch(fn);
 }

@@ -548,6 +548,90 @@ class _SavedLike:
         self.needs_input_grad = (n[0], n[2], n[3])
 
 
+class GradSink:
+    """The fp32 gradient of one memory-token tensor that several :func:`token_linear_sink` calls read (the K and V
+    projections of the 3 decoder layers on one level): each call's input gradient -- the autocast-dtype GEMM result,
+    as the reference's per-call cast backward sees it -- is added into one fp32 buffer in one mixed-dtype pass (the
+    first is cast into it), and the call whose backward runs last hands the sum to autograd; the others return no
+    input gradient.  Autograd's path casts every call's gradient to fp32 and adds the fp32 tensors.  One sink per
+    tensor and forward."""
+
+    def __init__(self):
+        self.buf = None
+        self.pending = 0
+
+
+class _TokenLinearSink(Function):
+    """y = x_lp W^T + b (x_lp: the autocast-dtype copy of the fp32 tensor x, or of x + a constant embedding) with
+    x's gradient g W accumulated in the shared :class:`GradSink`: the same per-call terms as the reference's autocast
+    path (an fp16 / bf16 GEMM result each, summed in fp32 over the calls) without a cast and an fp32 add per call."""
+
+    @staticmethod
+    def forward(ctx, x, x_lp, weight, bias, sink):
+        ctx.save_for_backward(x_lp, weight)
+        ctx.has_bias = bias is not None
+        ctx.sink = sink
+        ctx.x_shape = x.shape
+        sink.pending += 1
+        return F.linear(x_lp, weight, bias)
+
+    @staticmethod
+    def backward(ctx, grad):
+        x_lp, w = ctx.saved_tensors
+        sink = ctx.sink
+        gx = None
+        if ctx.needs_input_grad[0]:
+            g2 = grad.reshape(-1, grad.shape[-1])
+            if not g2.is_contiguous():
+                g2 = g2.contiguous()
+            gx_lp = g2 @ w                                   # the autocast-dtype input gradient of this call
+            if sink.buf is None:
+                sink.buf = gx_lp.to(torch.float32)
+            else:
+                torch.add(sink.buf, gx_lp, out=sink.buf)         # fp32 + low precision -> fp32, one pass
+            sink.pending -= 1
+            if sink.pending == 0:
+                gx, sink.buf = sink.buf.view(ctx.x_shape), None
+        sub = _SavedLike(ctx, x_lp, w)
+        sub.needs_input_grad = (False, ctx.needs_input_grad[2], ctx.needs_input_grad[3])
+        _, gw, gb = _TokenLinear.backward(sub, grad)
+        return gx, None, gw, gb, None
+
+
+def token_linear_sink(x, weight, bias, x_lp, sink):
+    """``F.linear`` under autocast for a memory-token projection whose input's low-precision copy ``x_lp`` was made
+    once (:func:`lowp_memory`) and whose fp32 input gradient goes to ``sink`` (:class:`GradSink`).  ``x`` is the
+    fp32 tensor that receives the gradient (for a key ``memory + pos`` with a constant ``pos``: ``memory``)."""
+    dt = x_lp.dtype
+    weight = weight.to(dt)
+    bias = bias.to(dt) if bias is not None else None
+    with torch.autocast("cuda", enabled=False):
+        return _TokenLinearSink.apply(x, x_lp, weight, bias, sink)
+
+
+def lowp_memory(src, pos):
+    """Per decoder level, ``(key_lp, memory_lp, sink)`` for the cross-attention K / V projections under CUDA autocast
+    in fp16 / bf16: memory and memory + pos cast once per forward (the add and the cast in one kernel: the fp32 sum
+    rounded to the autocast dtype, as autocast's cast of the fp32 sum), and one :class:`GradSink` for memory's
+    gradient; None per level elsewhere (the caller then runs the plain per-call path)."""
+    if not src or src[0].device.type != "cuda" or not torch.is_autocast_enabled("cuda"):
+        return [None] * len(src)
+    dt = torch.get_autocast_dtype("cuda")
+    if dt not in (torch.float16, torch.bfloat16) or src[0].dtype != torch.float32:
+        return [None] * len(src)
+    out = []
+    for s, p in zip(src, pos):
+        sd = s.detach()
+        shape = torch.broadcast_shapes(sd.shape, p.shape)
+        # memory's own layout (a transposed view of the NCHW input): the K projection then runs the same GEMM as
+        # on autocast's cast of memory + pos (a contiguous copy runs another kernel, another summation order)
+        k_lp = (torch.empty_like(sd, dtype=dt) if shape == sd.shape
+                else torch.empty(shape, device=sd.device, dtype=dt))
+        torch.add(sd, p.detach(), out=k_lp)
+        out.append((k_lp, sd.to(dt), GradSink()))
+    return out
+
+
 def token_linear(x, weight, bias=None, x_lp=None):
     """``F.linear`` for memory-token projections (autocast applied here as F.linear would).  ``x_lp``: an
     optional detached copy of x in the autocast dtype, made once and shared by several calls."""

@@ -89,6 +89,20 @@ def gemm_nt(a, b, bias=None, relu=False, mask=None, out=None, engine=None, b_kn=
     return out
 
 
+def gemm_nt_rowadd(a, b, r, period):
+    """C = a @ b.T + r[row % period] (x3 engine); a (M, K), b (N, K), r (period, N) fp32 row-major."""
+    M, K = a.shape
+    N = b.shape[0]
+    out = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    wsb = ctypes.c_int64(0)
+    _native.call("m2f_gemm_f32x3_nt_workspace", N, K, ctypes.byref(wsb))
+    ws = torch.empty(max(wsb.value, 16), device=a.device, dtype=torch.uint8)
+    _native.call("m2f_gemm_f32x3_nt_rowadd", a.data_ptr(), _c64(a.stride(0)), b.data_ptr(), _c64(b.stride(0)), 0,
+                 r.data_ptr(), _c64(r.stride(0)), period, out.data_ptr(), _c64(out.stride(0)), M, N, K, ws.data_ptr(),
+                 _c64(ws.numel()), _stream(a))
+    return out
+
+
 def gemm_nt_bits(a, b, bias=None, bits_out=None, bits_in=None, b_kn=False):
     """x3 NT GEMM with the ReLU as a 1-bit mask: ``bits_out`` (M, N/32) int32 -> C = relu(a b^T + bias) and the
     mask of C > 0 written there; ``bits_in`` -> C = (a b^T + bias) where the mask bit is set, else 0."""
@@ -274,19 +288,34 @@ class EncoderInProjF32(Function):
 
     Wq / bq are the sampling-offset and attention-weight projections stacked.  ``src`` has three consumers,
     so autograd would add three (N*S, 256) gradients; here grad_src = grad_value . Wv + grad_proj . Wq +
-    grad_residual leaves the two input-gradient GEMMs with the sums in their epilogues."""
+    grad_residual leaves the two input-gradient GEMMs with the sums in their epilogues.
+
+    A position embedding shared by the batch (pos (1, S, C), the encoder's case) is not added to src: by linearity
+    proj = src Wq^T + R with R = pos Wq^T + bq formed once on the S rows of one image and added row-periodically in
+    the GEMM epilogue (m2f_gemm_f32x3_nt_rowadd), so the (N*S, C) query is never materialised or saved.  The
+    backward then forms d Wq = grad_proj^T src + (sum_n grad_proj[n])^T pos and d pos = (sum_n grad_proj[n]) Wq."""
 
     @staticmethod
     def forward(ctx, src, pos, wv, bv, wq, bq):
         s2 = _rows(src)
         if not s2.is_contiguous():
             s2 = s2.contiguous()
-        # pos may be one (1, S, C) embedding shared by the batch: broadcast here, summed over the batch in
-        # the backward
-        q2 = (s2.view(src.shape) + pos).view(s2.shape) if pos is not None else s2
         value = gemm_nt(s2, wv, bv)
-        proj = gemm_nt(q2, wq, bq)
-        ctx.save_for_backward(s2, q2, wv, wq)
+        S = src.shape[-2] if src.dim() >= 2 else 0
+        ctx.shared_pos = (pos is not None and src.dim() == 3 and pos.dim() == 3 and pos.shape[0] == 1
+                          and pos.shape[1:] == src.shape[1:] and src.shape[0] > 1)
+        if ctx.shared_pos:
+            p2 = pos.reshape(S, pos.shape[-1])
+            if not p2.is_contiguous():
+                p2 = p2.contiguous()
+            r = gemm_nt(p2, wq, bq)                               # pos Wq^T + bq, once per layer (S rows)
+            proj = gemm_nt_rowadd(s2, wq, r, S)
+            ctx.save_for_backward(s2, p2, wv, wq)
+        else:
+            # pos may be one (1, S, C) embedding broadcast over a batch of 1, or a full tensor
+            q2 = (s2.view(src.shape) + pos).view(s2.shape) if pos is not None else s2
+            proj = gemm_nt(q2, wq, bq)
+            ctx.save_for_backward(s2, q2, wv, wq)
         ctx.in_shape = src.shape
         ctx.has_pos = pos is not None
         ctx.pos_shape = pos.shape if pos is not None else None
@@ -302,18 +331,34 @@ class EncoderInProjF32(Function):
         gq = _grad_rows(gproj, torch.empty(s2.shape[0], wq.shape[0], device=s2.device))
         gr = _rows(gpass).contiguous() if gpass is not None else None
         dsrc = dpos = None
-        if ctx.has_pos and nig[1]:
-            dq = gemm_nt(gq, wq, b_kn=True)
-            dpos = dq.view(ctx.in_shape)
-            if ctx.pos_shape != ctx.in_shape:
-                dpos = dpos.sum(0, keepdim=True)
+        dwq = dbq = None
+        if ctx.shared_pos:
+            p2 = q2                                               # the (S, C) embedding
+            N, S = ctx.in_shape[0], ctx.in_shape[1]
+            gqs = gq.view(N, S, -1).sum(0)                        # sum_n grad_proj[n]: (S, 3 M L P)
+            if nig[1]:
+                dpos = gemm_nt(gqs, wq, b_kn=True).view(ctx.pos_shape)
             if nig[0]:
-                dsrc = gemm_nt(gv, wv, b_kn=True, add=(dq, gr)).view(ctx.in_shape)
-        elif nig[0]:
-            t = gemm_nt(gq, wq, b_kn=True, add=(gr,))
-            dsrc = gemm_nt(gv, wv, b_kn=True, add=(t,), out=t).view(ctx.in_shape)
+                t = gemm_nt(gq, wq, b_kn=True, add=(gr,))
+                dsrc = gemm_nt(gv, wv, b_kn=True, add=(t,), out=t).view(ctx.in_shape)
+            if nig[4] or nig[5]:
+                dwq, dbq = gemm_tn(gq, s2, colsum=ctx.biases[1] and nig[5])
+                if nig[4]:
+                    dwq = dwq + gemm_tn(gqs, p2)[0]
+        else:
+            if ctx.has_pos and nig[1]:
+                dq = gemm_nt(gq, wq, b_kn=True)
+                dpos = dq.view(ctx.in_shape)
+                if ctx.pos_shape != ctx.in_shape:
+                    dpos = dpos.sum(0, keepdim=True)
+                if nig[0]:
+                    dsrc = gemm_nt(gv, wv, b_kn=True, add=(dq, gr)).view(ctx.in_shape)
+            elif nig[0]:
+                t = gemm_nt(gq, wq, b_kn=True, add=(gr,))
+                dsrc = gemm_nt(gv, wv, b_kn=True, add=(t,), out=t).view(ctx.in_shape)
+            if nig[4] or nig[5]:
+                dwq, dbq = gemm_tn(gq, q2, colsum=ctx.biases[1] and nig[5])
         dwv, dbv = gemm_tn(gv, s2, colsum=ctx.biases[0] and nig[3]) if (nig[2] or nig[3]) else (None, None)
-        dwq, dbq = gemm_tn(gq, q2, colsum=ctx.biases[1] and nig[5]) if (nig[4] or nig[5]) else (None, None)
         return dsrc, dpos, dwv, dbv, dwq, dbq
 
 

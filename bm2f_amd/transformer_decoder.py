@@ -60,8 +60,11 @@ class SelfAttentionLayer(nn.Module):
         B, L, C = q_in.shape
         H = a.num_heads
         w, b = decoder_ops.lp(a.in_proj_weight), decoder_ops.lp(a.in_proj_bias)
-        qk = F.linear(q_in, w[:2 * C], b[:2 * C])
-        v = F.linear(v_in, w[2 * C:], b[2 * C:])
+        # split, not slices: the in-projection's gradient is then one cat of the pieces (SplitBackward) instead of
+        # a zero-filled full-size tensor per slice, added up
+        (w_qk, w_v), (b_qk, b_v) = w.split([2 * C, C]), (b.split([2 * C, C]) if b is not None else (None, None))
+        qk = F.linear(q_in, w_qk, b_qk)
+        v = F.linear(v_in, w_v, b_v)
         q, k = qk.split(C, dim=-1)
         heads = lambda t: t.view(B, L, H, C // H).transpose(1, 2)  # noqa: E731
         drop = a.dropout if self.training else 0.0
@@ -103,10 +106,19 @@ class CrossAttentionLayer(nn.Module):
             raise NotImplementedError("attention dropout > 0 is not supported by the masked-attention kernel")
         C = query.shape[-1]
         w, b = decoder_ops.lp(a.in_proj_weight), decoder_ops.lp(a.in_proj_bias)
-        q = F.linear(query, w[:C], b[:C])
-        k_lp, v_lp = lowp if lowp is not None else (None, None)
-        k = decoder_ops.token_linear(key, w[C:2 * C], b[C:2 * C], x_lp=k_lp)
-        v = decoder_ops.token_linear(value, w[2 * C:], b[2 * C:], x_lp=v_lp)
+        (w_q, w_k, w_v) = w.split(C)   # one SplitBackward (see SelfAttentionLayer)
+        b_q, b_k, b_v = b.split(C) if b is not None else (None, None, None)
+        q = F.linear(query, w_q, b_q)
+        if lowp is not None and len(lowp) == 3:
+            # (key_lp, memory_lp, sink): both projections' input gradients go to the fp32 memory (value) through the
+            # level's sink (decoder_ops.GradSink); the key's pos is a constant
+            k_lp, v_lp, sink = lowp
+            k = decoder_ops.token_linear_sink(value, w_k, b_k, k_lp, sink)
+            v = decoder_ops.token_linear_sink(value, w_v, b_v, v_lp, sink)
+        else:
+            k_lp, v_lp = lowp if lowp is not None else (None, None)
+            k = decoder_ops.token_linear(key, w_k, b_k, x_lp=k_lp)
+            v = decoder_ops.token_linear(value, w_v, b_v, x_lp=v_lp)
         o = decoder_ops.masked_attention(q, k, v, bits, a.num_heads)
         return decoder_ops.linear(o, a.out_proj)
 
@@ -116,7 +128,10 @@ class CrossAttentionLayer(nn.Module):
         autocast-dtype copies (key, memory) made once per forward for the layers sharing a level."""
         if memory_key_padding_mask is not None:
             raise NotImplementedError("the decoder passes no key padding mask (reference :405)")
-        key = memory_plus_pos if memory_plus_pos is not None else (memory if pos is None else memory + pos)
+        if memory_lowp is not None and len(memory_lowp) == 3:
+            key = None   # the projections read the once-cast memory + pos (decoder_ops.lowp_memory)
+        else:
+            key = memory_plus_pos if memory_plus_pos is not None else (memory if pos is None else memory + pos)
         if self.normalize_before:
             t2 = self.norm(tgt)
             q = t2 if query_pos is None else t2 + query_pos
@@ -181,6 +196,9 @@ def _migrate_static_query(module, state_dict, prefix, local_metadata):
 @register(transformer_decoder_registry)
 class MultiScaleMaskedTransformerDecoder(nn.Module):
     _version = 2
+    # under CUDA autocast: K / V memory projections on once-cast copies with one fp32 gradient sink per level
+    # (decoder_ops.lowp_memory); False restores the per-level cast copies with autograd's gradient sums
+    sink_memory_grads = True
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys, unexpected_keys,
                               error_msgs):
@@ -245,7 +263,7 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
         }
 
     # -- memory / positional inputs: (B, HW_l, C) per level, mem + pos precomputed once --------------
-    def _levels(self, x):
+    def _levels(self, x, with_key=True):
         src, pos, key, size_list = [], [], [], []
         for i in range(self.num_feature_levels):
             size_list.append(tuple(x[i].shape[-2:]))
@@ -258,7 +276,7 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
             s = decoder_ops.row_bias_add(self.input_proj[i](x[i]).flatten(2).transpose(1, 2), self.level_embed.weight[i])
             src.append(s)
             pos.append(p)
-            key.append(s + p)
+            key.append(s + p if with_key else None)
         return src, pos, key, size_list
 
     @staticmethod
@@ -291,8 +309,18 @@ class MultiScaleMaskedTransformerDecoder(nn.Module):
     def _forward(self, x, mask_features, mask=None):
         assert len(x) == self.num_feature_levels
         del mask
-        src, pos, key, size_list = self._levels(x)
-        lowp = self._lowp_levels(src, key)
+        lowp = None
+        if self.sink_memory_grads and x[0].device.type == "cuda" and torch.is_autocast_enabled("cuda"):
+            # K / V projections on once-cast memory (and memory + pos) whose fp32 gradients collect in one sink per
+            # level (decoder_ops.lowp_memory): the fp32 memory + pos itself is then never formed
+            src, pos, key, size_list = self._levels(x, with_key=False)
+            lowp = decoder_ops.lowp_memory(src, pos)
+            if any(lv is None for lv in lowp):
+                key, lowp = [s + p for s, p in zip(src, pos)], None
+        else:
+            src, pos, key, size_list = self._levels(x)
+        if lowp is None:
+            lowp = self._lowp_levels(src, key)
         bs = src[0].shape[0]
         query_embed = self.query_embed.weight.unsqueeze(0).expand(bs, -1, -1)
         output = self.query_feat.weight.unsqueeze(0).repeat(bs, 1, 1)

@@ -260,6 +260,13 @@ int m2f_gemm_f32x3_nt_add(const float* A, int64_t lda, const float* B, int64_t l
                           int relu, const float* mask, int64_t ldm, const float* D1, const float* D2, int64_t ldd,
                           float* C, int64_t ldc, int M, int N, int K, void* workspace, int64_t workspace_bytes,
                           void* stream);
+/* m2f_gemm_f32x3_nt_rowadd: C = A.B^T + R[m % period] -- a row-periodic addend (R [period][N], row stride ldr).  The
+ *   encoder's query projection (src + pos) Wq^T + bq (ms_deform_attn.py:97-103 with msdeformattn.py:115) for a
+ *   position embedding shared by the batch: R = pos Wq^T + bq is formed once per layer on the S rows of one image,
+ *   so the (N*S, C) sum src + pos is never materialised.  Same constraints as the addends of _nt_add. */
+int m2f_gemm_f32x3_nt_rowadd(const float* A, int64_t lda, const float* B, int64_t ldb, int b_kn, const float* R,
+                             int64_t ldr, int period, float* C, int64_t ldc, int M, int N, int K, void* workspace,
+                             int64_t workspace_bytes, void* stream);
 /* m2f_gemm_f32x3_nt_bits: the FFN's ReLU as a 1-bit mask (msdeformattn.py:101-106).  With bits_out (relu != 0):
  *   C = relu(A.B^T + bias) and bits_out[m][n / 32] bit n % 32 = (C[m][n] > 0).  With bits_in (relu == 0):
  *   C = (A.B^T + bias) where the bit is set, else 0 -- the ReLU backward of grad_h = grad_y . W2 read from
@@ -375,6 +382,14 @@ int m2f_group_norm_bwd_f32(const float* dy, const float* x, const float* mean, c
 int m2f_upsample2x_add_fwd_f32(const float* src, int64_t sN, int64_t sC, int64_t sY, int64_t sX, const float* lateral,
                                float* out, int N, int C, int h, int w, void* stream);
 int m2f_upsample2x_bwd_f32(const float* grad_out, float* grad_src, int N, int C, int h, int w, void* stream);
+/* Channels-last coarse map (the encoder's (N, HW, C) output seen as (N, C, h, w); msdeformattn.py:335-349): src is
+ * (N, h, w, C) with batch stride sN elements (sN >= h*w*C, a multiple of 4: the level's slice of the (N, S, C) encoder
+ * output), grad_src (N, h, w, C) contiguous, lateral / out / grad_out NCHW; C % 64 == 0, w <= 256 (bwd: w even); same
+ * taps, products and summation order as the NCHW pair above.  Replace the transposing copy before the forward and the
+ * mixed-layout gradient sum after the backward. */
+int m2f_upsample2x_add_fwd_nhwc_f32(const float* src, int64_t sN, const float* lateral, float* out, int N, int C, int h,
+                                    int w, void* stream);
+int m2f_upsample2x_bwd_nhwc_f32(const float* grad_out, float* grad_src, int N, int C, int h, int w, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Weak-supervision criterion (SUP_TYPE "mask_projection_and_pairwise"), SURVEY 8(f) ranks 1 and 3.

@@ -51,14 +51,16 @@ def test_conv_x3_fallback_shapes(device):
 
 
 @pytest.mark.parametrize("N,C,h,w,transposed", [(2, 256, 16, 16, True), (1, 8, 5, 6, False), (3, 4, 1, 2, True),
-                                                (2, 16, 7, 10, False)])
+                                                (2, 16, 7, 10, False), (2, 128, 13, 6, True), (1, 64, 3, 256, True),
+                                                (1, 64, 2, 7, True)])
 def test_upsample2x_add_vs_fp64(device, N, C, h, w, transposed):
     """conv_ops.upsample_add (csrc/upsample.hip) = lateral + F.interpolate(bilinear, align_corners=False) at
-    2x, forward and both gradients, against fp64 torch; the coarse map as the encoder's transposed view."""
+    2x, forward and both gradients, against fp64 torch; the coarse map as the encoder's transposed view (C % 64 == 0
+    and even w <= 256: the channels-last LDS-tiled kernels, gradient returned channels-last)."""
     torch.manual_seed(N * 100 + h)
-    if transposed:
-        z = torch.randn(N, h * w, C, device=device, requires_grad=True)
-        src = z.transpose(1, 2).view(N, C, h, w)
+    if transposed:   # the last level of the encoder's (N, S, C) output, as forward_features slices it
+        z = torch.randn(N, h * w + 5 * 4, C, device=device, requires_grad=True)
+        src = z[:, 20:].transpose(1, 2).view(N, C, h, w)
     else:
         z = torch.randn(N, C, h, w, device=device, requires_grad=True)
         src = z
@@ -67,7 +69,7 @@ def test_upsample2x_add_vs_fp64(device, N, C, h, w, transposed):
     g = torch.randn_like(y)
     y.backward(g)
     zd = z.detach().double().requires_grad_()
-    srcd = zd.transpose(1, 2).reshape(N, C, h, w) if transposed else zd
+    srcd = zd[:, 20:].transpose(1, 2).reshape(N, C, h, w) if transposed else zd
     latd = lat.detach().double().requires_grad_()
     yd = latd + F.interpolate(srcd, size=(2 * h, 2 * w), mode="bilinear", align_corners=False)
     yd.backward(g.double())
@@ -75,6 +77,10 @@ def test_upsample2x_add_vs_fp64(device, N, C, h, w, transposed):
     assert _rel(y, yd) < 1e-6
     assert _rel(z.grad, zd.grad) < 1e-6
     assert torch.equal(lat.grad, g)
+    if transposed and C % 64 == 0 and w % 2 == 0 and w <= 256:   # the channels-last pair: its own layout both ways
+        assert conv_ops._nhwc_view(src)
+        y2 = conv_ops.upsample_add(src.detach().contiguous(), lat.detach())   # NCHW kernels on the same values
+        torch.testing.assert_close(y, y2, rtol=1e-6, atol=1e-6)
     # the library's fp32 result for the same inputs (its NHWC path for the transposed view)
     torch.testing.assert_close(y, lat + F.interpolate(src, size=(2 * h, 2 * w), mode="bilinear",
                                                       align_corners=False), rtol=1e-6, atol=1e-6)

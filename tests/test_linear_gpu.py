@@ -162,7 +162,10 @@ def test_gemm_nt_addends_vs_fp64(device, M, N, K, n_add, bias, alias):
 def test_encoder_layer_residual_fused_matches_autograd_sums(device, pos_batch):
     """The encoder layer with residual gradients summed in GEMM epilogues (EncoderInProjF32 /
     FFNResidualF32) against the same layer with plain autograd sums: outputs equal, gradients to fp32
-    rounding of the reordered sums."""
+    rounding of the reordered sums.  A batch-shared embedding (pos_batch 1) is folded into the query projection by
+    linearity (src Wq^T + (pos Wq^T + bq), m2f_gemm_f32x3_nt_rowadd), a different fp32 rounding of the same sum:
+    outputs within 1e-5, gradients 1e-3 (measured 1.8e-4: a reordered rounding of a sampling coordinate moves
+    its d loc term)."""
     from bm2f_amd import pixel_decoder
     from bm2f_amd.msda import attach_host_shapes
 
@@ -191,9 +194,25 @@ def test_encoder_layer_residual_fused_matches_autograd_sums(device, pos_batch):
             res[fused] = [out.detach(), src.grad, pos.grad] + [p.grad.clone() for p in layer.parameters()]
         finally:
             pixel_decoder.RESIDUAL_FUSED = True
-    assert torch.equal(res[True][0], res[False][0])
+    if pos_batch == 2:
+        assert torch.equal(res[True][0], res[False][0])
+    else:
+        assert _rel(res[True][0], res[False][0]) < 1e-5
     for a, b in zip(res[True][1:], res[False][1:]):
-        assert _rel(a, b) < 1e-6
+        assert _rel(a, b) < (1e-6 if pos_batch == 2 else 1e-3)
+
+
+@pytest.mark.parametrize("M,period,N,K", [(2 * 5376, 5376, 288, 256), (3 * 100, 100, 96, 64), (999, 1000, 128, 32)])
+def test_gemm_nt_rowadd_vs_fp64(device, M, period, N, K):
+    """m2f_gemm_f32x3_nt_rowadd: C = A B^T + R[m % period] against fp64."""
+    torch.manual_seed(M)
+    a = torch.randn(M, K, device=device)
+    w = torch.randn(N, K, device=device) / K ** 0.5
+    r = torch.randn(period, N, device=device)
+    out = linear_ops.gemm_nt_rowadd(a, w, r, period)
+    idx = torch.arange(M, device=device) % period
+    ref = a.double() @ w.double().t() + r.double()[idx]
+    assert _rel(out, ref) < 2e-6
 
 
 @pytest.mark.parametrize("M,N,K,b_kn", [(1000, 1024, 256, False), (777, 64, 96, False), (513, 256, 1024, True)])

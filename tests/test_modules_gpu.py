@@ -115,17 +115,20 @@ def test_decoder_teacher_forced_masks_exact(device):
 
 
 def test_decoder_amp_cast_once_matches_per_layer_casts(device, monkeypatch):
-    """Under bf16 autocast the decoder casts each level's memory tokens once per forward
-    (_lowp_levels / token_linear x_lp) instead of in every layer: outputs identical, input gradients equal
-    up to the order of the fp32 gradient sums."""
+    """Under bf16 autocast the decoder casts each level's memory tokens once per forward and collects the K / V
+    projections' input gradients in one fp32 sink per level (decoder_ops.lowp_memory / GradSink; "sink"), or casts
+    once with autograd's sums ("once": _lowp_levels / token_linear x_lp), instead of casting in every layer
+    ("per_layer"): outputs identical, input gradients equal up to the order of the fp32 gradient sums."""
     from bm2f_amd.transformer_decoder import MultiScaleMaskedTransformerDecoder as Dec
     torch.manual_seed(0)
     d = build_decoder().to(device)
     x0 = [torch.randn(2, 256, s, s, device=device) for s in (4, 8, 16)]
     mf0 = torch.randn(2, 256, 32, 32, device=device)
     res = {}
-    for once in (True, False):
-        if not once:
+    for mode in ("sink", "once", "per_layer"):
+        if mode != "sink":
+            monkeypatch.setattr(Dec, "sink_memory_grads", False)
+        if mode == "per_layer":
             monkeypatch.setattr(Dec, "_lowp_levels", staticmethod(lambda src, key: [None] * len(src)))
         x = [t.clone().requires_grad_() for t in x0]
         mf = mf0.clone().requires_grad_()
@@ -134,8 +137,9 @@ def test_decoder_amp_cast_once_matches_per_layer_casts(device, monkeypatch):
             loss = sum(h["pred_masks"].float().square().mean() + h["pred_logits"].float().square().mean()
                        for h in [out] + out["aux_outputs"])
         loss.backward()
-        res[once] = (out["pred_masks"].detach(), [t.grad for t in x], mf.grad)
-    assert torch.equal(res[True][0], res[False][0])
-    for a, b in zip(res[True][1], res[False][1]):
-        assert rel_err(a.cpu(), b.cpu().numpy()) < 1e-5
-    assert rel_err(res[True][2].cpu(), res[False][2].cpu().numpy()) < 1e-5
+        res[mode] = (out["pred_masks"].detach(), [t.grad for t in x], mf.grad)
+    for mode in ("sink", "once"):
+        assert torch.equal(res[mode][0], res["per_layer"][0])
+        for a, b in zip(res[mode][1], res["per_layer"][1]):
+            assert rel_err(a.cpu(), b.cpu().numpy()) < 1e-5
+        assert rel_err(res[mode][2].cpu(), res["per_layer"][2].cpu().numpy()) < 1e-5
