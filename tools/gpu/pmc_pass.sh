@@ -1,7 +1,7 @@
 # One rocprofv3 --pmc pass per counter set over a command, each its own run (gpurun rules: no trace domains beside
 # --pmc, at most 8 SQ / 4 TCC / 2 TA / 2 TD / 2 GRBM counters per pass), summaries per kernel.
 #   PMC_TAG=name PMC_CMD="python3 tools/msda_bench.py --fused --fwd-only --iters 3" bash tools/gpu/pmc_pass.sh SET...
-# SET: issue | wait | lds | ta | fetch | write | mfma
+# SET: issue | wait | lds | ta | fetch | write | mfma | coexec
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd "$R" && mkdir -p gpurun_out && export TMPDIR=/tmp
@@ -13,6 +13,7 @@ declare -A C=(
   [fetch]="FETCH_SIZE GRBM_GUI_ACTIVE"
   [write]="WRITE_SIZE GRBM_GUI_ACTIVE"
   [mfma]="SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_F32 GRBM_GUI_ACTIVE"
+  [coexec]="SQ_VALU_MFMA_BUSY_CYCLES SQ_VALU_MFMA_COEXEC_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_INST_LEVEL_LDS SQ_WAVE_CYCLES GRBM_GUI_ACTIVE"
 )
 for s in "$@"; do
   d="gpurun_out/pmc_${PMC_TAG}_$s"
