@@ -465,8 +465,11 @@ __global__ void __launch_bounds__(256) msda_det_convert_kernel(const long long* 
 // slots of each cell are sorted by sample, so a window row's fp32 partial is summed in a fixed order.  A
 // conversion pass writes grad_value.  Non-finite grad_output falls back to the fp32 atomics (flag set by the scale
 // pass), as the reference's kernel propagates them.
+// Occupancy: four waves per SIMD (<= 128 VGPRs; a 1024-thread workgroup needs that) except for four levels, which
+// run 512-thread workgroups only, at two waves per SIMD (<= 256 VGPRs): the L = 4 body (the reference module's
+// default n_levels, ops/modules/ms_deform_attn.py:35) spilled 3-10 VGPRs at 128.
 template <int LT, bool FUSED, int TPB, bool OVERLAP = true, bool DET = false, bool STAMP = false, bool NOFLUSH = false>
-__global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
+__global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd_f32_tiled(
     const float* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ attn, FrontEnd fe,
     const float* __restrict__ gout, TileGeom geo, int S, int M, float* __restrict__ gvalue,
     float* __restrict__ gloc, float* __restrict__ gattn, unsigned long long* __restrict__ gacc = nullptr,
@@ -929,9 +932,9 @@ __global__ void __launch_bounds__(TPB, 4) msda_bwd_f32_tiled(
           *reinterpret_cast<float2*>(gloc + nq * (3 * M * LP) + (m * LT + l) * P * 2 + 2 * j) =
               ok ? make_float2(px, py) : make_float2(0.f, 0.f);
         } else {
-          const int64_t kl = ((nq * M + m) * LT + l) * P;
-          gattn[kl + j] = ok ? pa : 0.f;
-          *reinterpret_cast<float2*>(gloc + 2 * (kl + j)) =
+          const unsigned kl = ((static_cast<unsigned>(n * S + q) * M + m) * LT + l) * P + j;  // < 2^28 (host)
+          *reinterpret_cast<float*>(reinterpret_cast<char*>(gattn) + kl * 4u) = ok ? pa : 0.f;
+          *reinterpret_cast<float2*>(reinterpret_cast<char*>(gloc) + kl * 8u) =
               ok ? make_float2(W * px, H * py) : make_float2(0.f, 0.f);
         }
         // out-of-window points (rare; flags are per query, so quad-uniform): every lane adds its 8 channels of
@@ -1835,6 +1838,8 @@ int fwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
 bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, size_t& lds, int& threads) {
   if (!host_shapes || d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
   if (static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 >= (int64_t{1} << 31)) return false;  // 32-bit byte offsets
+  // the op-level (unfused) kernels address loc (8 B per sample) and grad_attn / grad_loc in 32 bits
+  if (static_cast<int64_t>(d.N) * d.Lq * d.M * d.L * d.P * 8 >= (int64_t{1} << 31)) return false;
   geo = TileGeom{};
   geo.L = d.L;
   int64_t total = 0;
@@ -1860,7 +1865,8 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   // offsets, where the larger tiles flush fewer window rows per owned row and the halo keeps samples out of the
   // direct atomics (profiles/r04_i*_mb.txt).  The deterministic mode keeps 512 / 12x12 / 8 (2.74 vs 3.55 ms).
   const bool det = m2f::option(m2f::kOptMsdaBwdDet, 0) != 0;
-  const int first = m2f::option(m2f::kOptMsdaThreads, det ? 512 : 1024) >= 1024 ? 1024 : 512;
+  // four levels: 512-thread workgroups only (the L = 4 body needs more than the 128 VGPRs of a 1024-thread one)
+  const int first = d.L == 4 ? 512 : m2f::option(m2f::kOptMsdaThreads, det ? 512 : 1024) >= 1024 ? 1024 : 512;
   geo.ratio23 = std::max(1, m2f::option(m2f::kOptMsdaBwdRatio, 1));
   const TileGeom base = geo;
   // a default 1024-thread geometry whose LDS does not fit (e.g. four levels: 16 samples per query) falls back to
@@ -1933,10 +1939,13 @@ template <int LT, bool FUSED>
 void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
                   const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
                   const DetBufs& det, hipStream_t st) {
-  if (threads == 1024)
-    launch_tiled_t<LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
-  else
-    launch_tiled_t<LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
+  if constexpr (LT < 4) {
+    if (threads == 1024) {
+      launch_tiled_t<LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
+      return;
+    }
+  }
+  launch_tiled_t<LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
 }
 
 template <bool FUSED>

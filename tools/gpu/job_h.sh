@@ -1,0 +1,13 @@
+# x3 A/B: prefetch loads fenced ahead of the chunk MFMAs (-DM2F_X3_SB) vs the default build, alternating rounds
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
+for r in 1 2; do
+  for lib in bm2f_amd/lib/libbm2f.so tools/lib/libbm2f_x3sb_gemm.so; do
+    echo "== round $r gemm $lib" >> gpurun_out/r5h_ab.log
+    timeout -k 10 200 python -u tools/gemm_x3_bench.py --x3-only --cfgs "" --lib $lib >> gpurun_out/r5h_ab.log 2>&1 || exit 1
+  done
+  for lib in bm2f_amd/lib/libbm2f.so tools/lib/libbm2f_x3sb_conv.so; do
+    echo "== round $r conv $lib" >> gpurun_out/r5h_ab.log
+    timeout -k 10 200 python -u tools/conv_bench.py --x3-only --lib $lib >> gpurun_out/r5h_ab.log 2>&1 || exit 1
+  done
+done

@@ -110,6 +110,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=16)
     ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--levels", type=int, default=3, choices=[3, 4],
+                    help="4: add the 1/64 level (the reference module's default n_levels = 4)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--stress", action="store_true")
     ap.add_argument("--no-host-shapes", action="store_true")
@@ -128,7 +130,7 @@ def main():
         k, v_ = kv.split("=")
         _native.set_option(k, int(v_))
     r = a.res
-    shapes = [(r // 32, r // 32), (r // 16, r // 16), (r // 8, r // 8)]
+    shapes = [(r // s, r // s) for s in ((64, 32, 16, 8) if a.levels == 4 else (32, 16, 8))]
     v, st, lsi, loc, attn, gout = make_inputs(a.n, shapes, stress=a.stress, noise=a.noise)
     if a.no_host_shapes:
         delattr(st, "_bm2f_host_shapes")
