@@ -74,6 +74,9 @@ def parse_args(argv=None):
     ap.add_argument("--graph", type=int, default=None, choices=[0, 1],
                     help="capture the step in a HIP graph and replay it (default: on for the per-rank configs 4 / 5 "
                          "at one rank, whose small steps are host-launch bound; off for config 2)")
+    ap.add_argument("--channels-last", type=int, default=1, choices=[0, 1],
+                    help="config 2: run the R50 backbone channels-last (MIOpen NHWC kernels, no layout transposes; default: 156.8 vs "
+                         "158.4 ms per step NCHW on one box, profiles/r05_g_bench_cl*.json)")
     ap.add_argument("--allow-knobs", action="store_true")
     ap.add_argument("--master-port", type=int, default=29531)
     a = ap.parse_args(argv)
@@ -536,7 +539,7 @@ def main():
 
     torch.manual_seed(0)
     if args.config == 2:
-        model = MaskFormerR50(default_cfg(num_queries=args.queries)).to(device)
+        model = MaskFormerR50(default_cfg(num_queries=args.queries), channels_last=bool(args.channels_last)).to(device)
         g = torch.Generator(device=device).manual_seed(1000 + rank)
         images = torch.randn(args.batch, 3, args.res, args.res, device=device, generator=g) * 57.0 + 117.0
     elif args.config == 4:   # 2 images per GPU at 1024^2, Swin-L features
@@ -676,7 +679,8 @@ def main():
                                    + (" with GradScaler" if args.amp == "fp16" else ""),
                        "model": "maskformer2_R50", "global_batch": world * args.batch,
                        "seq_len": sum((args.res // s) ** 2 for s in (32, 16, 8)), "queries": args.queries,
-                       "parallelism": f"dp{world}", "env": knobs},
+                       "parallelism": f"dp{world}", "env": knobs,
+                       "backbone_layout": "channels_last" if args.channels_last else "nchw"},
             "roofline": roof, "roofline_all": roof_all, "achievable": peaks, "modes": modes, "cpu_baseline": cpu,
             "msda_op_dropin": dropin,
         }

@@ -54,7 +54,11 @@ class FrozenBNConv(nn.Module):
     def conv_shift(self, x):
         """(conv(x) with the BN scale folded into the weights, per-channel BN shift)."""
         scale, shift = self._consts()
-        w = _ScaledWeight.apply(self.conv.weight, scale, x.dtype)
+        # a channels-last input gets a channels-last weight copy: MIOpen then runs its NHWC kernels on the tensors
+        # as they are, with no NCHW <-> NHWC transposes around each convolution
+        cl = x.dim() == 4 and x.shape[1] > 1 and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)
+        w = _ScaledWeight.apply(self.conv.weight, scale, x.dtype,
+                                torch.channels_last if cl else torch.contiguous_format)
         return F.conv2d(x, w, None, self.conv.stride, self.conv.padding), shift
 
     def forward(self, x):
@@ -67,8 +71,8 @@ class _ScaledWeight(torch.autograd.Function):
     weight gradient back in fp32 in one pass."""
 
     @staticmethod
-    def forward(ctx, w, scale, dtype):
-        out = torch.empty(w.shape, dtype=dtype, device=w.device)
+    def forward(ctx, w, scale, dtype, fmt=torch.contiguous_format):
+        out = torch.empty(w.shape, dtype=dtype, device=w.device, memory_format=fmt)
         torch.mul(w, scale.view(-1, 1, 1, 1), out=out)
         ctx.save_for_backward(scale)
         return out
@@ -78,7 +82,7 @@ class _ScaledWeight(torch.autograd.Function):
         (scale,) = ctx.saved_tensors
         gw = torch.empty(grad.shape, dtype=torch.float32, device=grad.device)   # the parameter's own layout
         torch.mul(grad, scale.view(-1, 1, 1, 1), out=gw)
-        return gw, None, None
+        return gw, None, None, None
 
 
 class _BiasAct(torch.autograd.Function):
@@ -202,8 +206,9 @@ class Bottleneck(nn.Module):
 
 
 class ResNet50(nn.Module):
-    def __init__(self):
+    def __init__(self, channels_last=False):
         super().__init__()
+        self.channels_last = channels_last   # NHWC activations end to end (MIOpen's NHWC kernels, no transposes)
         self.stem = FrozenBNConv(3, 64, 7, 2, 3)
         cfg = [("res2", 3, 64, 256, 1), ("res3", 4, 128, 512, 2), ("res4", 6, 256, 1024, 2),
                ("res5", 3, 512, 2048, 2)]
@@ -221,6 +226,8 @@ class ResNet50(nn.Module):
         return {k: ShapeSpec(channels=ch[k], stride=st[k]) for k in self.stage_names}
 
     def forward(self, x):
+        if self.channels_last:
+            x = x.contiguous(memory_format=torch.channels_last)
         x = bias_act(*self.stem.conv_shift(x))
         x = max_pool_stem(x)
         out = {}
@@ -263,10 +270,10 @@ class MaskFormerHead(nn.Module):
 
 
 class MaskFormerR50(nn.Module):
-    def __init__(self, cfg=None):
+    def __init__(self, cfg=None, channels_last=False):
         super().__init__()
         cfg = cfg or default_cfg()
-        self.backbone = ResNet50()
+        self.backbone = ResNet50(channels_last)
         self.sem_seg_head = MaskFormerHead(cfg, self.backbone.output_shape())
         self.register_buffer("pixel_mean", torch.tensor(PIXEL_MEAN).view(-1, 1, 1), False)
         self.register_buffer("pixel_std", torch.tensor(PIXEL_STD).view(-1, 1, 1), False)

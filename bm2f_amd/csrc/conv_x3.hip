@@ -174,6 +174,7 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
   {
     auto step = [&](int c, Regs& cur, Regs& nxt) {
       if (c + 2 < nk) gload(cur, c + 2);
+      M2F_X3_PREFETCH_FENCE();
       chunk_mfma(c & 1, fa);
       if (c + 1 < nk) {
         bstore(nxt, (c + 1) & 1);
@@ -357,6 +358,7 @@ __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __re
     __syncthreads();
     auto step = [&](int c, Regs& cur, Regs& nxt) {
       if (c + 2 < nk) gload(cur, c + 2);
+      M2F_X3_PREFETCH_FENCE();
       chunk_mfma(c & 1, fa);
       if (c + 1 < nk) {
         bstore(nxt, c + 1, (c + 1) & 1);

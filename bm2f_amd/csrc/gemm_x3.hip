@@ -203,6 +203,7 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
   __syncthreads();
   auto step = [&](int c, Regs& cur, const Regs& nxt, const bf8 (&fc)[3], bf8 (&fn)[3]) {
     gload(cur, c + 2);
+    M2F_X3_PREFETCH_FENCE();
     chunk_mfma(c & 1, fc);
     bstore(nxt, (c + 1) & 1);
     asplit(nxt, c + 1, fn);
@@ -484,6 +485,7 @@ __global__ void __launch_bounds__(64 * NW, NW >= 8 ? 1 : 2) x3_tn_kernel(const f
     __syncthreads();
     auto step = [&](int c, Regs& cur, const Regs& nxt, const bf8 (&fc)[3], bf8 (&fn)[3]) {
       gload(cur, c + 2);
+      M2F_X3_PREFETCH_FENCE();
       chunk_mfma(c & 1, fc);
       bstore(nxt, c + 1, (c + 1) & 1);
       asplit(nxt, c + 1, fn);

@@ -13,6 +13,14 @@ using bf4 = __bf16 __attribute__((ext_vector_type(4)));
 
 constexpr int kBK = 16;  // k per stage = one 32x32x16 MFMA step
 
+// A/B experiment hook (tools/build_variant.py ... -DM2F_X3_SB): keep a pipeline step's prefetch loads ahead of its
+// MFMAs (the scheduler otherwise sinks them behind the chunk's MFMAs, so the next step waits on them)
+#ifdef M2F_X3_SB
+#define M2F_X3_PREFETCH_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define M2F_X3_PREFETCH_FENCE()
+#endif
+
 __device__ __forceinline__ f16v mfma(bf8 a, bf8 b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }

@@ -29,8 +29,12 @@ def main():
     import argparse
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="", help="shapes whose name contains this")
+    ap.add_argument("--lib", default=None, help="another build of libbm2f.so (A/B)")
     ap.add_argument("--x3-only", action="store_true", help="skip the MIOpen timings (A/B runs)")
     a = ap.parse_args()
+    if a.lib:
+        from bm2f_amd import _native as _nat
+        _nat._LIB_PATH = os.path.abspath(a.lib)
     dev = torch.device("cuda")
     shapes = [("layer_1 3x3", 16, 256, 256, 256, 256, 3, False), ("adapter_1 1x1", 16, 256, 256, 256, 256, 1, False),
               ("mask_features 1x1", 16, 256, 256, 256, 256, 1, True), ("input_proj res3", 16, 512, 256, 128, 128, 1, True),

@@ -30,8 +30,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=16 * 21504)
     ap.add_argument("--cfgs", default="0,2,3", help="x3_nt_cfg option values to time")
+    ap.add_argument("--lib", default=None, help="another build of libbm2f.so (A/B)")
     ap.add_argument("--x3-only", action="store_true", help="time only the x3 engine (A/B runs)")
     a = ap.parse_args()
+    if a.lib:
+        from bm2f_amd import _native as _nat
+        _nat._LIB_PATH = os.path.abspath(a.lib)
     M = a.rows
     dev = torch.device("cuda")
     torch.manual_seed(0)
