@@ -56,6 +56,8 @@ _SIGNATURES = {
     "m2f_conv_f32x3_workspace": [_i, _i, _i, _i, _i, _i, _p],
     "m2f_conv_f32x3": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _l, _p],
     "m2f_conv_f32x3_wgrad": [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _p, _l, _p],
+    "m2f_conv_x3_io": [_p, _i, _i, _p, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _l, _p],
+    "m2f_conv_x3_wgrad_io": [_p, _p, _i, _i, _p, _p, _i, _i, _i, _i, _i, _i, _p, _l, _p],
     "m2f_bias_act_nchw": [_p, _p, _p, _l, _i, _l, _i, _i, _p],
     "m2f_relu_bwd_sum": [_p, _i, _p, _p, _l, _i, _p],
     "m2f_upsample2x_add_fwd_f32": [_p, _l, _l, _l, _l, _p, _p, _i, _i, _i, _i, _p],

@@ -40,17 +40,39 @@ def _ptr(t):
     return t.data_ptr() if t is not None else None
 
 
+_DT = {torch.float32: 0, torch.float16: 1, torch.bfloat16: 2}   # M2F_F32 / M2F_F16 / M2F_BF16
+
+
+def _act16(x):
+    """A 16-bit activation as the 1x1 kernels read it: (tensor, nhwc) -- channels-last kept as it is, anything else
+    made NCHW-contiguous."""
+    if x.is_contiguous(memory_format=torch.channels_last) and not x.is_contiguous():
+        return x, 1
+    return x.contiguous(), 0
+
+
 class Conv2dX3(Function):
+    """fp32 conv on the x3 kernels.  A 16-bit input (the backbone's autocast features feeding a 1x1 conv) is read
+    as it is, NCHW or channels-last, instead of through the reference's ``.float()`` copy (exact: the same
+    results), and its gradient is written back in its dtype and layout (the cast's backward rounding)."""
+
     @staticmethod
     def forward(ctx, x, weight, bias):
-        x = x.contiguous()
         weight = weight.contiguous()
         N, Ci, H, W = x.shape
         Co, k = weight.shape[0], weight.shape[-1]
         out = torch.empty(N, Co, H, W, device=x.device, dtype=torch.float32)
         ws = _workspace(N, Ci, Co, H, W, k, x.device)
-        _native.call("m2f_conv_f32x3", x.data_ptr(), weight.data_ptr(), _ptr(bias), out.data_ptr(), N, Ci, Co, H, W,
-                     k, 0, ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(x))
+        ctx.nhwc = 0
+        if x.dtype == torch.float32:
+            x = x.contiguous()
+            _native.call("m2f_conv_f32x3", x.data_ptr(), weight.data_ptr(), _ptr(bias), out.data_ptr(), N, Ci, Co, H,
+                         W, k, 0, ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(x))
+        else:
+            x, ctx.nhwc = _act16(x)
+            _native.call("m2f_conv_x3_io", x.data_ptr(), _DT[x.dtype], ctx.nhwc, weight.data_ptr(), _ptr(bias),
+                         out.data_ptr(), 0, 0, N, Ci, Co, H, W, k, 0, ws.data_ptr(), ctypes.c_int64(ws.numel()),
+                         _stream(x))
         ctx.save_for_backward(x, weight)
         ctx.has_bias = bias is not None
         return out
@@ -63,11 +85,24 @@ class Conv2dX3(Function):
         Co, k = weight.shape[0], weight.shape[-1]
         ws = _workspace(N, Ci, Co, H, W, k, x.device)
         dx = dw = db = None
+        want_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if x.dtype != torch.float32:   # 16-bit 1x1 input
+            if ctx.needs_input_grad[0]:
+                dx = (torch.empty(N, H, W, Ci, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2) if ctx.nhwc
+                      else torch.empty(N, Ci, H, W, device=x.device, dtype=x.dtype))
+                _native.call("m2f_conv_x3_io", g.data_ptr(), 0, 0, weight.data_ptr(), None, dx.data_ptr(), _DT[x.dtype],
+                             ctx.nhwc, N, Ci, Co, H, W, k, 1, ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(g))
+            if ctx.needs_input_grad[1] or want_b:
+                tck = torch.empty(k * k, Ci, Co, device=x.device, dtype=torch.float32)
+                db = torch.empty(Co, device=x.device, dtype=torch.float32) if want_b else None
+                _native.call("m2f_conv_x3_wgrad_io", g.data_ptr(), x.data_ptr(), _DT[x.dtype], ctx.nhwc, tck.data_ptr(),
+                             _ptr(db), N, Ci, Co, H, W, k, ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(g))
+                dw = tck.permute(2, 1, 0).reshape(Co, Ci, k, k) if ctx.needs_input_grad[1] else None
+            return dx, dw, db
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             _native.call("m2f_conv_f32x3", g.data_ptr(), weight.data_ptr(), None, dx.data_ptr(), N, Ci, Co, H, W, k, 1,
                          ws.data_ptr(), ctypes.c_int64(ws.numel()), _stream(g))
-        want_b = ctx.has_bias and ctx.needs_input_grad[2]
         if k == 3 and WGRAD3 == "tn" and ctx.needs_input_grad[1]:
             dw = _wgrad3_tn(g, x)
             db = g.sum((2, 3)).sum(0) if want_b else None   # two reductions with many outputs (graph-safe)
@@ -127,10 +162,12 @@ def _wgrad3_tn(g, x):
 
 
 def eligible(x, conv) -> bool:
-    """Shapes and settings the x3 conv kernels cover (else F.conv2d)."""
-    if not (x.is_cuda and x.dtype == torch.float32 and conv.weight.dtype == torch.float32 and x.dim() == 4):
+    """Shapes and settings the x3 conv kernels cover (else F.conv2d): fp32 input, or a 16-bit one into a 1x1 conv."""
+    if not (x.is_cuda and x.dtype in _DT and conv.weight.dtype == torch.float32 and x.dim() == 4):
         return False
     k = conv.weight.shape[-1]
+    if x.dtype != torch.float32 and k != 1:
+        return False
     if conv.weight.shape[-2] != k or k not in (1, 3) or conv.groups != 1:
         return False
     if tuple(conv.stride) != (1, 1) or tuple(conv.dilation) != (1, 1) or tuple(conv.padding) != (k // 2, k // 2):

@@ -20,6 +20,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 namespace {
 
 using namespace m2f_x3;
@@ -28,6 +30,63 @@ __device__ __forceinline__ void tap_shift(int T, int tap, int& dy, int& dx) {
   dy = T == 9 ? tap / 3 - 1 : 0;
   dx = T == 9 ? tap % 3 - 1 : 0;
 }
+
+// 16-bit activations (the backbone's autocast features, 1x1 convs only): the reference upcasts them with .float()
+// (msdeformattn.py:320, 336), an exact conversion, so the kernels read them as they are and convert in registers;
+// the input gradient goes back rounded to the feature dtype (round-to-nearest-even, as the cast's backward).
+template <typename TI>
+__device__ __forceinline__ float lo16(unsigned u) {
+  if constexpr (std::is_same<TI, _Float16>::value)
+    return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<unsigned short>(u & 0xffffu)));
+  else
+    return __uint_as_float(u << 16);
+}
+template <typename TI>
+__device__ __forceinline__ float hi16(unsigned u) {
+  if constexpr (std::is_same<TI, _Float16>::value)
+    return static_cast<float>(__builtin_bit_cast(_Float16, static_cast<unsigned short>(u >> 16)));
+  else
+    return __uint_as_float(u & 0xffff0000u);
+}
+template <typename TI>
+__device__ __forceinline__ float to_f(TI v) {
+  if constexpr (std::is_same<TI, float>::value) return v;
+  else return static_cast<float>(v);
+}
+// two floats -> one word of two 16-bit values (element 0 in the low half)
+template <typename TO>
+__device__ __forceinline__ unsigned pack2(float a, float b) {
+  using h2 = TO __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(unsigned, h2{static_cast<TO>(a), static_cast<TO>(b)});
+}
+
+// a lane's 8 A values in flight (loaded in one pipeline step, converted in the next): fp32 or 16-bit scalars
+// (channel-strided NCHW reads), or one 16-byte vector of 8 consecutive channels (NHWC, 16-bit)
+template <typename TI, bool NHWC>
+struct ARaw {
+  TI v[8];
+  __device__ __forceinline__ void load(const TI* src, int64_t stride) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = src[static_cast<int64_t>(e) * stride];
+  }
+  __device__ __forceinline__ void get(float (&x)[8]) const {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = to_f(v[e]);
+  }
+};
+template <typename TI>
+struct ARaw<TI, true> {
+  using u4 = unsigned __attribute__((ext_vector_type(4)));
+  u4 v;
+  __device__ __forceinline__ void load(const TI* src, int64_t) { v = *reinterpret_cast<const u4*>(src); }
+  __device__ __forceinline__ void get(float (&x)[8]) const {
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      x[2 * p] = lo16<TI>(v[p]);
+      x[2 * p + 1] = hi16<TI>(v[p]);
+    }
+  }
+};
 
 // Bs[c][p][n][16] (swizzled rows, NP rows) for the conv GEMM.  Chunk c holds channels 16 (c / T) .. +15 of
 // tap c % T: the taps of one channel group are adjacent in k, so the pixel rows a block loads for one tap are
@@ -68,11 +127,17 @@ __global__ void __launch_bounds__(256) x3_conv_presplit(const float* __restrict_
 // ---------------------------------------------------------------------------------------------------
 // forward / input gradient.  grid (HW / 128, ceil(Cout / 256), N); 4 waves x 32 pixels; Cout tile 256.
 // ---------------------------------------------------------------------------------------------------
-template <int T>
-__global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict__ I, int Ca, int H, int W,
+// TI / INHWC: the A operand's type and layout (16-bit and NHWC: T == 1 forward only); TO / ONHWC: the output's
+// (16-bit and NHWC: T == 1 input gradient only)
+template <int T, typename TI = float, typename TO = float, bool INHWC = false, bool ONHWC = false>
+__global__ void __launch_bounds__(256, 2) x3_conv_kernel(const TI* __restrict__ I, int Ca, int H, int W,
                                                          const __bf16* __restrict__ Bs, int NP,
-                                                         const float* __restrict__ bias, float* __restrict__ O,
+                                                         const float* __restrict__ bias, TO* __restrict__ O,
                                                          int Cout) {
+  static_assert(T == 1 || (std::is_same<TI, float>::value && std::is_same<TO, float>::value && !INHWC && !ONHWC),
+                "16-bit / NHWC operands: 1x1 only");
+  static_assert(!(INHWC && std::is_same<TI, float>::value) && !(ONHWC && std::is_same<TO, float>::value),
+                "NHWC operands are 16-bit");
   constexpr int NW = 4, NT = 256, BN = 256, TJ = BN / 32;
   constexpr int PIECES = 3 * BN * 2, NBL = PIECES / NT;
   constexpr int CHUNK = 3 * BN * 16;
@@ -102,12 +167,12 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int pix = p0 + w * 32 + li, py = pix / W, px = pix - py * W;
-  const float* In = I + static_cast<int64_t>(n) * Ca * HW;
+  const TI* In = I + static_cast<int64_t>(n) * Ca * HW;
   const int cpt = Ca / kBK;               // chunks per tap
   const int nk = T * cpt;
 
   struct Regs {
-    float a[8];
+    ARaw<TI, INHWC> a;
     bf8 b[NBL];
   };
   auto gload = [&](Regs& r, int c) {
@@ -120,9 +185,11 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
     tap_shift(T, tap, dy, dx);
     const int yy = py + dy, xx = px + dx;
     const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
-    const float* src = In + static_cast<int64_t>(ci0) * HW + (ok ? yy * W + xx : 0);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) r.a[e] = src[static_cast<int64_t>(e) * HW];
+    if constexpr (INHWC) {
+      r.a.load(In + static_cast<int64_t>(pix) * Ca + ci0, 1);
+    } else {
+      r.a.load(In + static_cast<int64_t>(ci0) * HW + (ok ? yy * W + xx : 0), HW);
+    }
     const __bf16* bc = Bs + static_cast<int64_t>(cc) * 3 * NP * 16;
 #pragma unroll
     for (int u = 0; u < NBL; ++u) {
@@ -141,8 +208,9 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
     const int yy = py + dy, xx = px + dx;
     const bool ok = yy >= 0 && yy < H && xx >= 0 && xx < W;
     float v[8];
+    r.a.get(v);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = ok ? r.a[e] : 0.f;
+    for (int e = 0; e < 8; ++e) v[e] = ok ? v[e] : 0.f;
     split8(v, fa);
   };
 
@@ -191,22 +259,48 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
   // epilogue: tile j holds C[pixel = (e&3)+8(e>>2)+4lh][co = li]; the image is stored transposed
   // ([co][pixel]) and read back as float4 runs of pixels
   float* img = reinterpret_cast<float*>(smem) + w * 32 * EP;
-  float* Ob = O + static_cast<int64_t>(n) * Cout * HW;
+  TO* Ob = O + static_cast<int64_t>(n) * Cout * HW;
   const int er = lane >> 3, ec = (lane & 7) * 4;
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
+    if constexpr (ONHWC) {
+      // pixel-major image [pixel][co] (row stride 33), read back as 8 consecutive channels of one pixel: a 16-byte
+      // store of 8 16-bit values, 4 lanes per pixel row of the tile
 #pragma unroll
-    for (int e = 0; e < 16; ++e) img[li * EP + (e & 3) + 8 * (e >> 2) + 4 * lh] = acc[j][e];
+      for (int e = 0; e < 16; ++e) img[((e & 3) + 8 * (e >> 2) + 4 * lh) * 33 + li] = acc[j][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) img[li * EP + (e & 3) + 8 * (e >> 2) + 4 * lh] = acc[j][e];
+    }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (ONHWC) {
+      using u4 = unsigned __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int lr = q * 8 + er, co = n20 + j * 32 + lr;
-      f4 v = *reinterpret_cast<const f4*>(&img[lr * EP + ec]);
-      if (co < Cout) {
-        if (bias) v += bias[co];
-        *reinterpret_cast<f4*>(Ob + static_cast<int64_t>(co) * HW + p0 + w * 32 + ec) = v;
+      for (int it = 0; it < 2; ++it) {
+        const int item = lane + 64 * it, pr = item >> 2, grp = item & 3, co = n20 + j * 32 + grp * 8;
+        const float* s = &img[pr * 33 + grp * 8];
+        if (co < Cout) {
+          const u4 pk = {pack2<TO>(s[0], s[1]), pack2<TO>(s[2], s[3]), pack2<TO>(s[4], s[5]), pack2<TO>(s[6], s[7])};
+          *reinterpret_cast<u4*>(O + (static_cast<int64_t>(n) * HW + p0 + w * 32 + pr) * Cout + co) = pk;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int lr = q * 8 + er, co = n20 + j * 32 + lr;
+        f4 v = *reinterpret_cast<const f4*>(&img[lr * EP + ec]);
+        if (co < Cout) {
+          if (bias) v += bias[co];
+          TO* dst = Ob + static_cast<int64_t>(co) * HW + p0 + w * 32 + ec;
+          if constexpr (std::is_same<TO, float>::value) {
+            *reinterpret_cast<f4*>(dst) = v;
+          } else {
+            using u2 = unsigned __attribute__((ext_vector_type(2)));
+            *reinterpret_cast<u2*>(dst) = u2{pack2<TO>(v[0], v[1]), pack2<TO>(v[2], v[3])};
+          }
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -220,9 +314,10 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const float* __restrict
 // (multiples of 16: a chunk never crosses an image).  Block: 4 waves x 32 (tap, ci) columns, 256 co.
 // grid = splits * tiles, tiles = ceil(T*Ci / 128) * ceil(Co / 256).
 // ---------------------------------------------------------------------------------------------------
-template <int T>
+// TI / INHWC: the input's type and layout (16-bit and NHWC: T == 1 only)
+template <int T, typename TI = float, bool INHWC = false>
 __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __restrict__ dO,
-                                                               const float* __restrict__ I, int N, int Co, int Ci,
+                                                               const TI* __restrict__ I, int N, int Co, int Ci,
                                                                int H, int W, int rows_per_split,
                                                                float* __restrict__ slab, float* __restrict__ bias_slab) {
   constexpr int NW = 4, NT = 256, BN = 256, TJ = BN / 32;
@@ -251,8 +346,11 @@ __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __re
   tap_shift(T, tap, dy, dx);
   const bool csum = bias_slab != nullptr && b1 == 0;
 
+  static_assert(T == 1 || (std::is_same<TI, float>::value && !INHWC), "16-bit / NHWC input: 1x1 only");
+  constexpr bool k32 = std::is_same<TI, float>::value;
   struct Regs {
-    f4 a[3];
+    f4 a[k32 ? 3 : 1];                      // fp32: 8 (1x1) or 12 (3x3) pixels of the lane's channel
+    ARaw<TI, !INHWC> h;                     // 16-bit NCHW: one 16-byte vector of 8 pixels; NHWC: 8 strided scalars
     f4 b[NJ][2];
   };
   // chunk c: pixels m = r0 + 16c .. +15 of one image; lane rows 8lh .. 8lh+7 (same image row: W % 8 == 0).
@@ -264,11 +362,15 @@ __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __re
     const int n = static_cast<int>(m / HW), p = static_cast<int>(m - static_cast<int64_t>(n) * HW);
     const int pa = p + lh * 8, y = pa / W, x0 = pa - y * W;
     const int yy = y + dy;
-    const float* row = I + (static_cast<int64_t>(n) * Ci + ci) * HW + static_cast<int64_t>(yy >= 0 && yy < H ? yy : y) * W;
-    if (T == 1) {
+    if constexpr (!k32) {
+      if constexpr (INHWC) r.h.load(I + (static_cast<int64_t>(n) * HW + pa) * Ci + ci, Ci);
+      else r.h.load(I + (static_cast<int64_t>(n) * Ci + ci) * HW + pa, 1);
+    } else if (T == 1) {
+      const TI* row = I + (static_cast<int64_t>(n) * Ci + ci) * HW + static_cast<int64_t>(y) * W;
       r.a[0] = *reinterpret_cast<const f4*>(row + x0);
       r.a[1] = *reinterpret_cast<const f4*>(row + x0 + 4);
     } else {  // one code path for every tap: 12 pixels from base (x0 - 4, or x0 when dx = +1)
+      const TI* row = I + (static_cast<int64_t>(n) * Ci + ci) * HW + static_cast<int64_t>(yy >= 0 && yy < H ? yy : y) * W;
       const int base = dx > 0 ? x0 : x0 - 4;
       r.a[0] = *reinterpret_cast<const f4*>(row + max(base, 0));
       r.a[1] = *reinterpret_cast<const f4*>(row + base + 4);
@@ -312,7 +414,9 @@ __global__ void __launch_bounds__(256, 2) x3_conv_wgrad_kernel(const float* __re
     const int pa = p + lh * 8, y = pa / W, x0 = pa - y * W, yy = y + dy;
     const bool rok = live && yy >= 0 && yy < H;
     float v[8];
-    if (T == 1) {
+    if constexpr (!k32) {
+      r.h.get(v);
+    } else if (T == 1) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = r.a[e >> 2][e & 3];
     } else {
@@ -470,19 +574,37 @@ extern "C" int m2f_conv_f32x3_workspace(int N, int Ci, int Co, int H, int W, int
   return m2f::ok();
 }
 
-// mode 0: O = conv(I, Wt) (+ bias): I [N][Ci][H][W], O [N][Co][H][W]
-// mode 1: O = conv_transpose-style input gradient of dO: I = dO [N][Co][H][W], O = dI [N][Ci][H][W]
-extern "C" int m2f_conv_f32x3(const float* I, const float* Wt, const float* bias, float* O, int N, int Ci, int Co,
-                              int H, int W, int ksize, int mode, void* workspace, int64_t workspace_bytes,
-                              void* stream) {
-  const char* fn = "m2f_conv_f32x3";
+namespace {
+
+// 1x1 launches with 16-bit / NHWC operands (mode 0: the input; mode 1: the output)
+template <typename TI, typename TO, bool INHWC, bool ONHWC>
+void launch_1x1(const void* I, int Ca, int H, int W, const __bf16* Bs, int NP, const float* bias, void* O, int Nn, int N,
+                hipStream_t st) {
+  const dim3 grid((H * W) / 128, (Nn + 255) / 256, N);
+  x3_conv_kernel<1, TI, TO, INHWC, ONHWC><<<grid, 256, 0, st>>>(static_cast<const TI*>(I), Ca, H, W, Bs, NP, bias,
+                                                                 static_cast<TO*>(O), Nn);
+}
+
+int conv_impl(const char* fn, const void* I, int i_dtype, int i_nhwc, const float* Wt, const float* bias, void* O,
+              int o_dtype, int o_nhwc, int N, int Ci, int Co, int H, int W, int ksize, int mode, void* workspace,
+              int64_t workspace_bytes, void* stream) {
   const int T = ksize * ksize;
   int rc = conv_check(fn, N, mode == 0 ? Ci : Co, H, W, mode == 0 ? Co : Ci, T);
   if (rc) return rc;
   if (!I || !Wt || !O || !workspace) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
   if (mode != 0 && mode != 1) return m2f::fail(M2F_EINVAL, "%s: mode %d", fn, mode);
   if (mode == 1 && bias) return m2f::fail(M2F_EINVAL, "%s: the input gradient takes no bias", fn);
-  if (!m2f::aligned(O, 16) || !m2f::aligned(workspace, 16)) return m2f::fail(M2F_EINVAL, "%s: misaligned", fn);
+  const bool i16 = i_dtype == M2F_F16 || i_dtype == M2F_BF16, o16 = o_dtype == M2F_F16 || o_dtype == M2F_BF16;
+  if ((i_dtype != M2F_F32 && !i16) || (o_dtype != M2F_F32 && !o16)) return m2f::fail(M2F_EINVAL, "%s: dtype", fn);
+  // the forward reads 16-bit / NHWC activations and writes fp32 NCHW; the input gradient reads fp32 NCHW and
+  // writes 16-bit / NHWC; both only for 1x1, NHWC only for 16-bit
+  const bool io_ok = mode == 0 ? (o_dtype == M2F_F32 && !o_nhwc && (!i_nhwc || i16))
+                               : (i_dtype == M2F_F32 && !i_nhwc && (!o_nhwc || o16));
+  if (!io_ok || ((i16 || o16 || i_nhwc || o_nhwc) && T != 1))
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: operand types / layouts (in %d/%d, out %d/%d, %dx%d, mode %d)", fn, i_dtype,
+                     i_nhwc, o_dtype, o_nhwc, ksize, ksize, mode);
+  if (!m2f::aligned(O, 16) || !m2f::aligned(workspace, 16) || (i_nhwc && !m2f::aligned(I, 16)))
+    return m2f::fail(M2F_EINVAL, "%s: misaligned", fn);
   const int Ca = mode == 0 ? Ci : Co, Nn = mode == 0 ? Co : Ci;
   if (workspace_bytes < conv_ws(Ca, Nn, T)) return m2f::fail(M2F_EINVAL, "%s: workspace too small", fn);
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -494,24 +616,46 @@ extern "C" int m2f_conv_f32x3(const float* I, const float* Wt, const float* bias
   if (T == 9) {
     const int64_t nblk = static_cast<int64_t>((H * W) / 128) * ((Nn + 255) / 256) * N;
     if (nblk > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many tiles", fn);
-    x3_conv_kernel<9><<<static_cast<unsigned>(nblk), 256, 0, st>>>(I, Ca, H, W, Bs, NP, bias, O, Nn);
+    x3_conv_kernel<9><<<static_cast<unsigned>(nblk), 256, 0, st>>>(static_cast<const float*>(I), Ca, H, W, Bs, NP,
+                                                                    bias, static_cast<float*>(O), Nn);
+  } else if (mode == 0) {
+    if (i_dtype == M2F_F32) launch_1x1<float, float, false, false>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
+    else if (i_dtype == M2F_F16 && i_nhwc) launch_1x1<_Float16, float, true, false>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
+    else if (i_dtype == M2F_F16) launch_1x1<_Float16, float, false, false>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
+    else if (i_nhwc) launch_1x1<__bf16, float, true, false>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
+    else launch_1x1<__bf16, float, false, false>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
   } else {
-    const dim3 grid((H * W) / 128, (Nn + 255) / 256, N);
-    x3_conv_kernel<1><<<grid, 256, 0, st>>>(I, Ca, H, W, Bs, NP, bias, O, Nn);
+    if (o_dtype == M2F_F32) launch_1x1<float, float, false, false>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
+    else if (o_dtype == M2F_F16 && o_nhwc) launch_1x1<float, _Float16, false, true>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
+    else if (o_dtype == M2F_F16) launch_1x1<float, _Float16, false, false>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
+    else if (o_nhwc) launch_1x1<float, __bf16, false, true>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
+    else launch_1x1<float, __bf16, false, false>(I, Ca, H, W, Bs, NP, bias, O, Nn, N, st);
   }
   return m2f::check_launch(fn);
 }
 
-// dW_tck [k*k][Ci][Co] = sum_{n,p} dO[n][co][p] I[n][ci][p + s(tap)]; dbias [Co] = sum dO (if dbias)
-extern "C" int m2f_conv_f32x3_wgrad(const float* dO, const float* I, float* dW, float* dbias, int N, int Ci, int Co,
-                                    int H, int W, int ksize, void* workspace, int64_t workspace_bytes, void* stream) {
-  const char* fn = "m2f_conv_f32x3_wgrad";
+template <typename TI, bool INHWC>
+void launch_wgrad(int T, unsigned grid, const float* dO, const void* I, int N, int Co, int Ci, int H, int W, int rows,
+                  float* slab, float* bslab, hipStream_t st) {
+  if (T == 9)
+    x3_conv_wgrad_kernel<9><<<grid, 256, 0, st>>>(dO, static_cast<const float*>(I), N, Co, Ci, H, W, rows, slab, bslab);
+  else
+    x3_conv_wgrad_kernel<1, TI, INHWC><<<grid, 256, 0, st>>>(dO, static_cast<const TI*>(I), N, Co, Ci, H, W, rows, slab,
+                                                             bslab);
+}
+
+int wgrad_impl(const char* fn, const float* dO, const void* I, int i_dtype, int i_nhwc, float* dW, float* dbias, int N,
+               int Ci, int Co, int H, int W, int ksize, void* workspace, int64_t workspace_bytes, void* stream) {
   const int T = ksize * ksize;
   int rc = conv_check(fn, N, Ci, H, W, Co, T);
   if (rc) return rc;
   if (Co % 16) return m2f::fail(M2F_EUNSUPPORTED, "%s: out channels %% 16 != 0", fn);
   if (!dO || !I || !dW || !workspace) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
-  if (!m2f::aligned(dO, 16)) return m2f::fail(M2F_EINVAL, "%s: misaligned", fn);
+  const bool i16 = i_dtype == M2F_F16 || i_dtype == M2F_BF16;
+  if (i_dtype != M2F_F32 && !i16) return m2f::fail(M2F_EINVAL, "%s: dtype", fn);
+  if ((i16 || i_nhwc) && (T != 1 || !i16))
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: 16-bit / NHWC input needs a 16-bit 1x1 conv", fn);
+  if (!m2f::aligned(dO, 16) || (i16 && !i_nhwc && !m2f::aligned(I, 16))) return m2f::fail(M2F_EINVAL, "%s: misaligned", fn);
   const int64_t M = static_cast<int64_t>(N) * H * W;
   const WgPlan p = wg_plan(M, T * Ci, Co);
   const int64_t need = static_cast<int64_t>(p.splits) * (static_cast<int64_t>(T) * Ci * Co + Co) * 4;
@@ -521,10 +665,12 @@ extern "C" int m2f_conv_f32x3_wgrad(const float* dO, const float* I, float* dW, 
   float* bslab = slab + static_cast<int64_t>(p.splits) * T * Ci * Co;
   const int tiles = ((T * Ci + 127) / 128) * ((Co + 255) / 256);
   const unsigned grid = static_cast<unsigned>(p.splits * tiles);
-  if (T == 9)
-    x3_conv_wgrad_kernel<9><<<grid, 256, 0, st>>>(dO, I, N, Co, Ci, H, W, p.rows, slab, dbias ? bslab : nullptr);
-  else
-    x3_conv_wgrad_kernel<1><<<grid, 256, 0, st>>>(dO, I, N, Co, Ci, H, W, p.rows, slab, dbias ? bslab : nullptr);
+  float* bs = dbias ? bslab : nullptr;
+  if (i_dtype == M2F_F32) launch_wgrad<float, false>(T, grid, dO, I, N, Co, Ci, H, W, p.rows, slab, bs, st);
+  else if (i_dtype == M2F_F16 && i_nhwc) launch_wgrad<_Float16, true>(T, grid, dO, I, N, Co, Ci, H, W, p.rows, slab, bs, st);
+  else if (i_dtype == M2F_F16) launch_wgrad<_Float16, false>(T, grid, dO, I, N, Co, Ci, H, W, p.rows, slab, bs, st);
+  else if (i_nhwc) launch_wgrad<__bf16, true>(T, grid, dO, I, N, Co, Ci, H, W, p.rows, slab, bs, st);
+  else launch_wgrad<__bf16, false>(T, grid, dO, I, N, Co, Ci, H, W, p.rows, slab, bs, st);
   if ((rc = m2f::check_launch(fn))) return rc;
   // the slab sum lands as [(tap, ci)][co]; the caller permutes it to [co][ci][tap]
   const int64_t n = static_cast<int64_t>(T) * Ci * Co;
@@ -535,4 +681,36 @@ extern "C" int m2f_conv_f32x3_wgrad(const float* dO, const float* I, float* dW, 
     return m2f::check_launch(fn);
   }
   return m2f::ok();
+}
+
+}  // namespace
+
+// mode 0: O = conv(I, Wt) (+ bias): I [N][Ci][H][W], O [N][Co][H][W]
+// mode 1: O = conv_transpose-style input gradient of dO: I = dO [N][Co][H][W], O = dI [N][Ci][H][W]
+extern "C" int m2f_conv_f32x3(const float* I, const float* Wt, const float* bias, float* O, int N, int Ci, int Co,
+                              int H, int W, int ksize, int mode, void* workspace, int64_t workspace_bytes,
+                              void* stream) {
+  return conv_impl("m2f_conv_f32x3", I, M2F_F32, 0, Wt, bias, O, M2F_F32, 0, N, Ci, Co, H, W, ksize, mode, workspace,
+                   workspace_bytes, stream);
+}
+
+extern "C" int m2f_conv_x3_io(const void* I, int i_dtype, int i_nhwc, const float* Wt, const float* bias, void* O,
+                              int o_dtype, int o_nhwc, int N, int Ci, int Co, int H, int W, int ksize, int mode,
+                              void* workspace, int64_t workspace_bytes, void* stream) {
+  return conv_impl("m2f_conv_x3_io", I, i_dtype, i_nhwc, Wt, bias, O, o_dtype, o_nhwc, N, Ci, Co, H, W, ksize, mode,
+                   workspace, workspace_bytes, stream);
+}
+
+// dW_tck [k*k][Ci][Co] = sum_{n,p} dO[n][co][p] I[n][ci][p + s(tap)]; dbias [Co] = sum dO (if dbias)
+extern "C" int m2f_conv_f32x3_wgrad(const float* dO, const float* I, float* dW, float* dbias, int N, int Ci, int Co,
+                                    int H, int W, int ksize, void* workspace, int64_t workspace_bytes, void* stream) {
+  return wgrad_impl("m2f_conv_f32x3_wgrad", dO, I, M2F_F32, 0, dW, dbias, N, Ci, Co, H, W, ksize, workspace,
+                    workspace_bytes, stream);
+}
+
+extern "C" int m2f_conv_x3_wgrad_io(const float* dO, const void* I, int i_dtype, int i_nhwc, float* dW, float* dbias,
+                                    int N, int Ci, int Co, int H, int W, int ksize, void* workspace,
+                                    int64_t workspace_bytes, void* stream) {
+  return wgrad_impl("m2f_conv_x3_wgrad_io", dO, I, i_dtype, i_nhwc, dW, dbias, N, Ci, Co, H, W, ksize, workspace,
+                    workspace_bytes, stream);
 }

@@ -218,6 +218,15 @@ def _as_f32_nchw(x):
     return _F32Contiguous.apply(x)
 
 
+def _conv_input(x, conv):
+    """The input of a conv on a backbone feature: a 16-bit feature into a 1x1 conv the x3 kernels take goes in as it
+    is (they read it converted, exactly the ``.float()`` of the reference), anything else through
+    :func:`_as_f32_nchw`."""
+    if x.dtype in (torch.float16, torch.bfloat16) and conv_ops.eligible(x, conv):
+        return x
+    return _as_f32_nchw(x)
+
+
 @register(lambda: SEM_SEG_HEADS_REGISTRY)
 class MSDeformAttnPixelDecoder(nn.Module):
     """Deformable-encoder pixel decoder (msdeformattn.py:164-358)."""
@@ -311,8 +320,8 @@ class MSDeformAttnPixelDecoder(nn.Module):
     def _forward_features(self, features):
         srcs, pos = [], []
         for idx, f in enumerate(self.transformer_in_features[::-1]):
-            x = _as_f32_nchw(features[f])
             proj = self.input_proj[idx]
+            x = _conv_input(features[f], proj[0])
             srcs.append(group_norm_act(conv_ops.conv2d(x, proj[0]), proj[1]))   # 1x1 conv (x3) + GroupNorm
             pos.append(self.pe_layer(x))
 
@@ -323,7 +332,7 @@ class MSDeformAttnPixelDecoder(nn.Module):
         out = [z.transpose(1, 2).view(bs, -1, h, w) for z, (h, w) in zip(torch.split(y, sizes, dim=1), host_shapes)]
 
         for idx, f in enumerate(self.in_features[:self.num_fpn_levels][::-1]):
-            x = _as_f32_nchw(features[f])
+            x = _conv_input(features[f], self.lateral_convs[idx])
             cur_fpn = conv_ops.conv_norm_act(x, self.lateral_convs[idx])
             y = conv_ops.upsample_add(out[-1], cur_fpn)   # cur_fpn + bilinear resize of out[-1], one pass
             out.append(conv_ops.conv_norm_act(y, self.output_convs[idx]))

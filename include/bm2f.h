@@ -294,6 +294,19 @@ int m2f_conv_f32x3(const float* I, const float* W, const float* bias, float* O, 
                    int ksize, int mode, void* workspace, int64_t workspace_bytes, void* stream);
 int m2f_conv_f32x3_wgrad(const float* grad_out, const float* I, float* dW_tck, float* dbias, int N, int Ci, int Co,
                          int H, int Wd, int ksize, void* workspace, int64_t workspace_bytes, void* stream);
+/* The same convolutions on the backbone's 16-bit features without the reference's .float() copy
+ * (msdeformattn.py:320, 336; the conversion is exact, so the results are those of the fp32 calls on
+ * the upcast tensor): 1x1 only.  m2f_conv_x3_io mode 0 reads I as i_dtype (M2F_F32 / M2F_F16 /
+ * M2F_BF16), NCHW or (i_nhwc, 16-bit only) NHWC, and writes fp32 NCHW (o_dtype M2F_F32, o_nhwc 0);
+ * mode 1 reads fp32 NCHW grad_out and writes the input gradient as o_dtype, NCHW or (o_nhwc) NHWC,
+ * rounded to nearest even (the cast's backward).  m2f_conv_x3_wgrad_io: as m2f_conv_f32x3_wgrad with
+ * I of i_dtype / i_nhwc.  Workspace as above. */
+int m2f_conv_x3_io(const void* I, int i_dtype, int i_nhwc, const float* W, const float* bias, void* O, int o_dtype,
+                   int o_nhwc, int N, int Ci, int Co, int H, int Wd, int ksize, int mode, void* workspace,
+                   int64_t workspace_bytes, void* stream);
+int m2f_conv_x3_wgrad_io(const float* grad_out, const void* I, int i_dtype, int i_nhwc, float* dW_tck, float* dbias,
+                         int N, int Ci, int Co, int H, int Wd, int ksize, void* workspace, int64_t workspace_bytes,
+                         void* stream);
 
 /* Fused per-channel bias (+ residual) + ReLU in place over an NCHW activation (dtype M2F_BF16, M2F_F16
  * or M2F_F32), memory NCHW or (channels_last != 0) NHWC: x = max(x + residual + bias[c], 0).  The

@@ -43,6 +43,39 @@ def test_conv_x3_vs_fp64(device, N, Ci, Co, H, W, k, bias, wgrad3, monkeypatch):
         assert _rel(conv.bias.grad, bd.grad) < 2e-6
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("layout", ["nchw", "channels_last"])
+@pytest.mark.parametrize("N,Ci,Co,H,W,bias", [(2, 512, 256, 16, 16, True), (1, 64, 48, 8, 16, False),
+                                              (3, 256, 256, 16, 8, True)])
+def test_conv_x3_16bit_input_bitwise(device, dtype, layout, N, Ci, Co, H, W, bias):
+    """A 16-bit backbone feature into a 1x1 conv (m2f_conv_x3_io / _wgrad_io: read as it is, NCHW or channels-last)
+    gives bit for bit what the fp32 kernels give on the reference's ``x.float()``: output, weight and bias gradients
+    equal, and the input gradient equals the fp32 one rounded to the feature dtype (the cast's backward), returned
+    in the feature's layout."""
+    torch.manual_seed(Ci + Co + H + (layout == "nchw"))
+    conv = nn.Conv2d(Ci, Co, 1, bias=bias).to(device)
+    x16 = torch.randn(N, Ci, H, W, device=device).to(dtype)
+    if layout == "channels_last":
+        x16 = x16.contiguous(memory_format=torch.channels_last)
+    x16.requires_grad_()
+    assert conv_ops.eligible(x16, conv)
+    y = conv_ops.conv2d(x16, conv)
+    g = torch.randn_like(y)
+    y.backward(g)
+    dw, db = conv.weight.grad.clone(), conv.bias.grad.clone() if bias else None
+    conv.zero_grad()
+    x32 = x16.detach().float().contiguous().requires_grad_()
+    y32 = conv_ops.conv2d(x32, conv)
+    y32.backward(g)
+    assert y.dtype == torch.float32 and torch.equal(y, y32)
+    assert x16.grad.dtype == dtype and torch.equal(x16.grad, x32.grad.to(dtype))
+    if layout == "channels_last":
+        assert x16.grad.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(dw, conv.weight.grad)
+    if bias:
+        assert torch.equal(db, conv.bias.grad)
+
+
 def test_conv_x3_fallback_shapes(device):
     conv = nn.Conv2d(256, 256, 3, padding=1, stride=2).to(device)
     x = torch.randn(1, 256, 16, 16, device=device)

@@ -219,10 +219,11 @@ def main():
     ap.add_argument("--prof-steps", type=int, default=2)
     ap.add_argument("--amp", default="fp16", choices=["fp16", "bf16"])
     ap.add_argument("--no-sites", action="store_true")
+    ap.add_argument("--channels-last", type=int, default=1, choices=[0, 1], help="backbone layout (as bench.py)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     torch.manual_seed(0)
-    model = MaskFormerR50(default_cfg()).to(dev)
+    model = MaskFormerR50(default_cfg(), channels_last=bool(a.channels_last)).to(dev)
     opt = make_optimizer(model)
     amp = torch.float16 if a.amp == "fp16" else torch.bfloat16
     scaler = make_scaler(amp) or torch.amp.GradScaler("cuda", enabled=False)
