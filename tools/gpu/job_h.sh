@@ -11,3 +11,5 @@ for r in 1 2; do
     timeout -k 10 200 python -u tools/conv_bench.py --x3-only --lib $lib >> gpurun_out/r5h_ab.log 2>&1 || exit 1
   done
 done
+# masked attention: per-kernel durations (main kernel vs combine / dq reduce) at the decoder shapes
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/r5h_mattn_prof" -o mattn -- python3 "$GRAFT_REPO_ROOT/tools/mattn_bench.py" > "$GRAFT_REPO_ROOT/gpurun_out/r5h_mattn.log" 2>&1 || exit 1
