@@ -66,6 +66,7 @@ _SIGNATURES = {
     "m2f_upsample2x_bwd_nhwc_f32": [_p, _p, _i, _i, _i, _i, _p],
     "m2f_maxpool3s2_fwd": [_p, _p, _p, _l, _i, _i, _i, _p],
     "m2f_maxpool3s2_bwd": [_p, _p, _p, _l, _i, _i, _i, _p],
+    "m2f_maxpool3s2_nhwc": [_i, _p, _p, _p, _i, _i, _i, _i, _i, _p],
     "m2f_stream_copy": [_p, _p, _l, _i, _p],
     "m2f_gather_probe": [_p, _i, _l, _p, _i, _p],
     "m2f_set_option": [ctypes.c_char_p, _l],
@@ -73,6 +74,7 @@ _SIGNATURES = {
     "m2f_transpose_f32": [_p, _l, _l, _p, _l, _l, _i, _i, _i, _p],
     "m2f_colsum_workspace": [_l, _i, _p],
     "m2f_colsum": [_i, _p, _l, _i, _p, _l, _p, _p],
+    "m2f_sum_to_f32": [_p, _i, _l, _i, _p, _p],
     "m2f_group_norm_workspace": [_i, _i, _i, _l, _p],
     "m2f_group_norm_fwd_f32": [_p, _p, _p, _i, _i, _i, _l, _f, _i, _p, _p, _p, _p, _l, _p],
     "m2f_group_norm_bwd_f32": [_p, _p, _p, _p, _p, _p, _i, _i, _i, _l, _i, _p, _p, _p, _p, _l, _p],

@@ -176,8 +176,39 @@ class _MaxPool3s2(torch.autograd.Function):
         return gx
 
 
+class _MaxPool3s2NHWC(torch.autograd.Function):
+    """The same pool on a channels-last 16-bit x (csrc/eltwise.hip ``m2f_maxpool3s2_nhwc``), y channels-last."""
+
+    @staticmethod
+    def forward(ctx, x):
+        from . import _native
+        N, C, H, W = x.shape
+        OH, OW = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = torch.empty(N, OH, OW, C, device=x.device, dtype=x.dtype).permute(0, 3, 1, 2)
+        win = torch.empty(N, OH, OW, C, device=x.device, dtype=torch.uint8)
+        _native.call("m2f_maxpool3s2_nhwc", 0, x.data_ptr(), y.data_ptr(), win.data_ptr(), N, H, W, C,
+                     _CODE[x.dtype], torch.cuda.current_stream(x.device).cuda_stream)
+        ctx.save_for_backward(win)
+        ctx.in_shape = x.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, grad):
+        from . import _native
+        (win,) = ctx.saved_tensors
+        N, C, H, W = ctx.in_shape
+        g = grad.contiguous(memory_format=torch.channels_last)
+        gx = torch.empty(N, H, W, C, device=g.device, dtype=g.dtype).permute(0, 3, 1, 2)
+        _native.call("m2f_maxpool3s2_nhwc", 1, g.data_ptr(), gx.data_ptr(), win.data_ptr(), N, H, W, C,
+                     _CODE[g.dtype], torch.cuda.current_stream(g.device).cuda_stream)
+        return gx
+
+
 def max_pool_stem(x):
     """detectron2 BasicStem's ``F.max_pool2d(x, kernel_size=3, stride=2, padding=1)``."""
+    if (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 4 and x.shape[1] % 8 == 0
+            and not x.is_contiguous() and x.is_contiguous(memory_format=torch.channels_last)):
+        return _MaxPool3s2NHWC.apply(x)
     if x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32) and x.dim() == 4 and x.is_contiguous():
         return _MaxPool3s2.apply(x)
     return F.max_pool2d(x, kernel_size=3, stride=2, padding=1)

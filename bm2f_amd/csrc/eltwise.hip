@@ -139,6 +139,67 @@ extern "C" int m2f_relu_bwd_sum(const void* const* grads, int ngrads, const void
 }
 
 // ---------------------------------------------------------------------------------------------------
+// The fp32 sum of k same-shaped low-precision (or fp32) tensors, in order: out = ((s_0 + s_1) + ...) + s_{k-1}
+// with every term converted to fp32 and every add an fp32 add -- the values of out = s_0.float() followed by
+// k - 1 in-place `out += s_i` (torch's mixed-dtype add), in one pass (k reads, one write) instead of k.  The
+// decoder's memory-token input gradients: one per K / V projection of every layer reading a level
+// (mask2former_transformer_decoder.py:103-108), summed in fp32 as autograd sums the cast backward's results.
+// ---------------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kMaxSumTerms = 8;
+
+struct SumTerms {
+  const void* s[kMaxSumTerms];
+};
+
+template <typename T, int V>
+__global__ void __launch_bounds__(256) sum_to_f32_kernel(SumTerms ts, int k, float* __restrict__ out, int64_t nvec) {
+  using VT = Vec<T, V>;
+  const int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (i >= nvec) return;
+  float acc[V];
+  const VT s0 = reinterpret_cast<const VT*>(ts.s[0])[i];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = static_cast<float>(s0.v[e]);
+  for (int t = 1; t < k; ++t) {
+    const VT st = reinterpret_cast<const VT*>(ts.s[t])[i];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] += static_cast<float>(st.v[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < V; e += 4)
+    *reinterpret_cast<float4*>(out + i * V + e) = make_float4(acc[e], acc[e + 1], acc[e + 2], acc[e + 3]);
+}
+
+}  // namespace
+
+extern "C" int m2f_sum_to_f32(const void* const* srcs, int k, int64_t n, int dtype, float* out, void* stream) {
+  const char* fn = "m2f_sum_to_f32";
+  if (!srcs || k < 1 || k > kMaxSumTerms || !out || n < 0)
+    return m2f::fail(M2F_EINVAL, "%s: bad arguments (1 <= terms <= %d)", fn, kMaxSumTerms);
+  if (dtype != M2F_BF16 && dtype != M2F_F16 && dtype != M2F_F32)
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d", fn, dtype);
+  const int V = 8;
+  SumTerms ts{};
+  bool aligned = m2f::aligned(out, 16);
+  for (int t = 0; t < k; ++t) {
+    if (!srcs[t]) return m2f::fail(M2F_EINVAL, "%s: null term %d", fn, t);
+    ts.s[t] = srcs[t];
+    aligned = aligned && m2f::aligned(srcs[t], 16);
+  }
+  if (n % V || !aligned) return m2f::fail(M2F_EUNSUPPORTED, "%s: needs n %% %d == 0 and 16-byte aligned tensors", fn, V);
+  const int64_t nvec = n / V;
+  if (nvec == 0) return m2f::ok();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = m2f::ceil_div(nvec, 256);
+  if (dtype == M2F_BF16) sum_to_f32_kernel<__bf16, 8><<<grid, 256, 0, st>>>(ts, k, out, nvec);
+  else if (dtype == M2F_F16) sum_to_f32_kernel<_Float16, 8><<<grid, 256, 0, st>>>(ts, k, out, nvec);
+  else sum_to_f32_kernel<float, 8><<<grid, 256, 0, st>>>(ts, k, out, nvec);
+  return m2f::check_launch(fn);
+}
+
+// ---------------------------------------------------------------------------------------------------
 // The benchmark backbone's stem max pool, kernel 3, stride 2, padding 1 (detectron2 BasicStem), NCHW.
 // Forward: torch's max_pool2d_with_indices rule (first maximum in window order, NaN wins), the winner
 // kept as a 1-byte window position (0..8) instead of an int64 flat index.  Backward: each input pixel
@@ -253,7 +314,119 @@ __global__ void __launch_bounds__(256) maxpool3s2_bwd8(const T* __restrict__ gy,
   }
 }
 
+// NHWC (channels-last) forms: a thread per (pixel, 8 channels), every window read as 16-byte channel vectors; the
+// same per-channel rules and order as the NCHW kernels above (first maximum in window order, a NaN wins; the
+// backward's (ph, pw) order with an fp32 sum).  C % 8 == 0.
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool3s2_fwd_nhwc(const T* __restrict__ x, T* __restrict__ y,
+                                                          uint8_t* __restrict__ win, int H, int W, int OH, int OW,
+                                                          int C, int64_t total8) {
+  using VT = Vec<T, 8>;
+  const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (t >= total8) return;
+  const int C8 = C / 8;
+  const int c8 = static_cast<int>(t % C8);
+  int64_t r = t / C8;
+  const int ow = static_cast<int>(r % OW);
+  r /= OW;
+  const int oh = static_cast<int>(r % OH);
+  const int64_t n = r / OH;
+  const int h0 = 2 * oh - 1, w0 = 2 * ow - 1;
+  const int hs = max(h0, 0), he = min(h0 + 3, H), ws = max(w0, 0), we = min(w0 + 3, W);
+  float best[8];
+  int bi[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    best[e] = -INFINITY;
+    bi[e] = (hs - h0) * 3 + (ws - w0);
+  }
+  const T* xp = x + (n * H * W) * C + c8 * 8;
+  for (int h = hs; h < he; ++h)
+    for (int w = ws; w < we; ++w) {
+      const VT v = *reinterpret_cast<const VT*>(xp + (static_cast<int64_t>(h) * W + w) * C);
+      const int k = (h - h0) * 3 + (w - w0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = static_cast<float>(v.v[e]);
+        if (f > best[e] || f != f) {
+          best[e] = f;
+          bi[e] = k;
+        }
+      }
+    }
+  VT o;
+  uint8_t wb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o.v[e] = static_cast<T>(best[e]);
+    wb[e] = static_cast<uint8_t>(bi[e]);
+  }
+  const int64_t oo = ((n * OH + oh) * OW + ow) * C + c8 * 8;
+  *reinterpret_cast<VT*>(y + oo) = o;
+  *reinterpret_cast<uint2*>(win + oo) = *reinterpret_cast<const uint2*>(wb);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool3s2_bwd_nhwc(const T* __restrict__ gy, const uint8_t* __restrict__ win,
+                                                          T* __restrict__ gx, int H, int W, int OH, int OW, int C,
+                                                          int64_t total8) {
+  using VT = Vec<T, 8>;
+  const int64_t t = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x;
+  if (t >= total8) return;
+  const int C8 = C / 8;
+  const int c8 = static_cast<int>(t % C8);
+  int64_t r = t / C8;
+  const int w = static_cast<int>(r % W);
+  r /= W;
+  const int h = static_cast<int>(r % H);
+  const int64_t n = r / H;
+  const int phs = h + 1 < 3 ? 0 : (h - 2) / 2 + 1, phe = min((h + 1) / 2 + 1, OH);
+  const int pws = w + 1 < 3 ? 0 : (w - 2) / 2 + 1, pwe = min((w + 1) / 2 + 1, OW);
+  float acc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+  for (int ph = phs; ph < phe; ++ph)
+    for (int pw = pws; pw < pwe; ++pw) {
+      const int64_t o = ((n * OH + ph) * OW + pw) * C + c8 * 8;
+      const VT g = *reinterpret_cast<const VT*>(gy + o);
+      uint8_t wb[8];
+      *reinterpret_cast<uint2*>(wb) = *reinterpret_cast<const uint2*>(win + o);
+      const int k = (h - (2 * ph - 1)) * 3 + (w - (2 * pw - 1));
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (wb[e] == k) acc[e] += static_cast<float>(g.v[e]);
+    }
+  VT o;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) o.v[e] = static_cast<T>(acc[e]);
+  *reinterpret_cast<VT*>(gx + ((n * H + h) * W + w) * C + c8 * 8) = o;
+}
+
 }  // namespace
+
+extern "C" int m2f_maxpool3s2_nhwc(int backward, const void* src, void* dst, uint8_t* window, int N, int H, int W,
+                                   int C, int dtype, void* stream) {
+  const char* fn = "m2f_maxpool3s2_nhwc";
+  if (!src || !dst || !window || N < 0 || H <= 0 || W <= 0 || C <= 0) return m2f::fail(M2F_EINVAL, "%s: bad arguments", fn);
+  if (dtype != M2F_BF16 && dtype != M2F_F16) return m2f::fail(M2F_EUNSUPPORTED, "%s: dtype %d (16-bit only)", fn, dtype);
+  if (C % 8 || !m2f::aligned(src, 16) || !m2f::aligned(dst, 16) || !m2f::aligned(window, 8))
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs C %% 8 == 0 and aligned tensors", fn);
+  const int OH = (H - 1) / 2 + 1, OW = (W - 1) / 2 + 1;
+  const int64_t total8 = static_cast<int64_t>(N) * (backward ? static_cast<int64_t>(H) * W : static_cast<int64_t>(OH) * OW) * (C / 8);
+  if (total8 == 0) return m2f::ok();
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const unsigned grid = m2f::ceil_div(total8, 256);
+#define M2F_MPN(T)                                                                                                     \
+  if (backward)                                                                                                        \
+    maxpool3s2_bwd_nhwc<T><<<grid, 256, 0, st>>>(static_cast<const T*>(src), window, static_cast<T*>(dst), H, W, OH,   \
+                                                 OW, C, total8);                                                       \
+  else                                                                                                                 \
+    maxpool3s2_fwd_nhwc<T><<<grid, 256, 0, st>>>(static_cast<const T*>(src), static_cast<T*>(dst), window, H, W, OH,   \
+                                                 OW, C, total8);
+  if (dtype == M2F_BF16) { M2F_MPN(__bf16) } else { M2F_MPN(_Float16) }
+#undef M2F_MPN
+  return m2f::check_launch(fn);
+}
 
 extern "C" int m2f_maxpool3s2_fwd(const void* x, void* y, uint8_t* window, int64_t planes, int H, int W, int dtype,
                                   void* stream) {

@@ -551,14 +551,41 @@ class _SavedLike:
 class GradSink:
     """The fp32 gradient of one memory-token tensor that several :func:`token_linear_sink` calls read (the K and V
     projections of the 3 decoder layers on one level): each call's input gradient -- the autocast-dtype GEMM result,
-    as the reference's per-call cast backward sees it -- is added into one fp32 buffer in one mixed-dtype pass (the
-    first is cast into it), and the call whose backward runs last hands the sum to autograd; the others return no
-    input gradient.  Autograd's path casts every call's gradient to fp32 and adds the fp32 tensors.  One sink per
-    tensor and forward."""
+    as the reference's per-call cast backward sees it -- is kept, and the call whose backward runs last sums them in
+    fp32 in arrival order in one pass (m2f_sum_to_f32: the values of a cast of the first and an fp32 add of each
+    further one, without re-reading and re-writing the fp32 sum per call) and hands the sum to autograd; the others
+    return no input gradient.  Autograd's path casts every call's gradient to fp32 and adds the fp32 tensors.  One
+    sink per tensor and forward."""
 
     def __init__(self):
-        self.buf = None
+        self.terms = []
         self.pending = 0
+
+    def add(self, g):
+        self.terms.append(g)
+        self.pending -= 1
+        if self.pending:
+            return None
+        terms, self.terms = self.terms, []
+        return sum_to_f32(terms)
+
+
+def sum_to_f32(terms):
+    """``terms[0].float() + terms[1] + ...`` in fp32, in order (each add an fp32 add of the converted term): one pass
+    on m2f_sum_to_f32 for up to 8 same-shaped contiguous CUDA tensors, torch's adds otherwise."""
+    t0 = terms[0]
+    ok = (t0.is_cuda and 1 <= len(terms) <= 8 and t0.numel() % 8 == 0
+          and all(t.shape == t0.shape and t.dtype == t0.dtype and t.is_contiguous() and t.data_ptr() % 16 == 0
+                  for t in terms))
+    if not ok:
+        out = t0.to(torch.float32)
+        for t in terms[1:]:
+            torch.add(out, t, out=out)
+        return out
+    out = torch.empty(t0.shape, dtype=torch.float32, device=t0.device)
+    ptrs = (ctypes.c_void_p * len(terms))(*[t.data_ptr() for t in terms])
+    _native.call("m2f_sum_to_f32", ptrs, len(terms), t0.numel(), _code(t0.dtype), out.data_ptr(), _stream(t0))
+    return out
 
 
 class _TokenLinearSink(Function):
@@ -585,13 +612,9 @@ class _TokenLinearSink(Function):
             if not g2.is_contiguous():
                 g2 = g2.contiguous()
             gx_lp = g2 @ w                                   # the autocast-dtype input gradient of this call
-            if sink.buf is None:
-                sink.buf = gx_lp.to(torch.float32)
-            else:
-                torch.add(sink.buf, gx_lp, out=sink.buf)         # fp32 + low precision -> fp32, one pass
-            sink.pending -= 1
-            if sink.pending == 0:
-                gx, sink.buf = sink.buf.view(ctx.x_shape), None
+            total = sink.add(gx_lp)
+            if total is not None:
+                gx = total.view(ctx.x_shape)
         sub = _SavedLike(ctx, x_lp, w)
         sub.needs_input_grad = (False, ctx.needs_input_grad[2], ctx.needs_input_grad[3])
         _, gw, gb = _TokenLinear.backward(sub, grad)

@@ -308,6 +308,12 @@ int m2f_conv_x3_wgrad_io(const float* grad_out, const void* I, int i_dtype, int 
                          int N, int Ci, int Co, int H, int Wd, int ksize, void* workspace, int64_t workspace_bytes,
                          void* stream);
 
+/* out[n] (fp32) = ((s_0 + s_1) + ...) + s_{k-1}, every term converted to fp32 (dtype M2F_F16 / M2F_BF16 /
+ * M2F_F32) and added in fp32 in order -- the values of out = s_0.float() and k - 1 in-place mixed-dtype adds, in
+ * one pass.  srcs: a host array of k <= 8 device pointers; n % 8 == 0, 16-byte aligned.  Replaces the autograd
+ * sums of the decoder's memory-token input gradients (mask2former_transformer_decoder.py:103-108). */
+int m2f_sum_to_f32(const void* const* srcs, int k, int64_t n, int dtype, float* out, void* stream);
+
 /* Fused per-channel bias (+ residual) + ReLU in place over an NCHW activation (dtype M2F_BF16, M2F_F16
  * or M2F_F32), memory NCHW or (channels_last != 0) NHWC: x = max(x + residual + bias[c], 0).  The
  * benchmark backbone's FrozenBN shift + shortcut + ReLU in one pass (not on the reference's hot path).
@@ -331,6 +337,11 @@ int m2f_relu_bwd_sum(const void* const* grads, int ngrads, const void* y, void* 
 int m2f_maxpool3s2_fwd(const void* x, void* y, uint8_t* window, int64_t planes, int H, int W, int dtype, void* stream);
 int m2f_maxpool3s2_bwd(const void* grad_y, const uint8_t* window, void* grad_x, int64_t planes, int H, int W, int dtype,
                        void* stream);
+/* The same max pool on a channels-last (NHWC) 16-bit tensor (N, H, W, C), C % 8 == 0: backward = 0 reads src = x
+ * and writes dst = y (N, OH, OW, C) and window (N, OH, OW, C) bytes; backward = 1 reads src = grad_y and window and
+ * writes dst = grad_x (N, H, W, C). */
+int m2f_maxpool3s2_nhwc(int backward, const void* src, void* dst, uint8_t* window, int N, int H, int W, int C,
+                        int dtype, void* stream);
 
 /* Explicit tuning options: geometry / engine overrides for tests and tools (the library never reads the
  * environment).  value < 0 restores the built-in default.  Names: msda_threads, msda_tile, msda_tile_w,

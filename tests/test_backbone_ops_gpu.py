@@ -78,6 +78,32 @@ def test_stem_maxpool_matches_torch(device, dtype, H, W):
     assert torch.equal(xa.grad, xb.grad)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("H,W,C", [(16, 24, 64), (7, 9, 8), (1, 1, 16), (5, 16, 24)])
+def test_stem_maxpool_nhwc_matches_torch(device, dtype, H, W, C):
+    """The channels-last stem max pool (m2f_maxpool3s2_nhwc) against F.max_pool2d(3, 2, 1) on the same
+    channels-last tensor: forward and gradient bit-exact (ties, -inf, NaN), output and gradient channels-last."""
+    from bm2f_amd.bench_model import max_pool_stem
+    torch.manual_seed(H * 31 + W + C)
+    x = torch.randint(-3, 4, (2, C, H, W), device=device).to(dtype)
+    x.view(-1)[::7] = float("-inf")
+    if H * W > 4:
+        x.view(-1)[5] = float("nan")
+    x = x.contiguous(memory_format=torch.channels_last)
+    xa = x.clone(memory_format=torch.channels_last).requires_grad_()
+    xb = x.clone(memory_format=torch.channels_last).requires_grad_()
+    ya = max_pool_stem(xa)
+    yb = F.max_pool2d(xb, kernel_size=3, stride=2, padding=1)
+    assert ya.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(ya.isnan(), yb.isnan())
+    assert torch.equal(ya.nan_to_num(), yb.nan_to_num())
+    g = torch.randn_like(yb)
+    ya.backward(g)
+    yb.backward(g)
+    assert xa.grad.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(xa.grad, xb.grad)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float32])
 def test_bias_act_nan_follows_torch(device, dtype):
     """NaN activations: the forward propagates them as torch's relu does, and the multi-consumer backward

@@ -21,6 +21,26 @@ def test_colsum_matches_fp64(device, dt, rows, cols):
     assert torch.equal(got, colsum_f32(x))   # same order every call
 
 
+@pytest.mark.parametrize("dt", [torch.float16, torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("k", [1, 2, 6, 8])
+def test_sum_to_f32_bitwise_vs_sequential_adds(device, dt, k):
+    """m2f_sum_to_f32 (the decoder's memory-gradient sink) equals terms[0].float() followed by k - 1 in-place
+    mixed-dtype adds -- the arithmetic of autograd's cast-and-accumulate -- bit for bit."""
+    from bm2f_amd.decoder_ops import sum_to_f32
+    g = torch.Generator(device=device).manual_seed(k)
+    terms = [(torch.randn(2048, 256, device=device, generator=g) * 10 ** (i % 3)).to(dt) for i in range(k)]
+    want = terms[0].float()
+    for t in terms[1:]:
+        torch.add(want, t, out=want)
+    got = sum_to_f32(terms)
+    assert got.dtype == torch.float32 and torch.equal(got, want)
+    odd = [t.reshape(-1)[:1001] for t in terms]          # 1001 elements: the torch path
+    want_odd = odd[0].float()
+    for t in odd[1:]:
+        torch.add(want_odd, t, out=want_odd)
+    assert torch.equal(sum_to_f32(odd), want_odd)
+
+
 def test_colsum_non_contiguous_input(device):
     from bm2f_amd.decoder_ops import colsum_f32
     x = torch.randn(256, 4096, device=device).t()   # (4096, 256) view with stride (1, 4096)
