@@ -578,7 +578,7 @@ def sum_to_f32(terms):
           and all(t.shape == t0.shape and t.dtype == t0.dtype and t.is_contiguous() and t.data_ptr() % 16 == 0
                   for t in terms))
     if not ok:
-        out = t0.to(torch.float32)
+        out = t0.to(torch.float32, copy=True)
         for t in terms[1:]:
             torch.add(out, t, out=out)
         return out

@@ -29,13 +29,13 @@ def test_sum_to_f32_bitwise_vs_sequential_adds(device, dt, k):
     from bm2f_amd.decoder_ops import sum_to_f32
     g = torch.Generator(device=device).manual_seed(k)
     terms = [(torch.randn(2048, 256, device=device, generator=g) * 10 ** (i % 3)).to(dt) for i in range(k)]
-    want = terms[0].float()
+    want = terms[0].to(torch.float32, copy=True)         # (an fp32 term's .float() would alias it)
     for t in terms[1:]:
         torch.add(want, t, out=want)
     got = sum_to_f32(terms)
     assert got.dtype == torch.float32 and torch.equal(got, want)
     odd = [t.reshape(-1)[:1001] for t in terms]          # 1001 elements: the torch path
-    want_odd = odd[0].float()
+    want_odd = odd[0].to(torch.float32, copy=True)
     for t in odd[1:]:
         torch.add(want_odd, t, out=want_odd)
     assert torch.equal(sum_to_f32(odd), want_odd)
