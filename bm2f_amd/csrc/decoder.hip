@@ -276,17 +276,37 @@ __device__ __forceinline__ void mask4(f4& s, uint32_t word) {
 // form: S^T tile = one MFMA per 16 keys (K = head dim 32), O^T += V^T P^T one per 32 keys, the key order inside the
 // K = 32 step permuted so that P's C fragments of two key tiles are the B operand as they are (element j < 4: key
 // 4g + j of the first tile, j >= 4: of the second) and V^T's A operand is two transposed reads of those tiles.
+// Workgroup -> (b * H + h, key chunk c) of a (B * H, nchunks) grid.  xmap = 1: the H heads of one (image, chunk) on
+// one XCD, one after another (workgroups are dealt to the 8 XCDs round-robin by linear id).  A head's K / V slice is
+// 64 bytes of each 512-byte key row (16-bit, 8 heads); with the plain mapping head h runs on XCD h (H = 8), so every
+// XCD's L2 fetched whole 128-byte lines for half of them (FETCH_SIZE 2.2-2.3x the K / V bytes).  The host sets xmap
+// only when B * nchunks % 8 == 0 (then L = 8t + x, h = t % H, b * nchunks + c = (t / H) * 8 + x is a bijection).
+__device__ __forceinline__ void mattn_block(int H, int xmap, int& bh, int& c) {
+  if (xmap) {
+    const int L = blockIdx.x + gridDim.x * blockIdx.y;
+    const int x = L & 7, t = L >> 3;
+    const int grp = (t / H) * 8 + x;
+    c = grp % gridDim.y;
+    bh = (grp / gridDim.y) * H + t % H;
+  } else {
+    bh = blockIdx.x;
+    c = blockIdx.y;
+  }
+}
+
 template <typename T, int TPW>
 __global__ void __launch_bounds__(256, TPW <= 2 ? 4 : TPW <= 4 ? 2 : 1) mattn_fwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
     int Lq, int Lk, int H, int qs, int kvs, int nw, float sl2, int chunk_len, T* __restrict__ out,
-    float* __restrict__ lse2, float* __restrict__ ws_o, float* __restrict__ ws_ml) {
+    float* __restrict__ lse2, float* __restrict__ ws_o, float* __restrict__ ws_ml, int xmap) {
   constexpr bool k16 = Elt<T>::k16;
   constexpr int RS = KVImage<T>::RS;
   __shared__ T Ks[2][KVImage<T>::ELEMS];
   __shared__ T Vs[2][KVImage<T>::ELEMS];
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
-  const int nchunks = gridDim.y, c = blockIdx.y;
+  int bh, c;
+  mattn_block(H, xmap, bh, c);
+  const int b = bh / H, h = bh % H;
+  const int nchunks = gridDim.y;
   const int key_begin = c * chunk_len;
   const int key_end = min(Lk, key_begin + chunk_len);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
@@ -534,7 +554,7 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
     const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
     const T* __restrict__ out, const T* __restrict__ dout, const float* __restrict__ lse2, int Lq, int Lk, int H,
     int qs, int kvs, int nw, float sl2, float scale, int chunk_len, int Lqp, T* __restrict__ dq,
-    T* __restrict__ dk, T* __restrict__ dv, float* __restrict__ ws_dq) {
+    T* __restrict__ dk, T* __restrict__ dv, float* __restrict__ ws_dq, int xmap) {
   constexpr bool k16 = Elt<T>::k16;
   constexpr int RS = KVImage<T>::RS;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -551,8 +571,10 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
   float* scr = reinterpret_cast<float*>(mw + 2 * Lqp);
   float* dqa = scr + 4 * 16 * 17;
 
-  const int bh = blockIdx.x, b = bh / H, h = bh % H;
-  const int nchunks = gridDim.y, c = blockIdx.y;
+  int bh, c;
+  mattn_block(H, xmap, bh, c);
+  const int b = bh / H, h = bh % H;
+  const int nchunks = gridDim.y;
   const int key_begin = c * chunk_len;
   const int key_end = min(Lk, key_begin + chunk_len);
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
@@ -870,6 +892,291 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
   }
 }
 
+// Two key tiles per wave (16-bit operands, dQ in registers: Lq <= 16 * NTR): per 128-key block wave w owns keys
+// 32w .. 32w + 31 (tile a: 32w + r, tile b: 32w + 16 + r).  Everything a query tile needs -- its Q / dO fragments,
+// mask words (both tiles' keys sit in one word), LSE, delta and the dO^T / Q^T fragments of the dV / dK products --
+// is read from LDS once for both key tiles, and dQ^T += K^T dS^T runs as one 16x16x32 product over the 32 keys
+// instead of four 16x16x16 ones.  The dS transpose goes through a 20-float-pitch scratch, so a lane reads its four
+// transposed values with one 16-byte read.  Same arithmetic per element as mattn_bwd_kernel (the dQ^T sum over a
+// block's keys is one MFMA chain in another key order).
+template <typename T, int NTR>
+__global__ void __launch_bounds__(256, 2) mattn_bwd2_kernel(
+    const T* __restrict__ q, const T* __restrict__ k, const T* __restrict__ v, const uint32_t* __restrict__ bits,
+    const T* __restrict__ out, const T* __restrict__ dout, const float* __restrict__ lse2, int Lq, int Lk, int H,
+    int qs, int kvs, int nw, float sl2, float scale, int chunk_len, int Lqp, T* __restrict__ dq,
+    T* __restrict__ dk, T* __restrict__ dv, float* __restrict__ ws_dq, int xmap) {
+  static_assert(Elt<T>::k16 && NTR > 0, "16-bit operands, register dQ");
+  constexpr int RS = KVImage<T>::RS;
+  constexpr int SP = 20;  // transpose scratch pitch (floats): 16-byte aligned rows, conflict-free column writes
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // carve: Qs, dOs [Lqp][RS] T | Ks, Vs [2][128][RS] T | lse, delta [Lqp] f32 | mw [2][4][Lqp] u32 | scr [4][16][SP]
+  //        f32 (x2: tiles a / b); dQacc [Lqp][kD] f32 over the K / V images once the key loop is done (two
+  //        workgroups per CU: 67.7 KB at Lqp = 112)
+  T* Qs = reinterpret_cast<T*>(smem);
+  T* dOs = Qs + Lqp * RS;
+  T* Ks2 = dOs + Lqp * RS;
+  T* Vs2 = Ks2 + 2 * 128 * RS;
+  size_t off = (reinterpret_cast<unsigned char*>(Vs2 + 2 * 128 * RS) - smem + 15) & ~size_t(15);
+  float* lse_s = reinterpret_cast<float*>(smem + off);
+  float* del_s = lse_s + Lqp;
+  uint32_t* mw2 = reinterpret_cast<uint32_t*>(del_s + Lqp);
+  float* scr = reinterpret_cast<float*>(mw2 + 8 * Lqp);
+  float* dqa = reinterpret_cast<float*>(Ks2);   // 16-byte aligned: Qs and dOs are Lqp * RS * 2 bytes, Lqp % 16 == 0
+
+  int bh, c;
+  mattn_block(H, xmap, bh, c);
+  const int b = bh / H, h = bh % H;
+  const int nchunks = gridDim.y;
+  const int key_begin = c * chunk_len;
+  const int key_end = min(Lk, key_begin + chunk_len);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, r = lane & 15;
+  const int64_t kvrow0 = static_cast<int64_t>(b) * Lk;
+  const int NT = Lqp / 16;
+  const int HD = H * kD;
+
+  // stage Q, dO (rows >= Lq zero), lse, delta (as mattn_bwd_kernel)
+  for (int idx = threadIdx.x; idx < Lqp * 4; idx += 256) {
+    const int qi = idx >> 2, part = idx & 3;
+    f4 qv = {0.f, 0.f, 0.f, 0.f}, gv = qv;
+    if (qi < Lq) {
+      qv = *reinterpret_cast<const f4*>(q + (static_cast<int64_t>(b) * Lq + qi) * qs + h * kD + part * 8);
+      gv = *reinterpret_cast<const f4*>(dout + (static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + part * 8);
+    }
+    const s4* qh = reinterpret_cast<const s4*>(&qv);
+    const s4* gh = reinterpret_cast<const s4*>(&gv);
+    s4* qd = reinterpret_cast<s4*>(Qs + qi * RS + part * 8);
+    s4* gd = reinterpret_cast<s4*>(dOs + qi * RS + part * 8);
+    qd[0] = qh[0]; qd[1] = qh[1];
+    gd[0] = gh[0]; gd[1] = gh[1];
+  }
+  for (int qi = threadIdx.x; qi < Lqp; qi += 256) {
+    float dl = 0.f, ls = INFINITY;
+    if (qi < Lq) {
+      const T* orow = out + (static_cast<int64_t>(b) * Lq + qi) * HD + h * kD;
+      const T* grow = dout + (static_cast<int64_t>(b) * Lq + qi) * HD + h * kD;
+      f4 ov[4], gv[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        ov[p] = *reinterpret_cast<const f4*>(orow + p * 8);
+        gv[p] = *reinterpret_cast<const f4*>(grow + p * 8);
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const T* oe = reinterpret_cast<const T*>(&ov[p]);
+        const T* ge = reinterpret_cast<const T*>(&gv[p]);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dl += Elt<T>::to_f(oe[e]) * Elt<T>::to_f(ge[e]);
+      }
+      ls = lse2[static_cast<int64_t>(bh) * Lq + qi];
+    }
+    del_s[qi] = dl;
+    lse_s[qi] = ls;
+  }
+
+  float* myscr = scr + w * 2 * 16 * SP;   // tile a's [16][SP], then tile b's
+  f4 dqacc[NTR][2];
+#pragma unroll
+  for (int qt = 0; qt < NTR; ++qt) dqacc[qt][0] = dqacc[qt][1] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // the next 128-key block's K / V rows (two 64-row halves) and mask words (4 per query) in registers
+  constexpr int kMaxMwPerThread = 1;   // Lqp <= 256 (the kernel runs at Lqp <= 128)
+  f4 kreg[2][2], vreg[2][2];
+  uint32_t mreg[kMaxMwPerThread][4];
+  auto prefetch = [&](int kb) {
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int kh = min(kb + 64 * hf, key_end - 1);   // a half past the chunk repeats its last row (masked)
+      stage_load<T, true>(k, kvrow0 + kh, key_end - kh, kvs, h * kD, kreg[hf]);
+      stage_load<T, true>(v, kvrow0 + kh, key_end - kh, kvs, h * kD, vreg[hf]);
+    }
+#pragma unroll
+    for (int u = 0; u < kMaxMwPerThread; ++u) {
+      const uint32_t* mr = bits + (static_cast<int64_t>(b) * Lq + min(static_cast<int>(threadIdx.x) + 256 * u, Lq - 1)) * nw;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) mreg[u][t] = mr[min((kb >> 5) + t, nw - 1)];
+    }
+  };
+  if (key_begin < key_end) prefetch(key_begin);
+  int buf = 0;
+  for (int kb0 = key_begin; kb0 < key_end; kb0 += 128, buf ^= 1) {
+    // two images: this block's was last read two blocks ago, before the previous block's barrier
+    T* Ks = Ks2 + buf * 128 * RS;
+    T* Vs = Vs2 + buf * 128 * RS;
+    uint32_t* mw = mw2 + buf * 4 * Lqp;
+    stage_store<T>(Ks, kreg[0]);
+    stage_store<T>(Ks + 64 * RS, kreg[1]);
+    stage_store<T>(Vs, vreg[0]);
+    stage_store<T>(Vs + 64 * RS, vreg[1]);
+    const int kvalid = key_end - kb0;
+#pragma unroll
+    for (int u = 0; u < kMaxMwPerThread; ++u) {
+      const int qi = threadIdx.x + 256 * u;
+      if (qi < Lqp) {
+        const uint32_t xr = qi < Lq ? 0u : 0xffffffffu;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          // keys 32t .. 32t + 31 of the block: those past the chunk (or past Lk: no such word) set
+          const int kv = kvalid - 32 * t;
+          const uint32_t xk = kv >= 32 ? 0u : (kv <= 0 ? 0xffffffffu : (0xffffffffu << (kv & 31)));
+          const uint32_t xw = (kb0 >> 5) + t < nw ? 0u : 0xffffffffu;
+          mw[t * Lqp + qi] = mreg[u][t] | xk | xw | xr;
+        }
+      }
+    }
+    __syncthreads();
+    if (kb0 + 128 < key_end) prefetch(kb0 + 128);   // in flight during this block's MFMAs
+    if (32 * w >= kvalid) continue;                 // both of this wave's tiles past the chunk (wave-uniform)
+    const int ka = 32 * w + r, kb = ka + 16;        // this lane's keys (columns) within the block
+
+    // K, V as B[k = d][col = key] for both tiles
+    const T* kra = Ks + ka * RS + 8 * g;
+    const T* krb = Ks + kb * RS + 8 * g;
+    const T* vra = Vs + ka * RS + 8 * g;
+    const T* vrb = Vs + kb * RS + 8 * g;
+    const s8 kba = cat8(*reinterpret_cast<const s4*>(kra), *reinterpret_cast<const s4*>(kra + 4));
+    const s8 kbb = cat8(*reinterpret_cast<const s4*>(krb), *reinterpret_cast<const s4*>(krb + 4));
+    const s8 vba = cat8(*reinterpret_cast<const s4*>(vra), *reinterpret_cast<const s4*>(vra + 4));
+    const s8 vbb = cat8(*reinterpret_cast<const s4*>(vrb), *reinterpret_cast<const s4*>(vrb + 4));
+    // K^T fragments of dQ^T += K^T dS^T (A[row d][k = key], the 32 keys in the order tile a 4g+j, tile b 4g+j)
+    s8 kta[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+      kta[dt] = cat8(tr_read(Ks + (32 * w + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3)),
+                     tr_read(Ks + (32 * w + 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3)));
+    f4 dka[2] = {f4{0.f, 0.f, 0.f, 0.f}, f4{0.f, 0.f, 0.f, 0.f}}, dkb[2] = {dka[0], dka[1]};
+    f4 dva[2] = {dka[0], dka[1]}, dvb[2] = {dka[0], dka[1]};
+    const uint32_t* mwsel = mw + w * Lqp;   // keys 32w .. 32w + 31: one word; tile a bit r, tile b bit 16 + r
+
+    // one query tile against the wave's 32 keys: P, dS of both tiles (packed for dV / dK), dQ^T
+    auto tile = [&](const int qt, f4* dqt, s4& pa, s4& sa, s4& pb, s4& sb) {
+      const T* qr = Qs + (qt * 16 + r) * RS + 8 * g;
+      const T* gr = dOs + (qt * 16 + r) * RS + 8 * g;
+      const s8 qf = cat8(*reinterpret_cast<const s4*>(qr), *reinterpret_cast<const s4*>(qr + 4));
+      const s8 gf = cat8(*reinterpret_cast<const s4*>(gr), *reinterpret_cast<const s4*>(gr + 4));
+      const f4 z = {0.f, 0.f, 0.f, 0.f};
+      const f4 s_a = mmak32<T>(qf, kba, z), s_b = mmak32<T>(qf, kbb, z);
+      const f4 dp_a = mmak32<T>(gf, vba, z), dp_b = mmak32<T>(gf, vbb, z);
+      const int q0 = qt * 16 + 4 * g;
+      const uint4 mq = *reinterpret_cast<const uint4*>(mwsel + q0);
+      const f4 lq = *reinterpret_cast<const f4*>(lse_s + q0);
+      const f4 dq4 = *reinterpret_cast<const f4*>(del_s + q0);
+      const uint32_t mqa[4] = {mq.x, mq.y, mq.z, mq.w};
+      f4 P_a, S_a, P_b, S_b;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float pva = mask_zero(mqa[i], r, ex2(fmaf(s_a[i], sl2, -lq[i])));
+        const float pvb = mask_zero(mqa[i], 16 + r, ex2(fmaf(s_b[i], sl2, -lq[i])));
+        P_a[i] = pva;
+        S_a[i] = pva * (dp_a[i] - dq4[i]);
+        P_b[i] = pvb;
+        S_b[i] = pvb * (dp_b[i] - dq4[i]);
+      }
+      pa = pack4<T>(P_a[0], P_a[1], P_a[2], P_a[3]);
+      sa = pack4<T>(S_a[0], S_a[1], S_a[2], S_a[3]);
+      pb = pack4<T>(P_b[0], P_b[1], P_b[2], P_b[3]);
+      sb = pack4<T>(S_b[0], S_b[1], S_b[2], S_b[3]);
+      // dS^T through the scratch: [q][key] rows of pitch SP, read back as dS^T[key = 4g + j][q = r]
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        myscr[(4 * g + i) * SP + r] = S_a[i];
+        myscr[16 * SP + (4 * g + i) * SP + r] = S_b[i];
+      }
+      __builtin_amdgcn_wave_barrier();
+      // (q = r, keys 4g .. 4g + 3): scr[key][q] is the transpose; read row q = r of the [q][key] image? no: the
+      // lane needs dS[q = r][key = 4g + j], i.e. row r, columns 4g .. 4g + 3 of the [q][key] image: one 16-B read
+      const f4 ta = *reinterpret_cast<const f4*>(myscr + r * SP + 4 * g);
+      const f4 tb = *reinterpret_cast<const f4*>(myscr + 16 * SP + r * SP + 4 * g);
+      __builtin_amdgcn_wave_barrier();
+      const s8 sbt = cat8(pack4<T>(ta[0], ta[1], ta[2], ta[3]), pack4<T>(tb[0], tb[1], tb[2], tb[3]));
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) dqt[dt] = mmak32<T>(kta[dt], sbt, dqt[dt]);
+    };
+    // dV^T += dO^T P, dK^T += Q^T dS for both key tiles over a pair of query tiles (the dO^T / Q^T fragments once)
+    auto dvdk2 = [&](int qa, s4 pa_a, s4 sa_a, s4 pa_b, s4 sa_b, int qb, s4 pb_a, s4 sb_a, s4 pb_b, s4 sb_b) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int ra = (qa * 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
+        const int rb = (qb * 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
+        const s8 go = cat8(tr_read(dOs + ra), tr_read(dOs + rb));
+        const s8 qo = cat8(tr_read(Qs + ra), tr_read(Qs + rb));
+        dva[dt] = mmak32<T>(go, cat8(pa_a, pb_a), dva[dt]);
+        dvb[dt] = mmak32<T>(go, cat8(pa_b, pb_b), dvb[dt]);
+        dka[dt] = mmak32<T>(qo, cat8(sa_a, sb_a), dka[dt]);
+        dkb[dt] = mmak32<T>(qo, cat8(sa_b, sb_b), dkb[dt]);
+      }
+    };
+    auto dvdk1 = [&](int qa, s4 pa_a, s4 sa_a, s4 pa_b, s4 sa_b) {
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int ro = (qa * 16 + 4 * g + (r >> 2)) * RS + dt * 16 + 4 * (r & 3);
+        const s4 go = tr_read(dOs + ro), qo = tr_read(Qs + ro);
+        dva[dt] = mma16<T>(go, pa_a, dva[dt]);
+        dvb[dt] = mma16<T>(go, pa_b, dvb[dt]);
+        dka[dt] = mma16<T>(qo, sa_a, dka[dt]);
+        dkb[dt] = mma16<T>(qo, sa_b, dkb[dt]);
+      }
+    };
+    s4 ppa = {0, 0, 0, 0}, spa = ppa, ppb = ppa, spb = ppa;   // an even query tile's P / dS waiting for its pair
+#pragma unroll
+    for (int qt = 0; qt < NTR; ++qt)
+      if (qt < NT) {
+        s4 pa, sa, pb, sb;
+        tile(qt, dqacc[qt], pa, sa, pb, sb);
+        if (qt & 1) dvdk2(qt - 1, ppa, spa, ppb, spb, qt, pa, sa, pb, sb);
+        else { ppa = pa; spa = sa; ppb = pb; spb = sb; }
+      }
+    if (NT & 1) dvdk1(NT - 1, ppa, spa, ppb, spb);
+    // dK, dV of both tiles: lane holds [d = dt*16 + 4g + i][key]
+#pragma unroll
+    for (int t2 = 0; t2 < 2; ++t2) {
+      const int kk = t2 ? kb : ka;
+      if (kk >= kvalid) continue;
+      const int64_t krow = (kvrow0 + kb0 + kk) * HD + h * kD;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const f4 kk4 = (t2 ? dkb[dt] : dka[dt]) * scale;
+        const f4 vv4 = t2 ? dvb[dt] : dva[dt];
+        *reinterpret_cast<s4*>(dk + krow + dt * 16 + 4 * g) = pack4<T>(kk4[0], kk4[1], kk4[2], kk4[3]);
+        *reinterpret_cast<s4*>(dv + krow + dt * 16 + 4 * g) = pack4<T>(vv4[0], vv4[1], vv4[2], vv4[3]);
+      }
+    }
+  }
+  // sum the four waves' register dQ^T into dqa (over the K / V images: zeroed once every wave is past its last
+  // block), one wave at a time
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < Lqp * kD / 4; idx += 256) reinterpret_cast<f4*>(dqa)[idx] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int ww = 0; ww < 4; ++ww) {
+    __syncthreads();
+    if (w == ww) {
+#pragma unroll
+      for (int qt = 0; qt < NTR; ++qt) {
+        if (qt < NT) {
+#pragma unroll
+          for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i] += dqacc[qt][dt][i];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int BH = gridDim.x;
+  for (int idx = threadIdx.x; idx < Lq * kD; idx += 256) {
+    const int qi = idx / kD, d = idx % kD;
+    const float val = dqa[idx] * scale;
+    if (nchunks == 1)
+      dq[(static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + d] = Elt<T>::from_f(val);
+    else
+      ws_dq[((static_cast<int64_t>(c) * BH + bh) * Lq + qi) * kD + d] = val;
+  }
+}
+
+size_t bwd2_lds_bytes(int Lqp, int elt) {
+  size_t bytes = static_cast<size_t>(2 * Lqp + 512) * kDP * elt;   // Q, dO and two 128-row K / V images
+  bytes = (bytes + 15) & ~size_t(15);
+  return bytes + sizeof(float) * 2 * Lqp + sizeof(uint32_t) * 8 * Lqp + sizeof(float) * 4 * 2 * 16 * 20;
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256) mattn_dq_reduce_kernel(const float* __restrict__ ws_dq, int nchunks, int BH,
                                                               int H, int Lq, T* __restrict__ dq) {
@@ -877,7 +1184,8 @@ __global__ void __launch_bounds__(256) mattn_dq_reduce_kernel(const float* __res
   const int64_t total = static_cast<int64_t>(BH) * Lq * kD;
   if (idx >= total) return;
   float acc = 0.f;
-  for (int c = 0; c < nchunks; ++c) acc += ws_dq[static_cast<int64_t>(c) * total + idx];
+#pragma unroll 8
+  for (int c = 0; c < nchunks; ++c) acc += ws_dq[static_cast<int64_t>(c) * total + idx];   // in chunk order
   const int d = static_cast<int>(idx % kD);
   const int64_t row = idx / kD;
   const int bh = static_cast<int>(row / Lq), qi = static_cast<int>(row % Lq);
@@ -934,6 +1242,9 @@ int attn_mask_impl(const char* fn, const void* logits, int B, int Q, int F, int 
   return m2f::check_launch(fn);
 }
 
+// mattn_block's head-per-XCD grouping where it is a bijection (option mattn_xcd = 0: the plain mapping)
+int xcd_map(int B, int nch) { return m2f::option(m2f::kOptMattnXcd, 1) != 0 && (B * nch) % 8 == 0 ? 1 : 0; }
+
 template <typename T>
 int mattn_fwd_impl(const char* fn, const void* q, const void* k, const void* v, const uint32_t* bits, int B, int Lq,
                    int Lk, int H, int D, int qs, int kvs, int nw, float scale, void* out, float* lse2, float* ws,
@@ -957,19 +1268,20 @@ int mattn_fwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   float* ws_ml = ws ? ws + static_cast<size_t>(nch) * B * H * Lq * kD : nullptr;
   const float sl2 = scale * kLog2e;
   const dim3 grid(B * H, nch);
+  const int xm = xcd_map(B, nch);
   const int tiles = (Lq + 15) / 16, tpw = (tiles + 3) / 4;
   const T* qq = static_cast<const T*>(q);
   const T* kk = static_cast<const T*>(k);
   const T* vv = static_cast<const T*>(v);
   T* oo = static_cast<T*>(out);
   if (tpw <= 1)
-    mattn_fwd_kernel<T, 1><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml);
+    mattn_fwd_kernel<T, 1><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml, xm);
   else if (tpw <= 2)
-    mattn_fwd_kernel<T, 2><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml);
+    mattn_fwd_kernel<T, 2><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml, xm);
   else if (tpw <= 4)
-    mattn_fwd_kernel<T, 4><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml);
+    mattn_fwd_kernel<T, 4><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml, xm);
   else
-    mattn_fwd_kernel<T, 8><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml);
+    mattn_fwd_kernel<T, 8><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml, xm);
   int rc = m2f::check_launch(fn);
   if (rc || nch == 1) return rc;
   const int64_t total = static_cast<int64_t>(B) * H * Lq * (kD / 4);
@@ -1007,6 +1319,28 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   const int mode = !reg_dq ? 0 : Lqp <= 128 ? 1 : (Lqp <= 208 && dqopt != 2) ? 3 : lds_wave <= 160 * 1024 ? 2 : 0;
   const size_t lds = mode == 2 ? lds_wave : bwd_lds_bytes(Lqp, Elt<T>::k16, sizeof(T));
   if (lds > 160 * 1024) return m2f::fail(M2F_EUNSUPPORTED, "%s: %zu B of LDS", fn, lds);
+  // 16-bit operands with dQ in registers (Lq <= 128): two key tiles per wave (option mattn_bwd_keys = 16: one)
+  if constexpr (Elt<T>::k16) {
+    if (mode == 1 && m2f::option(m2f::kOptMattnBwdKeys, 32) == 32) {
+      const size_t lds2 = bwd2_lds_bytes(Lqp, sizeof(T));
+      static bool attr2[2] = {false, false};
+      const int ai2 = std::is_same<T, __bf16>::value ? 0 : 1;
+      if (!attr2[ai2]) {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mattn_bwd2_kernel<T, 8>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr2[ai2] = true;
+      }
+      mattn_bwd2_kernel<T, 8><<<dim3(B * H, nch), 256, lds2, st>>>(
+          static_cast<const T*>(q), static_cast<const T*>(k), static_cast<const T*>(v), bits,
+          static_cast<const T*>(out), static_cast<const T*>(dout), lse2, Lq, Lk, H, qs, kvs, nw, scale * kLog2e, scale,
+          chunk, Lqp, static_cast<T*>(dq), static_cast<T*>(dk), static_cast<T*>(dv), ws, xcd_map(B, nch));
+      int rc = m2f::check_launch(fn);
+      if (rc || nch == 1) return rc;
+      const int64_t total = static_cast<int64_t>(B) * H * Lq * kD;
+      mattn_dq_reduce_kernel<T><<<m2f::ceil_div(total, 256), 256, 0, st>>>(ws, nch, B * H, H, Lq, static_cast<T*>(dq));
+      return m2f::check_launch(fn);
+    }
+  }
   auto kern = mode == 1   ? &mattn_bwd_kernel<T, 8>
               : mode == 3 ? &mattn_bwd_kernel<T, 13>
               : mode == 2 ? &mattn_bwd_kernel<T, -1>
@@ -1023,7 +1357,7 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   kern<<<grid, 256, lds, st>>>(
       static_cast<const T*>(q), static_cast<const T*>(k), static_cast<const T*>(v), bits, static_cast<const T*>(out),
       static_cast<const T*>(dout), lse2, Lq, Lk, H, qs, kvs, nw, scale * kLog2e, scale, chunk, Lqp,
-      static_cast<T*>(dq), static_cast<T*>(dk), static_cast<T*>(dv), ws);
+      static_cast<T*>(dq), static_cast<T*>(dk), static_cast<T*>(dv), ws, xcd_map(B, nch));
   int rc = m2f::check_launch(fn);
   if (rc || nch == 1) return rc;
   const int64_t total = static_cast<int64_t>(B) * H * Lq * kD;

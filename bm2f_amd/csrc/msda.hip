@@ -42,7 +42,8 @@ constexpr const char* kOptionNames[m2f::kOptCount] = {
     "msda_threads", "msda_tile", "msda_tile_w", "msda_halo", "msda_win_rows", "msda_bwd_tiled", "msda_fwd_tiled",
     "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap",
     "msda_bwd_det", "msda_fwd_pb", "msda_bwd_ratio", "msda_fwd_lds", "msda_fwd_tile", "msda_fwd_tile_w",
-    "msda_fwd_cap", "msda_fwd_halo", "mattn_fwd_minblk", "mattn_bwd_minblk", "mask_df_stage"};
+    "msda_fwd_cap", "msda_fwd_halo", "mattn_fwd_minblk", "mattn_bwd_minblk", "mask_df_stage",
+    "mattn_bwd_keys", "mattn_xcd"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
