@@ -22,6 +22,7 @@
 namespace {
 
 using f4 = float __attribute__((ext_vector_type(4)));
+using f2 = float __attribute__((ext_vector_type(2)));
 using s4 = short __attribute__((ext_vector_type(4)));
 using h4 = _Float16 __attribute__((ext_vector_type(4)));
 using lds_s4 = __attribute__((address_space(3))) s4;
@@ -84,10 +85,10 @@ __device__ __forceinline__ float mask_ninf(uint32_t word, float x) {
   const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(word), POS, 1));
   return __uint_as_float((m & 0xff800000u) | (~m & __float_as_uint(x)));
 }
-// x, or 0 where bit `pos` of `word` is set
-__device__ __forceinline__ float mask_zero(uint32_t word, uint32_t pos, float x) {
-  const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(word), pos, 1));
-  return __uint_as_float(~m & __float_as_uint(x));
+// x where bit `pos` of `kept` (an inverted mask word: bit set = key visible) is set, else 0 (v_bfe + v_and)
+__device__ __forceinline__ float keep_bit(uint32_t kept, uint32_t pos, float x) {
+  const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(kept), pos, 1));
+  return __uint_as_float(m & __float_as_uint(x));
 }
 // raw v_exp_f32 (2^x; -inf -> 0): the scores' exponents are <= 0, where exp2f's denormal range reduction only
 // changes results below 2^-126
@@ -637,8 +638,8 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
       }
       ls = lse2[static_cast<int64_t>(bh) * Lq + qi];
     }
-    del_s[qi] = dl;
-    lse_s[qi] = ls;
+    del_s[qi] = -dl;   // negated: the pair updates add them
+    lse_s[qi] = -ls;
   }
 
   float* myscr = scr + w * 16 * 17;
@@ -683,8 +684,8 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
         const int qi = threadIdx.x + 256 * u;
         if (qi < Lqp) {
           const uint32_t xr = qi < Lq ? 0u : 0xffffffffu;
-          mw[qi] = mreg[u][0] | x0 | xr;
-          mw[Lqp + qi] = mreg[u][1] | x1 | xw | xr;
+          mw[qi] = ~(mreg[u][0] | x0 | xr);   // inverted: bit set = key visible
+          mw[Lqp + qi] = ~(mreg[u][1] | x1 | xw | xr);
         }
       }
     }
@@ -754,15 +755,18 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
       // C layout: [q = qt*16 + 4g + i][key = koff]; the four queries' mask words, LSE and delta in one 16-B read each
       const int q0 = qt * 16 + 4 * g;
       const uint4 mq = *reinterpret_cast<const uint4*>(mwsel + q0);
-      const f4 lq = *reinterpret_cast<const f4*>(lse_s + q0);
-      const f4 dq4 = *reinterpret_cast<const f4*>(del_s + q0);
+      const f4 nlq = *reinterpret_cast<const f4*>(lse_s + q0);   // -LSE
+      const f4 ndq = *reinterpret_cast<const f4*>(del_s + q0);   // -delta
       const uint32_t mqa[4] = {mq.x, mq.y, mq.z, mq.w};
       f4 p, ds;
+      const f2 sl2v = {sl2, sl2};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float pv = mask_zero(mqa[i], bit, ex2(fmaf(s[i], sl2, -lq[i])));
-        p[i] = pv;
-        ds[i] = pv * (dp[i] - dq4[i]);
+      for (int i = 0; i < 4; i += 2) {   // two at a time (v_pk_fma / v_pk_add / v_pk_mul)
+        const f2 e = __builtin_elementwise_fma(f2{s[i], s[i + 1]}, sl2v, f2{nlq[i], nlq[i + 1]});
+        const f2 pv = {keep_bit(mqa[i], bit, ex2(e[0])), keep_bit(mqa[i + 1], bit, ex2(e[1]))};
+        const f2 dv = pv * (f2{dp[i], dp[i + 1]} + f2{ndq[i], ndq[i + 1]});
+        p[i] = pv[0]; p[i + 1] = pv[1];
+        ds[i] = dv[0]; ds[i + 1] = dv[1];
       }
       if constexpr (k16) {
         pbo = pack4<T>(p[0], p[1], p[2], p[3]);
@@ -969,8 +973,8 @@ __global__ void __launch_bounds__(256, 2) mattn_bwd2_kernel(
       }
       ls = lse2[static_cast<int64_t>(bh) * Lq + qi];
     }
-    del_s[qi] = dl;
-    lse_s[qi] = ls;
+    del_s[qi] = -dl;   // negated: the pair updates add them
+    lse_s[qi] = -ls;
   }
 
   float* myscr = scr + w * 2 * 16 * SP;   // tile a's [16][SP], then tile b's
@@ -1019,7 +1023,7 @@ __global__ void __launch_bounds__(256, 2) mattn_bwd2_kernel(
           const int kv = kvalid - 32 * t;
           const uint32_t xk = kv >= 32 ? 0u : (kv <= 0 ? 0xffffffffu : (0xffffffffu << (kv & 31)));
           const uint32_t xw = (kb0 >> 5) + t < nw ? 0u : 0xffffffffu;
-          mw[t * Lqp + qi] = mreg[u][t] | xk | xw | xr;
+          mw[t * Lqp + qi] = ~(mreg[u][t] | xk | xw | xr);   // inverted: bit set = key visible
         }
       }
     }
@@ -1058,18 +1062,25 @@ __global__ void __launch_bounds__(256, 2) mattn_bwd2_kernel(
       const f4 dp_a = mmak32<T>(gf, vba, z), dp_b = mmak32<T>(gf, vbb, z);
       const int q0 = qt * 16 + 4 * g;
       const uint4 mq = *reinterpret_cast<const uint4*>(mwsel + q0);
-      const f4 lq = *reinterpret_cast<const f4*>(lse_s + q0);
-      const f4 dq4 = *reinterpret_cast<const f4*>(del_s + q0);
+      const f4 nlq = *reinterpret_cast<const f4*>(lse_s + q0);   // -LSE
+      const f4 ndq = *reinterpret_cast<const f4*>(del_s + q0);   // -delta
       const uint32_t mqa[4] = {mq.x, mq.y, mq.z, mq.w};
+      // exponents, differences and products two at a time (v_pk_fma / v_pk_add / v_pk_mul: same roundings as the
+      // scalar forms)
       f4 P_a, S_a, P_b, S_b;
+      const f2 sl2v = {sl2, sl2};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float pva = mask_zero(mqa[i], r, ex2(fmaf(s_a[i], sl2, -lq[i])));
-        const float pvb = mask_zero(mqa[i], 16 + r, ex2(fmaf(s_b[i], sl2, -lq[i])));
-        P_a[i] = pva;
-        S_a[i] = pva * (dp_a[i] - dq4[i]);
-        P_b[i] = pvb;
-        S_b[i] = pvb * (dp_b[i] - dq4[i]);
+      for (int i = 0; i < 4; i += 2) {
+        const f2 nl = {nlq[i], nlq[i + 1]}, nd = {ndq[i], ndq[i + 1]};
+        const f2 ea = __builtin_elementwise_fma(f2{s_a[i], s_a[i + 1]}, sl2v, nl);
+        const f2 eb = __builtin_elementwise_fma(f2{s_b[i], s_b[i + 1]}, sl2v, nl);
+        const f2 pa2 = {keep_bit(mqa[i], r, ex2(ea[0])), keep_bit(mqa[i + 1], r, ex2(ea[1]))};
+        const f2 pb2 = {keep_bit(mqa[i], 16 + r, ex2(eb[0])), keep_bit(mqa[i + 1], 16 + r, ex2(eb[1]))};
+        const f2 sa2 = pa2 * (f2{dp_a[i], dp_a[i + 1]} + nd), sb2 = pb2 * (f2{dp_b[i], dp_b[i + 1]} + nd);
+        P_a[i] = pa2[0]; P_a[i + 1] = pa2[1];
+        P_b[i] = pb2[0]; P_b[i + 1] = pb2[1];
+        S_a[i] = sa2[0]; S_a[i + 1] = sa2[1];
+        S_b[i] = sb2[0]; S_b[i + 1] = sb2[1];
       }
       pa = pack4<T>(P_a[0], P_a[1], P_a[2], P_a[3]);
       sa = pack4<T>(S_a[0], S_a[1], S_a[2], S_a[3]);
@@ -1082,8 +1093,7 @@ __global__ void __launch_bounds__(256, 2) mattn_bwd2_kernel(
         myscr[16 * SP + (4 * g + i) * SP + r] = S_b[i];
       }
       __builtin_amdgcn_wave_barrier();
-      // (q = r, keys 4g .. 4g + 3): scr[key][q] is the transpose; read row q = r of the [q][key] image? no: the
-      // lane needs dS[q = r][key = 4g + j], i.e. row r, columns 4g .. 4g + 3 of the [q][key] image: one 16-B read
+      // the lane needs dS[q = r][key = 4g + j]: row r, columns 4g .. 4g + 3 of the [q][key] image, one 16-byte read
       const f4 ta = *reinterpret_cast<const f4*>(myscr + r * SP + 4 * g);
       const f4 tb = *reinterpret_cast<const f4*>(myscr + 16 * SP + r * SP + 4 * g);
       __builtin_amdgcn_wave_barrier();
