@@ -28,6 +28,8 @@ using h4 = _Float16 __attribute__((ext_vector_type(4)));
 using lds_s4 = __attribute__((address_space(3))) s4;
 
 constexpr int kD = 32;       // head dim (hidden 256 / 8 heads)
+constexpr int kDQ = kD + 1;   // row pitch of the register-dQ reductions' LDS image (floats): at most 2-way bank
+                              // conflicts (a pitch of kD puts the 16 lanes of a column group on one bank)
 constexpr int kDP = kD + 4;  // padded LDS row (elements) for 16-bit images: 72 B rows, 8 B aligned
 constexpr float kLog2e = 1.4426950408889634f;
 
@@ -571,6 +573,7 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
   uint32_t* mw = reinterpret_cast<uint32_t*>(del_s + Lqp);
   float* scr = reinterpret_cast<float*>(mw + 2 * Lqp);
   float* dqa = scr + 4 * 16 * 17;
+  const int dq_elems = NTR > 0 ? Lqp * kDQ : Lqp * kD;   // register-dQ modes: padded rows (kDQ)
 
   int bh, c;
   mattn_block(H, xmap, bh, c);
@@ -600,7 +603,7 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
       qd[0] = qh[0]; qd[1] = qh[1];
       gd[0] = gh[0]; gd[1] = gh[1];
     }
-    for (int idx = threadIdx.x; idx < Lqp * kD / 4; idx += 256) reinterpret_cast<f4*>(dqa)[idx] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int idx = threadIdx.x; idx < dq_elems / 4; idx += 256) reinterpret_cast<f4*>(dqa)[idx] = f4{0.f, 0.f, 0.f, 0.f};
   } else {
     for (int idx = threadIdx.x; idx < Lqp * kD; idx += 256) {
       const int qi = idx / kD, d = idx % kD;
@@ -613,6 +616,7 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
       dOs[qi * RS + d] = gv;
       dqa[idx] = 0.f;
     }
+    for (int idx = Lqp * kD + threadIdx.x; idx < dq_elems; idx += 256) dqa[idx] = 0.f;   // the padding
   }
   for (int qi = threadIdx.x; qi < Lqp; qi += 256) {
     float dl = 0.f, ls = INFINITY;
@@ -865,7 +869,7 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
   }
   if constexpr (NTR > 0) {
     // sum the four waves' register dQ^T into dqa, one wave at a time (plain LDS read-modify-write)
-    // lane holds dQ^T[d = dt*16 + 4g + i][q = qt*16 + r]
+    // lane holds dQ^T[d = dt*16 + 4g + i][q = qt*16 + r]; rows of kDQ floats
     for (int ww = 0; ww < 4; ++ww) {
       __syncthreads();
       if (w == ww) {
@@ -875,7 +879,7 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-              for (int i = 0; i < 4; ++i) dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i] += dqacc[qt][dt][i];
+              for (int i = 0; i < 4; ++i) dqa[(qt * 16 + r) * kDQ + dt * 16 + 4 * g + i] += dqacc[qt][dt][i];
           }
         }
       }
@@ -886,7 +890,7 @@ __global__ void __launch_bounds__(256, NTR > 8 ? 2 : 1) mattn_bwd_kernel(
   const int BH = gridDim.x;
   for (int idx = threadIdx.x; idx < Lq * kD; idx += 256) {
     const int qi = idx / kD, d = idx % kD;
-    float sum = dqa[idx];
+    float sum = dqa[NTR > 0 ? qi * kDQ + d : idx];
     if constexpr (NTR < 0) sum = ((sum + dqa[Lqp * kD + idx]) + dqa[2 * Lqp * kD + idx]) + dqa[3 * Lqp * kD + idx];
     const float val = sum * scale;
     if (nchunks == 1)
@@ -1154,7 +1158,7 @@ __global__ void __launch_bounds__(256, 2) mattn_bwd2_kernel(
   // sum the four waves' register dQ^T into dqa (over the K / V images: zeroed once every wave is past its last
   // block), one wave at a time
   __syncthreads();
-  for (int idx = threadIdx.x; idx < Lqp * kD / 4; idx += 256) reinterpret_cast<f4*>(dqa)[idx] = f4{0.f, 0.f, 0.f, 0.f};
+  for (int idx = threadIdx.x; idx < Lqp * kDQ / 4; idx += 256) reinterpret_cast<f4*>(dqa)[idx] = f4{0.f, 0.f, 0.f, 0.f};
   for (int ww = 0; ww < 4; ++ww) {
     __syncthreads();
     if (w == ww) {
@@ -1164,7 +1168,7 @@ __global__ void __launch_bounds__(256, 2) mattn_bwd2_kernel(
 #pragma unroll
           for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) dqa[(qt * 16 + r) * kD + dt * 16 + 4 * g + i] += dqacc[qt][dt][i];
+            for (int i = 0; i < 4; ++i) dqa[(qt * 16 + r) * kDQ + dt * 16 + 4 * g + i] += dqacc[qt][dt][i];
         }
       }
     }
@@ -1173,7 +1177,7 @@ __global__ void __launch_bounds__(256, 2) mattn_bwd2_kernel(
   const int BH = gridDim.x;
   for (int idx = threadIdx.x; idx < Lq * kD; idx += 256) {
     const int qi = idx / kD, d = idx % kD;
-    const float val = dqa[idx] * scale;
+    const float val = dqa[qi * kDQ + d] * scale;
     if (nchunks == 1)
       dq[(static_cast<int64_t>(b) * Lq + qi) * HD + h * kD + d] = Elt<T>::from_f(val);
     else
@@ -1233,7 +1237,7 @@ size_t bwd_lds_bytes(int Lqp, bool k16, int elt, int dq_copies = 1) {
   size_t bytes = static_cast<size_t>(2 * Lqp + 128) * RS * elt;
   bytes = (bytes + 15) & ~size_t(15);
   bytes += sizeof(float) * (2 * Lqp) + sizeof(uint32_t) * 2 * Lqp + sizeof(float) * 4 * 16 * 17 +
-           sizeof(float) * Lqp * kD * dq_copies;
+           sizeof(float) * (dq_copies == 1 ? Lqp * kDQ : Lqp * kD * dq_copies);
   return bytes;
 }
 
