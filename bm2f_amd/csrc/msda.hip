@@ -1453,7 +1453,7 @@ __device__ __forceinline__ void dpp_add4(unsigned& b1, unsigned& b2, unsigned& b
 }
 
 // The four points of one level for one query: lane j of the quad owns point j (mode md: 0 = skipped (nothing read),
-// 1 = corners in the LDS window at byte offsets a1..a4 (row bases with the half swap), 2 = corners in HBM at byte
+// 1 = corners in the LDS window at byte offsets a1..a4 (first-half bases, win_row), 2 = corners in HBM at byte
 // offsets a1..a4);
 // weights premultiplied by the attention weight, a corner outside the level weighted 0.
 __device__ __forceinline__ void quad_gather_win(const char* __restrict__ vbytes,
@@ -1478,14 +1478,14 @@ __device__ __forceinline__ void quad_gather_win(const char* __restrict__ vbytes,
         v[2] = ldb4(vbytes, b2); v[3] = ldb4(vhi, b2);
         v[4] = ldb4(vbytes, b3); v[5] = ldb4(vhi, b3);
         v[6] = ldb4(vbytes, b4); v[7] = ldb4(vhi, b4);
-      } else if (mq == 1) {  // the other half of a window row is the 64-byte xor (b < 64 within the half)
+      } else if (mq == 1) {  // the second half of a window row is 512 bytes on (an offset field of the read)
         // an address-space-3 load: with generic pointers the compiler merges the two branches' loads into one flat
         // load of a selected 64-bit address
         auto lds4 = [&](unsigned o) { return *(const __attribute__((address_space(3))) f4*)(win + o); };
-        v[0] = lds4(b1); v[1] = lds4(b1 ^ 64u);
-        v[2] = lds4(b2); v[3] = lds4(b2 ^ 64u);
-        v[4] = lds4(b3); v[5] = lds4(b3 ^ 64u);
-        v[6] = lds4(b4); v[7] = lds4(b4 ^ 64u);
+        v[0] = lds4(b1); v[1] = lds4(b1 + 512u);
+        v[2] = lds4(b2); v[3] = lds4(b2 + 512u);
+        v[4] = lds4(b3); v[5] = lds4(b3 + 512u);
+        v[6] = lds4(b4); v[7] = lds4(b4 + 512u);
       }
     };
     load_pt(std::integral_constant<int, 0>{});
@@ -1512,8 +1512,13 @@ __device__ __forceinline__ void quad_gather_win(const char* __restrict__ vbytes,
   batch(std::integral_constant<int, 2>{});
 }
 
-// window row r's LDS byte base (the 64-byte halves swapped when bit 1 of r is set)
-__device__ __forceinline__ unsigned win_row(int r) { return (static_cast<unsigned>(r) << 7) | ((r & 2) << 5); }
+// Window rows in 1 KB blocks of 8 (one LDS-DMA instruction each): row r's first 64-byte half at block (r >> 3), slot
+// r & 7 of the block's first 512 bytes, its second half 512 bytes on.  A quad's 64-byte read of either half lands in
+// bank quarter r & 3, as with the previous in-row half swap (x-adjacent queries at one scale: distinct quarters), and
+// the second half is a constant offset instead of an address xor per corner.  win_row: the first half's byte base.
+__device__ __forceinline__ unsigned win_row(int r) {
+  return (static_cast<unsigned>(r >> 3) << 10) | (static_cast<unsigned>(r & 7) << 6);
+}
 
 // FUSED: the samples come from the projection and the reference points (fe); otherwise (the reference op's
 // interface, m2f_msda_fwd_f32) from materialised sampling locations loc (N, S, M, L, P, 2) and attention weights
@@ -1701,9 +1706,10 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
       const float iww = ww > 0 ? 1.f / static_cast<float>(ww) : 0.f;
       const int nblk = (rows + 7) >> 3;
       for (int blk = wid; blk < nblk; blk += NW) {
-        const int r = min(blk * 8 + (lane >> 3), rows - 1);
+        // lane l fills block slot l: row blk * 8 + ((l >> 2) & 7), 16-byte chunk (l >> 5) * 4 + (l & 3) of it
+        const int r = min(blk * 8 + ((lane >> 2) & 7), rows - 1);
         const int yy = static_cast<int>((static_cast<float>(r) + 0.5f) * iww), xx = r - yy * ww;
-        const unsigned c = static_cast<unsigned>((lane & 7) ^ ((r & 2) << 1));
+        const unsigned c = static_cast<unsigned>(((lane >> 5) << 2) | (lane & 3));
         const unsigned goff = static_cast<unsigned>(mad_u24((wy0 + yy) * W + wx0 + xx, rsb, lbase)) + 16u * c;
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(vbytes + goff),
                                          (__attribute__((address_space(3))) void*)(smem + blk * 1024),
