@@ -74,9 +74,11 @@ def parse_args(argv=None):
     ap.add_argument("--graph", type=int, default=None, choices=[0, 1],
                     help="capture the step in a HIP graph and replay it (default: on for the per-rank configs 4 / 5 "
                          "at one rank, whose small steps are host-launch bound; off for config 2)")
-    ap.add_argument("--channels-last", type=int, default=1, choices=[0, 1],
-                    help="config 2: run the R50 backbone channels-last (MIOpen NHWC kernels, no layout transposes; default: 156.8 vs "
-                         "158.4 ms per step NCHW on one box, profiles/r05_g_bench_cl*.json)")
+    ap.add_argument("--channels-last", type=int, default=None, choices=[0, 1],
+                    help="config 2: run the R50 backbone channels-last (MIOpen NHWC kernels, no layout transposes; 156.8 vs "
+                         "158.4 ms per step NCHW on one box, profiles/r05_g_bench_cl*.json).  Default: on for fp16 autocast, "
+                         "whose NHWC kernels the shipped MIOpen find-db covers; off otherwise (without find-db entries "
+                         "MIOpen's fast find picks NHWC kernels that run the step ~10x slower)")
     ap.add_argument("--allow-knobs", action="store_true")
     ap.add_argument("--master-port", type=int, default=29531)
     a = ap.parse_args(argv)
@@ -539,6 +541,8 @@ def main():
 
     torch.manual_seed(0)
     if args.config == 2:
+        if args.channels_last is None:
+            args.channels_last = int(args.amp == "fp16")
         model = MaskFormerR50(default_cfg(num_queries=args.queries), channels_last=bool(args.channels_last)).to(device)
         g = torch.Generator(device=device).manual_seed(1000 + rank)
         images = torch.randn(args.batch, 3, args.res, args.res, device=device, generator=g) * 57.0 + 117.0
@@ -627,12 +631,16 @@ def main():
             if name == args.amp:
                 continue
             torch.cuda.empty_cache()
+            # the channels-last backbone only under fp16 autocast (the shipped NHWC find-db entries are fp16)
+            cl_mode = bool(args.channels_last) and name == "fp16"
+            model.backbone.channels_last = cl_mode
             el = run(name, args.mode_steps, 2, f"mode {name}")
             key = {"fp16": "amp_fp16", "bf16": "amp_bf16", "none": "fp32_parity"}[name]
             modes[key] = {"value": round(world * args.batch * args.mode_steps / el, 3), "unit": "images/s",
                           "ms_per_step": round(el / args.mode_steps * 1e3, 3), "steps": args.mode_steps, "warmup": 2,
                           "autocast": None if name == "none" else name,
-                          "grad_scaler": name == "fp16"}
+                          "grad_scaler": name == "fp16", "backbone_layout": "channels_last" if cl_mode else "nchw"}
+        model.backbone.channels_last = bool(args.channels_last)
 
     if rank == 0:
         value = world * args.batch * args.steps / elapsed

@@ -315,6 +315,29 @@ def test_masked_attention_bwd_key_tiles_vs_oracle(device, dtype, Q, Lk, keys):
         _masked_attention_case(device, dtype, Q, Lk)
 
 
+@pytest.mark.parametrize("Q,Lk", [(100, 16384), (200, 4096), (100, 1000)])
+def test_masked_attention_xcd_mapping_bitwise(device, Q, Lk):
+    """Option mattn_xcd (the heads of one (image, key chunk) on one XCD, decoder.hip mattn_block) only changes which
+    workgroup computes which (b*h, chunk) tile: output and gradients bitwise equal to the plain mapping."""
+    from bm2f_amd import _native, decoder_ops
+    B, H, C = 2, 8, 256
+    g = torch.Generator(device=device).manual_seed(Q * 7 + Lk)
+    q = torch.randn(B, Q, C, device=device, generator=g).half()
+    k = torch.randn(B, Lk, C, device=device, generator=g).half()
+    v = torch.randn(B, Lk, C, device=device, generator=g).half()
+    bits = _random_bits(B, Q, Lk, device, seed=Q + 1)
+    gout = torch.randn(B, Q, C, device=device, generator=g).half()
+    res = []
+    for xcd in (0, 1):
+        with _native.options(mattn_xcd=xcd):
+            qq, kk, vv = (t.clone().requires_grad_() for t in (q, k, v))
+            out = decoder_ops.masked_attention(qq, kk, vv, bits, H)
+            out.backward(gout)
+            res.append((out.detach(), qq.grad, kk.grad, vv.grad))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def _masked_attention_case(device, dtype, Q, Lk):
     from bm2f_amd import decoder_ops
     B, H, C = 2, 8, 256
