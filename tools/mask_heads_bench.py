@@ -17,9 +17,13 @@ def main():
     ap.add_argument("--queries", type=int, default=100)
     ap.add_argument("--res", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib", default=None, help="another build of libbm2f.so to load (A/B against a baseline build)")
     a = ap.parse_args()
     import torch
-    from bm2f_amd import decoder_ops
+    from bm2f_amd import _native, decoder_ops
+    if a.lib:
+        _native._LIB_PATH = os.path.abspath(a.lib)
+        print("lib:", os.path.basename(a.lib))
     dev = torch.device("cuda")
     B, Q, C, H = a.batch, a.queries, 256, a.res
     g = torch.Generator(device=dev).manual_seed(0)
