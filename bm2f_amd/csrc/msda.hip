@@ -1430,6 +1430,7 @@ constexpr int kFwdLdsThreads = 256;
 constexpr int kFwdLdsRounds = 3;   // queries per workgroup <= 3 * 64
 constexpr int kFwdLdsCap = 416;    // window rows at most: 52 KB + the boxes, three workgroups per CU (145 VGPRs: three
                                    // waves per SIMD; a four-wave build spills 16 registers and measured 0.635 vs 0.60 ms)
+constexpr int kFwdWinRows = kFwdLdsCap - 8;  // window rows the host may ask for: the last 1 KB block is the zero row
 
 // b_i = (quad lane C's a_i) + c for the four corners, as v_add_u32_dpp (hipcc leaves the DPP broadcast and the add
 // apart when the broadcast source comes out of a select).  The s_nop covers the DPP read-after-VALU-write hazard,
@@ -1512,6 +1513,45 @@ __device__ __forceinline__ void quad_gather_win(const char* __restrict__ vbytes,
   batch(std::integral_constant<int, 2>{});
 }
 
+// quad_gather_win when no lane of the wave reads HBM this round and level (the common case): every lane's corners
+// are window rows, a skipped point's the kernel's zero row (zero weights times zeros add +0), so there is no mode
+// broadcast, compare or branch per point
+__device__ __forceinline__ void quad_gather_lds(const __attribute__((address_space(3))) unsigned char* win, unsigned a1,
+                                                unsigned a2, unsigned a3, unsigned a4, float w1, float w2, float w3,
+                                                float w4, unsigned cjb, f4& acc0, f4& acc1) {
+  constexpr int kCtrl[4] = {0x00, 0x55, 0xAA, 0xFF};
+  auto lds4 = [&](unsigned o) { return *(const __attribute__((address_space(3))) f4*)(win + o); };
+  auto batch = [&](auto first) {
+    constexpr int F = decltype(first)::value;
+    f4 va[2][8];
+    auto load_pt = [&](auto pp) {
+      constexpr int I = decltype(pp)::value, C = kCtrl[F + I];
+      unsigned b1, b2, b3, b4;
+      dpp_add4<C>(b1, b2, b3, b4, a1, a2, a3, a4, cjb);
+      f4* v = va[I];
+      v[0] = lds4(b1); v[1] = lds4(b1 + 512u);
+      v[2] = lds4(b2); v[3] = lds4(b2 + 512u);
+      v[4] = lds4(b3); v[5] = lds4(b3 + 512u);
+      v[6] = lds4(b4); v[7] = lds4(b4 + 512u);
+    };
+    load_pt(std::integral_constant<int, 0>{});
+    load_pt(std::integral_constant<int, 1>{});
+    auto fma_pt = [&](auto pp) {
+      constexpr int I = decltype(pp)::value, C = kCtrl[F + I];
+      const float u1 = qpermf<C>(w1), u2 = qpermf<C>(w2), u3 = qpermf<C>(w3), u4 = qpermf<C>(w4);
+      const f4* v = va[I];
+      acc0 += u1 * v[0]; acc1 += u1 * v[1];
+      acc0 += u2 * v[2]; acc1 += u2 * v[3];
+      acc0 += u3 * v[4]; acc1 += u3 * v[5];
+      acc0 += u4 * v[6]; acc1 += u4 * v[7];
+    };
+    fma_pt(std::integral_constant<int, 0>{});
+    fma_pt(std::integral_constant<int, 1>{});
+  };
+  batch(std::integral_constant<int, 0>{});
+  batch(std::integral_constant<int, 2>{});
+}
+
 // Window rows in 1 KB blocks of 8 (one LDS-DMA instruction each): row r's first 64-byte half at block (r >> 3), slot
 // r & 7 of the block's first 512 bytes, its second half 512 bytes on.  A quad's 64-byte read of either half lands in
 // bank quarter r & 3, as with the previous in-row half swap (x-adjacent queries at one scale: distinct quarters), and
@@ -1535,6 +1575,8 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
   const int cap = geo.max_rows;  // window rows in use (a multiple of 8, <= kFwdLdsCap)
   int4* bbw = reinterpret_cast<int4*>(smem + kFwdLdsCap * 128);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, j = lane & 3;
+  // the zero row (window row kFwdWinRows, beyond every window): the LDS-only gather's skipped points read it
+  if (tid < 64) reinterpret_cast<f4*>(smem + kFwdWinRows * 128)[tid] = f4{0.f, 0.f, 0.f, 0.f};   // before any barrier
   // block -> (image, tile, head), the head fastest: XCD x (blocks are dealt round-robin) gathers one head's rows
   int b = blockIdx.x;
   const int m = b % M;
@@ -1729,10 +1771,19 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
       const int r1 = (y0 - wy0) * ww + (x0 - wx0), r3 = r1 + (ey ? ww : 0);
       const unsigned g1 = static_cast<unsigned>(mad_u24(mad_u24(y0, W, x0), rsb, lbase));
       const unsigned dx = ex ? rsb : 0u, dy = ey ? static_cast<unsigned>(W * rsb) : 0u;
-      const unsigned a1 = inwin ? win_row(r1) : g1, a2 = inwin ? win_row(r1 + ex) : g1 + dx;
-      const unsigned a3 = inwin ? win_row(r3) : g1 + dy, a4 = inwin ? win_row(r3 + ex) : g1 + dy + dx;
       const int md = ok ? (inwin ? 1 : 2) : 0;
-      quad_gather_win(vbytes, (const __attribute__((address_space(3))) unsigned char*)smem, md, a1, a2, a3, a4, gw[r][0], gw[r][1], gw[r][2], gw[r][3], cjb, acc0[r], acc1[r]);
+      const auto* win = (const __attribute__((address_space(3))) unsigned char*)smem;
+      // wave-uniform: window rows only (the op-level build, FUSED = false, keeps the general path: with both it spills)
+      if (FUSED && !__any(md == 2)) {
+        constexpr unsigned kZ = kFwdWinRows * 128u;   // win_row(kFwdWinRows): the zero row
+        const unsigned w1 = inwin ? win_row(r1) : kZ, w2 = inwin ? win_row(r1 + ex) : kZ;
+        const unsigned w3 = inwin ? win_row(r3) : kZ, w4 = inwin ? win_row(r3 + ex) : kZ;
+        quad_gather_lds(win, w1, w2, w3, w4, gw[r][0], gw[r][1], gw[r][2], gw[r][3], cjb, acc0[r], acc1[r]);
+      } else {
+        const unsigned a1 = inwin ? win_row(r1) : g1, a2 = inwin ? win_row(r1 + ex) : g1 + dx;
+        const unsigned a3 = inwin ? win_row(r3) : g1 + dy, a4 = inwin ? win_row(r3 + ex) : g1 + dy + dx;
+        quad_gather_win(vbytes, win, md, a1, a2, a3, a4, gw[r][0], gw[r][1], gw[r][2], gw[r][3], cjb, acc0[r], acc1[r]);
+      }
       if constexpr (!FUSED) asm volatile("" ::: "memory");  // one round's gather at a time (else the scheduler
                                                              // overlaps rounds and spills)
     }
@@ -2117,7 +2168,7 @@ bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeo
   geo.nty = (geo.H[fi] + th - 1) / th;
   geo.ntx = (geo.W[fi] + tw - 1) / tw;
   geo.max_halo = std::max(0, m2f::option(m2f::kOptMsdaFwdHalo, 8));
-  const int cap = std::min(m2f::option(m2f::kOptMsdaFwdCap, kFwdLdsCap), kFwdLdsCap) & ~7;
+  const int cap = std::min(m2f::option(m2f::kOptMsdaFwdCap, kFwdWinRows), kFwdWinRows) & ~7;
   int qt = 0, own = 0;
   for (int l = 0; l < d.L; ++l) {
     const int h = (geo.H[l] + geo.nty - 1) / geo.nty, w = (geo.W[l] + geo.ntx - 1) / geo.ntx;

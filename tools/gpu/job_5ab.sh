@@ -1,0 +1,16 @@
+# MSDA forward: LDS-only gather when no lane of the wave reads HBM (skipped points read a zero row kept in the
+# window's last 1 KB block: window rows <= 408): MSDA tests (bitwise vs the quad kernel, oracle parity, non-finite
+# values), then an alternating A/B of the forward against the previous build
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest tests/test_msda_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r5ab_tests.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest tests/test_scale_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread -k "fused" >> gpurun_out/r5ab_tests.log 2>&1 || exit 1
+B="$GRAFT_REPO_ROOT/tools/lib/libbm2f_base.so"
+for i in 1 2; do
+  timeout -k 10 120 python3 tools/msda_bench.py --fused --fwd-only --lib "$B" >> gpurun_out/r5ab_mb.txt 2>&1 || exit 1
+  timeout -k 10 120 python3 tools/msda_bench.py --fused --fwd-only >> gpurun_out/r5ab_mb.txt 2>&1 || exit 1
+  timeout -k 10 120 python3 tools/msda_bench.py --fused --fwd-only --noise 4 --lib "$B" >> gpurun_out/r5ab_mb.txt 2>&1 || exit 1
+  timeout -k 10 120 python3 tools/msda_bench.py --fused --fwd-only --noise 4 >> gpurun_out/r5ab_mb.txt 2>&1 || exit 1
+  timeout -k 10 120 python3 tools/msda_bench.py --fwd-only --lib "$B" >> gpurun_out/r5ab_mb.txt 2>&1 || exit 1
+  timeout -k 10 120 python3 tools/msda_bench.py --fwd-only >> gpurun_out/r5ab_mb.txt 2>&1 || exit 1
+done
