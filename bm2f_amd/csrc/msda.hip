@@ -1767,19 +1767,20 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
       const int ey = (fl >> 1) & 1, ex = (fl >> 2) & 1;
       const bool ok = fl & 1;
       const bool inwin = ok && y0 >= wy0 && y0 + ey <= wy1 && x0 >= wx0 && x0 + ex <= wx1;
-      // both address forms, then a select (straight-line code keeps the broadcasts foldable into v_add_u32_dpp)
-      const int r1 = (y0 - wy0) * ww + (x0 - wx0), r3 = r1 + (ey ? ww : 0);
-      const unsigned g1 = static_cast<unsigned>(mad_u24(mad_u24(y0, W, x0), rsb, lbase));
-      const unsigned dx = ex ? rsb : 0u, dy = ey ? static_cast<unsigned>(W * rsb) : 0u;
       const int md = ok ? (inwin ? 1 : 2) : 0;
       const auto* win = (const __attribute__((address_space(3))) unsigned char*)smem;
       // wave-uniform: window rows only (the op-level build, FUSED = false, keeps the general path: with both it spills)
       if (FUSED && !__any(md == 2)) {
-        constexpr unsigned kZ = kFwdWinRows * 128u;   // win_row(kFwdWinRows): the zero row
-        const unsigned w1 = inwin ? win_row(r1) : kZ, w2 = inwin ? win_row(r1 + ex) : kZ;
-        const unsigned w3 = inwin ? win_row(r3) : kZ, w4 = inwin ? win_row(r3 + ex) : kZ;
-        quad_gather_lds(win, w1, w2, w3, w4, gw[r][0], gw[r][1], gw[r][2], gw[r][3], cjb, acc0[r], acc1[r]);
+        // a skipped point's corners all on the zero row (row index kFwdWinRows, no +1 row / column)
+        const int q1 = inwin ? (y0 - wy0) * ww + (x0 - wx0) : kFwdWinRows;
+        const int qx = inwin ? ex : 0, q3 = q1 + (inwin && ey ? ww : 0);
+        quad_gather_lds(win, win_row(q1), win_row(q1 + qx), win_row(q3), win_row(q3 + qx), gw[r][0], gw[r][1],
+                        gw[r][2], gw[r][3], cjb, acc0[r], acc1[r]);
       } else {
+        // both address forms, then a select (straight-line code keeps the broadcasts foldable into v_add_u32_dpp)
+        const int r1 = (y0 - wy0) * ww + (x0 - wx0), r3 = r1 + (ey ? ww : 0);
+        const unsigned g1 = static_cast<unsigned>(mad_u24(mad_u24(y0, W, x0), rsb, lbase));
+        const unsigned dx = ex ? rsb : 0u, dy = ey ? static_cast<unsigned>(W * rsb) : 0u;
         const unsigned a1 = inwin ? win_row(r1) : g1, a2 = inwin ? win_row(r1 + ex) : g1 + dx;
         const unsigned a3 = inwin ? win_row(r3) : g1 + dy, a4 = inwin ? win_row(r3 + ex) : g1 + dy + dx;
         quad_gather_win(vbytes, win, md, a1, a2, a3, a4, gw[r][0], gw[r][1], gw[r][2], gw[r][3], cjb, acc0[r], acc1[r]);
