@@ -1552,6 +1552,21 @@ __device__ __forceinline__ void quad_gather_lds(const __attribute__((address_spa
   batch(std::integral_constant<int, 2>{});
 }
 
+// wave-wide min / max by DPP (no LDS round trips, unlike __shfl_xor's ds_bpermute): the four intra-row steps leave
+// every lane with its 16-lane row's result, row_bcast:15 / :31 fold the rows into lane 63, read out uniformly
+template <bool MAX>
+__device__ __forceinline__ int wave_minmax(int v) {
+  constexpr int id = MAX ? INT_MIN : INT_MAX;
+  auto op = [](int a, int b) { return MAX ? max(a, b) : min(a, b); };
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0xB1, 0xF, 0xF, false));    // quad_perm [1,0,3,2]
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x4E, 0xF, 0xF, false));    // quad_perm [2,3,0,1]
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x141, 0xF, 0xF, false));   // row_half_mirror
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x140, 0xF, 0xF, false));   // row_mirror
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x142, 0xA, 0xF, false));   // row_bcast:15 into rows 1, 3
+  v = op(v, __builtin_amdgcn_update_dpp(id, v, 0x143, 0xC, 0xF, false));   // row_bcast:31 into rows 2, 3
+  return __builtin_amdgcn_readlane(v, 63);
+}
+
 // Window rows in 1 KB blocks of 8 (one LDS-DMA instruction each): row r's first 64-byte half at block (r >> 3), slot
 // r & 7 of the block's first 512 bytes, its second half 512 bytes on.  A quad's 64-byte read of either half lands in
 // bank quarter r & 3, as with the previous in-row half swap (x-adjacent queries at one scale: distinct quarters), and
@@ -1718,11 +1733,8 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
     };
     if (FUSED && ((W & (W - 1)) | (H & (H - 1))) == 0) geometry(std::true_type{});
     else geometry(std::false_type{});
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      bmin_y = min(bmin_y, __shfl_xor(bmin_y, o)); bmax_y = max(bmax_y, __shfl_xor(bmax_y, o));
-      bmin_x = min(bmin_x, __shfl_xor(bmin_x, o)); bmax_x = max(bmax_x, __shfl_xor(bmax_x, o));
-    }
+    bmin_y = wave_minmax<false>(bmin_y); bmax_y = wave_minmax<true>(bmax_y);
+    bmin_x = wave_minmax<false>(bmin_x); bmax_x = wave_minmax<true>(bmax_x);
     if (lane == 0) bbw[l * NW + wid] = make_int4(bmin_y, bmax_y, bmin_x, bmax_x);
     __syncthreads();  // the boxes are in; every wave is done reading the previous level's window
     // 2. the window: the box clipped to the tile +- halo, the halo shrinking until the rows fit (uniform)
