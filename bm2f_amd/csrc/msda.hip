@@ -1077,7 +1077,7 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
     auto next_unit = [&]() {
       int nb = 0;
       if (lane == 0) nb = atomicAdd(&ts.next_batch, 1);
-      return __shfl(nb, 0);
+      return __builtin_amdgcn_readlane(nb, 0);   // lane 0's value, uniform (not an LDS permute round trip)
     };
     if constexpr (OVERLAP) {
       // R phase-2 units per phase-3 unit while phase 2 lasts (msda_bwd_ratio, default 1), then the rest of phase 3:
