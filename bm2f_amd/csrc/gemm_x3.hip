@@ -657,16 +657,17 @@ int nt_impl(const char* fn, const float* A, int64_t lda, const float* B, int64_t
                   (bits_out ? kBitsOut : 0) | (bits_in ? kBitsIn : 0);
   uint32_t* bits = bits_out ? bits_out : const_cast<uint32_t*>(bits_in);
   if (bits) ldm = ldbits;
-  // 96-wide columns of 4 waves for N = 3 * 96 k (the 288-wide sampling projection), else 128-wide columns
-  // of 8 waves (256 rows share one B chunk: 0.285 vs 0.321 ms at K = N = 256, 0.913 vs 0.949 at K = 1024,
-  // equal at N = 1024; tools/gemm_x3_bench.py, r2af)
-  int cfg = (N % 128 != 0 && N % 96 == 0) ? 1 : 3;
+  // 96-wide columns for N = 3 * 96 k (the 288-wide sampling projection), else 128-wide columns; 8 waves either
+  // way (256 rows share one B chunk: 128-wide 0.285 vs 0.321 ms at K = N = 256, 0.913 vs 0.949 at K = 1024, equal
+  // at N = 1024, tools/gemm_x3_bench.py, r2af; 96-wide 0.385 -> 0.365 ms at N = 288, profiles/r05_ah_x3_nt_cfg.txt)
+  int cfg = (N % 128 != 0 && N % 96 == 0) ? 4 : 3;
   cfg = m2f::option(m2f::kOptX3NtCfg, cfg);
   switch (cfg) {
     case 0: return launch_nt<128, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
     case 1: return launch_nt<96, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
     case 2: return launch_nt<256, 4>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
     case 3: return launch_nt<128, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
+    case 4: return launch_nt<96, 8>(epi, A, lda, Bs, NP, bias, mask, ldm, D1, D2, ldd, dper, bits, C, ldc, M, N, K, st);
     default: return m2f::fail(M2F_EINVAL, "%s: config %d", fn, cfg);
   }
 }
