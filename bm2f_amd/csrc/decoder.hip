@@ -548,6 +548,54 @@ __global__ void __launch_bounds__(256) mattn_combine_kernel(const float* __restr
   if (part == 0) lse2[row] = L > 0.f ? M + log2f(L) : INFINITY;
 }
 
+// Combine with one wave per (b*h, q): lane = 8 g + part, chunk group g takes chunks g, g + 8, ... with an online
+// merge of (max, sum, 4 channels), then the 8 groups merge across lanes. The per-thread form above walks the chunks
+// one after another (two passes of nchunks loads): with few rows (config 4's B = 2) it is latency-bound.
+__device__ __forceinline__ void merge_part(float& m, float& l, f4& acc, float m2, float l2, const f4& a2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -INFINITY) return;
+  const float w1 = exp2f(m - mn), w2 = exp2f(m2 - mn);
+  l = l * w1 + l2 * w2;
+  acc = acc * w1 + a2 * w2;
+  m = mn;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) mattn_combine_wave_kernel(const float* __restrict__ ws_o,
+                                                                 const float* __restrict__ ws_ml, int nchunks, int BH,
+                                                                 int H, int Lq, T* __restrict__ out,
+                                                                 float* __restrict__ lse2) {
+  const int64_t row = blockIdx.x * 4ll + (threadIdx.x >> 6);   // bh * Lq + q, wave-uniform
+  if (row >= static_cast<int64_t>(BH) * Lq) return;
+  const int lane = threadIdx.x & 63, g = lane >> 3, part = lane & 7;
+  float m = -INFINITY, l = 0.f;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c = g; c < nchunks; c += 8) {
+    const int64_t prow = static_cast<int64_t>(c) * BH * Lq + row;
+    const float2 ml = *reinterpret_cast<const float2*>(ws_ml + 2 * prow);
+    merge_part(m, l, acc, ml.x, ml.y, *reinterpret_cast<const f4*>(ws_o + prow * kD + part * 4));
+  }
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+    const float m2 = __shfl_xor(m, o), l2 = __shfl_xor(l, o);
+    f4 a2;
+    for (int i = 0; i < 4; ++i) a2[i] = __shfl_xor(acc[i], o);
+    merge_part(m, l, acc, m2, l2, a2);
+  }
+  if (g != 0) return;
+  const int bh = static_cast<int>(row / Lq), qi = static_cast<int>(row % Lq);
+  const int b = bh / H, h = bh % H;
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  acc *= inv;
+  T* orow = out + (static_cast<int64_t>(b) * Lq + qi) * (H * kD) + h * kD + part * 4;
+  if constexpr (Elt<T>::k16) {
+    *reinterpret_cast<s4*>(orow) = pack4<T>(acc[0], acc[1], acc[2], acc[3]);
+  } else {
+    *reinterpret_cast<f4*>(orow) = acc;
+  }
+  if (part == 0) lse2[row] = l > 0.f ? m + log2f(l) : INFINITY;
+}
+
 // ----------------------------------------------------------------------------------------------
 // 3. masked attention backward
 // ----------------------------------------------------------------------------------------------
@@ -1297,8 +1345,18 @@ int mattn_fwd_impl(const char* fn, const void* q, const void* k, const void* v, 
     mattn_fwd_kernel<T, 8><<<grid, 256, 0, st>>>(qq, kk, vv, bits, Lq, Lk, H, qs, kvs, nw, sl2, chunk, oo, lse2, ws_o, ws_ml, xm);
   int rc = m2f::check_launch(fn);
   if (rc || nch == 1) return rc;
-  const int64_t total = static_cast<int64_t>(B) * H * Lq * (kD / 4);
-  mattn_combine_kernel<T><<<m2f::ceil_div(total, 256), 256, 0, st>>>(ws_o, ws_ml, nch, B * H, H, Lq, oo, lse2);
+  // option mattn_combine: 0 = one thread per (row, 4 channels), 1 = one wave per row; default: the wave form from 16
+  // chunks up or when the thread form would fill fewer than 256 workgroups (config 4, B = 2: 15.4 -> 5.9 us at 32
+  // chunks, 5.1 -> 4.2 us at 8; config 2's 12,800 rows x 8 chunks stay on the thread form, 5.6 vs 7.5 us;
+  // profiles/r05_al_mattn_combine_ab.txt)
+  const int64_t rows = static_cast<int64_t>(B) * H * Lq;
+  const int cmb = m2f::option(m2f::kOptMattnCombine, -1);
+  if (cmb == 1 || (cmb != 0 && (nch >= 16 || rows * (kD / 4) < 256 * 256))) {
+    mattn_combine_wave_kernel<T><<<m2f::ceil_div(rows, 4), 256, 0, st>>>(ws_o, ws_ml, nch, B * H, H, Lq, oo, lse2);
+  } else {
+    const int64_t total = rows * (kD / 4);
+    mattn_combine_kernel<T><<<m2f::ceil_div(total, 256), 256, 0, st>>>(ws_o, ws_ml, nch, B * H, H, Lq, oo, lse2);
+  }
   return m2f::check_launch(fn);
 }
 

@@ -349,7 +349,8 @@ int m2f_maxpool3s2_nhwc(int backward, const void* src, void* dst, uint8_t* windo
  * msda_bwd_ratio, msda_bwd_det, msda_fwd_lds, msda_fwd_tile, msda_fwd_tile_w, msda_fwd_cap, msda_fwd_halo (MSDA
  * partitions, variants, LDS windows, deterministic mode), mattn_dq_atomic, mattn_fwd_minblk, mattn_bwd_minblk,
  * mattn_bwd_keys, mattn_xcd (masked-attention dQ variant, key blocks per workgroup at least, keys per wave in the
- * backward: 32 or 16, the heads of one image and key chunk on one XCD: 1 or 0), mask_df_stage (mask-einsum feature
+ * backward: 32 or 16, the heads of one image and key chunk on one XCD: 1 or 0), mattn_combine (forward chunk
+ * combine: a thread per row part 0, a wave per row 1), mask_df_stage (mask-einsum feature
  * gradient: k-steps per LDS stage, 4 or 1), gemm_nt_cfg, x3_tn_nw, x3_tn_blocks,
  * x3_nt_cfg (GEMM tilings).  Every option changes
  * the partition or kernel variant only; results agree to fp32 rounding (summation order may differ between

@@ -338,6 +338,36 @@ def test_masked_attention_xcd_mapping_bitwise(device, Q, Lk):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("dtype", [torch.float16, torch.float32])
+@pytest.mark.parametrize("Q,Lk", [(200, 4096), (200, 16384), (100, 16384), (1, 4097), (37, 1000)])
+@pytest.mark.parametrize("combine", [0, 1])
+def test_masked_attention_combine_vs_oracle(device, dtype, Q, Lk, combine):
+    """The forward's chunk combine one thread per (row, 4 channels) (mattn_combine 0) and one wave per row with the
+    8 chunk groups merged across lanes (1, the default from 16 chunks or few rows: config 4's B = 2)."""
+    from bm2f_amd import _native
+    with _native.options(mattn_combine=combine):
+        _masked_attention_case(device, dtype, Q, Lk)
+
+
+@pytest.mark.parametrize("Q,Lk", [(200, 4096), (100, 16384)])
+def test_masked_attention_combine_sparse_chunks(device, Q, Lk):
+    """Rows whose keys are almost all blocked (whole key chunks without a visible key: partial max -inf, sum 0):
+    both combine forms give the same output and LSE up to fp32 rounding."""
+    from bm2f_amd import _native, decoder_ops
+    B, H, C = 2, 8, 256
+    g = torch.Generator(device=device).manual_seed(Q + 3 * Lk)
+    q = torch.randn(B, Q, C, device=device, generator=g).half()
+    k = torch.randn(B, Lk, C, device=device, generator=g).half()
+    v = torch.randn(B, Lk, C, device=device, generator=g).half()
+    bits = _random_bits(B, Q, Lk, device, seed=Q + 5, p_block=0.9995)
+    outs = []
+    for combine in (0, 1):
+        with _native.options(mattn_combine=combine):
+            outs.append(decoder_ops.masked_attention(q, k, v, bits, H).float())
+    assert torch.isfinite(outs[1]).all()
+    torch.testing.assert_close(outs[1], outs[0], rtol=2e-3, atol=2e-3)
+
+
 def _masked_attention_case(device, dtype, Q, Lk):
     from bm2f_amd import decoder_ops
     B, H, C = 2, 8, 256

@@ -13,7 +13,7 @@ import sys
 
 CASES = [("config 2", 1024), ("config 2", 4096), ("config 2", 16384),
          ("config 4", 1024), ("config 4", 4096), ("config 4", 16384)]
-FAMILIES = (("fwd", "mattn_fwd_kernel"), ("combine", "mattn_combine_kernel"), ("bwd", "mattn_bwd"),
+FAMILIES = (("fwd", "mattn_fwd_kernel"), ("combine", "mattn_combine"), ("bwd", "mattn_bwd"),
             ("dq_reduce", "mattn_dq_reduce_kernel"))
 
 
@@ -33,7 +33,8 @@ def levels(path):
         fam = family(name)
         if fam is None:
             continue
-        case = min(nfwd // 46, len(CASES) - 1)
+        # every other kernel follows the forward launch it belongs to
+        case = min((nfwd if fam == "fwd" else max(nfwd - 1, 0)) // 46, len(CASES) - 1)
         if fam == "fwd":
             nfwd += 1
         per.setdefault((case, fam), []).append(dur / 1e3)
