@@ -24,6 +24,11 @@ Besides the contract fields it reports:
                 entry carries its fraction of the spec peak (frac) and of the measured one (frac_achievable).
   cpu_baseline  the reference's CPU path (oracle/cpu_path.py) on config 1 (1 x 512^2) and one 1024^2 image,
                 warm-up 1, median of 3, rank 0, N=1; value = the 1024^2 img/s.
+  world_seen / ranks_agree / rank_check
+                the process group's size as RCCL saw it (dist.get_world_size()), and whether every replica holds
+                bitwise-equal parameters after the timed steps (per-parameter checksums of the raw words,
+                all-gathered: bench_model.rank_consistency), with each rank's ms/step and their min / max -- so
+                a config-3 run (--gpus 8) carries its own evidence that DDP kept the ranks in step.
   env           every M2F_* variable in the environment.  The bench refuses to run with any set (they select
                 non-default engines or geometries); --allow-knobs permits them for experiments.
 """
@@ -533,8 +538,8 @@ def main():
     device = torch.device("cuda", local)
 
     from bm2f_amd import _native
-    from bm2f_amd.bench_model import (GraphStep, HeadBench, MaskFormerR50, default_cfg, head_features, make_optimizer,
-                                      make_scaler, train_step, wrap_ddp)
+    from bm2f_amd.bench_model import (GraphMemsetError, GraphStep, HeadBench, MaskFormerR50, default_cfg, head_features, make_optimizer,
+                                      make_scaler, rank_consistency, train_step, wrap_ddp)
 
     timer = KernelTimer()
     timer.install(_native)
@@ -567,16 +572,14 @@ def main():
         scaler = make_scaler(amp)
         t0 = time.perf_counter()
         if graph:   # warm-up steps run eagerly inside the capture helper, then the captured step is replayed
-            gstep = GraphStep(model, opt, images, amp, scaler=scaler, warmup=max(warmup, 2))
-            graph_info["nodes"] = gstep.nodes
-            log(f"{tag} warmup {warmup} + capture done ({time.perf_counter() - t0:.1f}s), nodes {gstep.nodes}")
-            if gstep.nodes.get("memset") and os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
-                log(f"{tag}: the captured step holds memset nodes, which packet capture replays wrongly: eager steps")
-                graph_info["fallback"] = "memset nodes under packet capture: eager steps"
+            try:
+                step_fn = GraphStep(model, opt, images, amp, scaler=scaler, warmup=max(warmup, 2))
+                graph_info["nodes"] = step_fn.nodes
+                log(f"{tag} warmup {warmup} + capture done ({time.perf_counter() - t0:.1f}s), nodes {step_fn.nodes}")
+            except GraphMemsetError as e:   # memset nodes replay wrongly under packet capture
+                log(f"{tag}: {e}: eager steps")
+                graph_info.update(nodes=e.nodes, fallback="memset nodes under packet capture: eager steps")
                 graph = False
-                del gstep
-            else:
-                step_fn = gstep
         if not graph:
             def step_fn():
                 return train_step(model, opt, images, amp, scaler=scaler)
@@ -596,14 +599,29 @@ def main():
         barrier()
         elapsed = time.perf_counter() - start
         if world > 1:
-            t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = t.item()
+            ts = [torch.zeros(1, device=device, dtype=torch.float64) for _ in range(world)]
+            dist.all_gather(ts, torch.tensor([elapsed], device=device, dtype=torch.float64))
+            per_rank = [float(t) for t in ts]
+            elapsed = max(per_rank)     # the job's time: the slowest rank
+        else:
+            per_rank = [elapsed]
+        rank_times[tag] = per_rank
         log(f"{tag}: {steps} steps in {elapsed:.3f}s")
         return elapsed
 
     graph_info = {}
+    rank_times = {}
     elapsed = run(args.amp, args.steps, args.warmup, "timed", graph=use_graph)
+    # config 3 checks itself: after the timed steps every replica must hold bitwise-equal parameters (a parameter
+    # DDP failed to reduce, or a rank that fell out of step, shows here), and the process group must be the size
+    # the launcher asked for
+    consistency = rank_consistency(model)
+    consistency["rank_ms_per_step"] = [round(t / args.steps * 1e3, 3) for t in rank_times["timed"]]
+    consistency["step_ms_min"] = min(consistency["rank_ms_per_step"])
+    consistency["step_ms_max"] = max(consistency["rank_ms_per_step"])
+    consistency["backend"] = dist.get_backend() if world > 1 else None
+    if not consistency["ranks_agree"]:
+        log(f"ranks disagree after the timed steps: {consistency['mismatched_params']} parameters differ")
     use_graph = use_graph and "fallback" not in graph_info
     peaks = None
     if world == 1 and not args.no_peaks:
@@ -691,6 +709,8 @@ def main():
                        "backbone_layout": "channels_last" if args.channels_last else "nchw"},
             "roofline": roof, "roofline_all": roof_all, "achievable": peaks, "modes": modes, "cpu_baseline": cpu,
             "msda_op_dropin": dropin,
+            "world_seen": consistency["world_seen"], "ranks_agree": consistency["ranks_agree"],
+            "rank_check": consistency,
         }
         if args.config in (4, 5):
             line.update(head_config_line(args, world, value, knobs))

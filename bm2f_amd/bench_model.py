@@ -4,15 +4,17 @@ Mirrors the reference's training forward (maskformer_model.py:258-320, mask_form
 with the criterion replaced by the sum of means of every head's outputs (the
 Hungarian matcher / weak-supervision losses are outside the hot path).  The backbone is
 detectron2's R50 as configured by the reference (Base-COCO-*.yaml: depth 50, STRIDE_IN_1X1 False,
-FrozenBN, FREEZE_AT 0, res2..res5), written here in plain PyTorch (MIOpen convs, NCHW: channels-last measured 20x slower in the
-backward under MIOPEN_FIND_MODE=FAST) since
-detectron2 / torchvision are absent; FrozenBN is folded into the conv weights on the fly (same
-function, one op fewer per conv).  Optimizer: AdamW + full-model grad-norm clipping
+FrozenBN, FREEZE_AT 0, res2..res5), written here in plain PyTorch (MIOpen convs) since detectron2 / torchvision
+are absent.  It runs NCHW or channels-last (``ResNet50(channels_last=True)``: MIOpen's NHWC kernels, no layout
+transposes); bench.py picks channels-last under fp16 autocast, whose NHWC kernels the shipped MIOpen find-db covers
+(without find-db entries MIOpen's FAST find mode picks NHWC kernels ~10x slower, so NCHW elsewhere).  FrozenBN is
+folded into the conv weights on the fly (same function, one op fewer per conv).  Optimizer: AdamW + full-model grad-norm clipping
 (train_net.py:185-263, SOLVER: BASE_LR 1e-4, WEIGHT_DECAY 0.05, CLIP_VALUE 0.01).
 """
 from __future__ import annotations
 
 import ctypes
+import os
 import types
 
 import torch
@@ -372,6 +374,49 @@ def wrap_ddp(model, device=None):
     return torch.nn.parallel.DistributedDataParallel(model, **kw)
 
 
+def param_digest(model):
+    """Per-parameter bit checksums, int64 (n_params,): the sum of each parameter's raw 32-bit words (16-bit
+    parameters are widened first).  Two replicas hold bitwise-equal parameters only if these agree, so comparing
+    them across ranks checks that data parallelism kept every replica in step (train_net.py:328 launches one
+    replica per GPU; DDP's all-reduce must leave them identical)."""
+    out = []
+    for p in model.parameters():
+        t = p.detach()
+        if t.element_size() != 4:
+            t = t.float()
+        out.append(t.contiguous().view(torch.int32).to(torch.int64).sum())
+    return torch.stack(out) if out else torch.zeros(0, dtype=torch.int64)
+
+
+def rank_consistency(model, elapsed=None):
+    """All-gather :func:`param_digest` (and each rank's timed-loop seconds) over the default process group.
+    Returns {"world_seen", "ranks_agree", "mismatched_params", "step_s_min", "step_s_max"}; at world size 1 (no
+    process group) the trivially consistent record of this process alone."""
+    import torch.distributed as dist
+    dig = param_digest(model)
+    if not (dist.is_available() and dist.is_initialized()):
+        rec = {"world_seen": 1, "ranks_agree": True, "mismatched_params": 0}
+        if elapsed is not None:
+            rec.update(step_s_min=elapsed, step_s_max=elapsed)
+        return rec
+    world = dist.get_world_size()
+    dev = dig.device if dist.get_backend() == "gloo" else next(model.parameters()).device
+    dig = dig.to(dev)
+    allg = [torch.empty_like(dig) for _ in range(world)]
+    dist.all_gather(allg, dig)
+    bad = torch.zeros(dig.numel(), dtype=torch.bool, device=dev)
+    for d in allg[1:]:
+        bad |= d != allg[0]
+    rec = {"world_seen": world, "ranks_agree": not bool(bad.any()), "mismatched_params": int(bad.sum())}
+    if elapsed is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        ts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(ts, t)
+        vals = [float(x) for x in ts]
+        rec.update(step_s_min=min(vals), step_s_max=max(vals))
+    return rec
+
+
 def graph_safe_sum(x):
     """``x.sum(dtype=float32)`` as dim-wise reductions over rows of at most 1024 elements, repeated until one
     remains: torch's single-output reduction of a large tensor zeroes its cross-block semaphores with a memset, and
@@ -482,6 +527,14 @@ def graph_node_counts(graph):
     return counts
 
 
+class GraphMemsetError(RuntimeError):
+    """A captured step holds memset nodes while graph packet capture is on (see :class:`GraphStep`)."""
+
+    def __init__(self, msg, nodes):
+        super().__init__(msg)
+        self.nodes = nodes
+
+
 class GraphStep:
     """The whole training step -- forward, loss, backward, GradScaler unscale / inf check, gradient clipping and
     the fused AdamW (capturable: its step counter lives on the device) -- captured once as a HIP graph
@@ -491,7 +544,12 @@ class GraphStep:
     torch's current stream (the capture stream), and nothing in the step reads a device value on the host (host
     spatial shapes are tagged up front, GradScaler hands found_inf to the fused optimizer).  Warm-up steps run
     eagerly on a side stream first (lazy state, MIOpen find-db, workspaces), as torch's whole-network capture
-    recipe prescribes."""
+    recipe prescribes.
+
+    Replay correctness: with the ROCm runtime's graph packet capture on (its default, unless
+    ``DEBUG_CLR_GRAPH_PACKET_CAPTURE=0`` was set before HIP started) a captured memset is not re-run correctly on
+    later replays.  The constructor counts the captured node kinds (``nodes``) and raises
+    :class:`GraphMemsetError` instead of returning a graph that would replay wrong sums."""
 
     def __init__(self, model, opt, images, amp_dtype, scaler=None, warmup=3, debug_dump=None, sdpa_math=False):
         from torch.nn.attention import SDPBackend, sdpa_kernel
@@ -516,6 +574,11 @@ class GraphStep:
             self.graph.debug_dump(debug_dump)
         # node kinds (kernel / memcpy / memset ...): a memset node replays wrongly under the runtime's packet capture
         self.nodes = graph_node_counts(self.graph)
+        if self.nodes.get("memset") and os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") != "0":
+            raise GraphMemsetError(
+                f"the captured step holds {self.nodes['memset']} memset node(s), which the ROCm runtime's graph packet "
+                "capture replays wrongly (tools/graph_memset_check.py): set DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 before HIP "
+                "starts, or run the step eagerly", self.nodes)
         self.graph.instantiate()
 
     def __call__(self):

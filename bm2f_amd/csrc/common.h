@@ -54,6 +54,11 @@ int64_t option_raw(Option o);  // -1 when unset
 // graph is not re-run correctly when the graph is replayed (tools/graph_memset_check.py), and callers capture the
 // library's launches in graphs (bench_model.GraphStep).  Returns a HIP error code.
 hipError_t zero_async(void* p, size_t bytes, hipStream_t st);
+// The same for a rows x cols fp32 matrix at row stride ld floats (a kernel: no memset node in a captured graph).
+hipError_t zero2d_f32_async(float* p, int64_t ld, int64_t cols, int64_t rows, hipStream_t st);
+// Raise `kernel`'s dynamic-LDS limit to `bytes` on the current device, once per (kernel, device, bytes) and
+// thread-safe; returns M2F_OK or an M2F_ELAUNCH status (with the HIP error in last_error) naming `fn`.
+int set_max_lds(const void* kernel, int bytes, const char* fn);
 inline int option(Option o, int dflt) {
   const int64_t v = option_raw(o);
   return v < 0 ? dflt : static_cast<int>(v);

@@ -606,6 +606,10 @@ int conv_impl(const char* fn, const void* I, int i_dtype, int i_nhwc, const floa
   if (!m2f::aligned(O, 16) || !m2f::aligned(workspace, 16) || (i_nhwc && !m2f::aligned(I, 16)))
     return m2f::fail(M2F_EINVAL, "%s: misaligned", fn);
   const int Ca = mode == 0 ? Ci : Co, Nn = mode == 0 ? Co : Ci;
+  // the 16-bit / NHWC epilogues store 8 output channels per 16-byte write, guarded per group start only: the
+  // output channel count must be whole 16-channel groups (conv_check validates the A operand's channels only)
+  if ((i16 || o16 || i_nhwc || o_nhwc) && Nn % 16)
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: 16-bit / NHWC operands need output channels %% 16 == 0 (got %d)", fn, Nn);
   if (workspace_bytes < conv_ws(Ca, Nn, T)) return m2f::fail(M2F_EINVAL, "%s: workspace too small", fn);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int NP = (Nn + 255) / 256 * 256, nchunks = T * Ca / kBK;

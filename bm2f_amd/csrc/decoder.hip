@@ -1394,13 +1394,7 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
   if constexpr (Elt<T>::k16) {
     if (mode == 1 && m2f::option(m2f::kOptMattnBwdKeys, 32) == 32) {
       const size_t lds2 = bwd2_lds_bytes(Lqp, sizeof(T));
-      static bool attr2[2] = {false, false};
-      const int ai2 = std::is_same<T, __bf16>::value ? 0 : 1;
-      if (!attr2[ai2]) {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mattn_bwd2_kernel<T, 8>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        attr2[ai2] = true;
-      }
+      if (int rc = m2f::set_max_lds(reinterpret_cast<const void*>(&mattn_bwd2_kernel<T, 8>), 160 * 1024, fn)) return rc;
       mattn_bwd2_kernel<T, 8><<<dim3(B * H, nch), 256, lds2, st>>>(
           static_cast<const T*>(q), static_cast<const T*>(k), static_cast<const T*>(v), bits,
           static_cast<const T*>(out), static_cast<const T*>(dout), lse2, Lq, Lk, H, qs, kvs, nw, scale * kLog2e, scale,
@@ -1416,14 +1410,7 @@ int mattn_bwd_impl(const char* fn, const void* q, const void* k, const void* v, 
               : mode == 3 ? &mattn_bwd_kernel<T, 13>
               : mode == 2 ? &mattn_bwd_kernel<T, -1>
                           : &mattn_bwd_kernel<T, 0>;
-  static bool attr_set[3][4] = {{false, false, false, false}, {false, false, false, false}, {false, false, false, false}};
-  const int ai = std::is_same<T, float>::value ? 0 : (std::is_same<T, __bf16>::value ? 1 : 2);
-  const int ki = mode;
-  if (!attr_set[ai][ki]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
-    attr_set[ai][ki] = true;
-  }
+  if (int rc = m2f::set_max_lds(reinterpret_cast<const void*>(kern), 160 * 1024, fn)) return rc;
   const dim3 grid(B * H, nch);
   kern<<<grid, 256, lds, st>>>(
       static_cast<const T*>(q), static_cast<const T*>(k), static_cast<const T*>(v), bits, static_cast<const T*>(out),

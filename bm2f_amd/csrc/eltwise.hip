@@ -10,6 +10,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <set>
+#include <tuple>
 
 namespace {
 
@@ -775,6 +778,13 @@ __global__ void __launch_bounds__(256) zero16_kernel(uint4* __restrict__ p, size
 __global__ void __launch_bounds__(256) zero1_kernel(unsigned char* __restrict__ p, size_t n) {
   for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += static_cast<size_t>(gridDim.x) * 256) p[i] = 0;
 }
+// rows x cols floats at row stride ld (floats): one grid-stride pass over the rows x cols elements
+__global__ void __launch_bounds__(256) zero2d_f32_kernel(float* __restrict__ p, int64_t ld, int64_t cols, int64_t n) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int64_t r = i / cols;
+    p[r * ld + (i - r * cols)] = 0.f;
+  }
+}
 }  // namespace
 
 namespace m2f {
@@ -790,5 +800,32 @@ hipError_t zero_async(void* p, size_t bytes, hipStream_t st) {
   }
   if (tail) zero1_kernel<<<1, 256, 0, st>>>(b + head + n16 * 16, tail);
   return hipGetLastError();
+}
+
+hipError_t zero2d_f32_async(float* p, int64_t ld, int64_t cols, int64_t rows, hipStream_t st) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if (ld == cols) return zero_async(p, static_cast<size_t>(rows * cols) * sizeof(float), st);
+  const int64_t n = rows * cols;
+  const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+  zero2d_f32_kernel<<<static_cast<unsigned>(blocks), 256, 0, st>>>(p, ld, cols, n);
+  return hipGetLastError();
+}
+
+int set_max_lds(const void* kernel, int bytes, const char* fn) {
+  // one hipFuncSetAttribute per (kernel, device, limit), thread-safe; the attribute is per device, so a process that
+  // launches on several devices sets it on each
+  static std::mutex mu;
+  static std::set<std::tuple<const void*, int, int>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return fail(M2F_ELAUNCH, "%s: hipGetDevice failed", fn);
+  std::lock_guard<std::mutex> lock(mu);
+  const auto key = std::make_tuple(kernel, dev, bytes);
+  if (done.count(key)) return M2F_OK;
+  const hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  if (e != hipSuccess)
+    return fail(M2F_ELAUNCH, "%s: hipFuncSetAttribute(MaxDynamicSharedMemorySize = %d) on device %d: %s", fn, bytes, dev,
+                hipGetErrorString(e));
+  done.insert(key);
+  return M2F_OK;
 }
 }  // namespace m2f

@@ -764,8 +764,7 @@ extern "C" int m2f_gemm_f32x3_tn(const float* A, int64_t lda, const float* B, in
     return m2f::ok();
   }
   // M == 0: C = 0, colsum = 0
-  if (hipMemset2DAsync(C, static_cast<size_t>(ldc) * 4, 0, static_cast<size_t>(N2) * 4, N1, st) != hipSuccess)
-    return m2f::fail(M2F_ELAUNCH, "%s: memset", fn);
+  if (m2f::zero2d_f32_async(C, ldc, N2, N1, st) != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: zero fill", fn);
   if (colsum && m2f::zero_async(colsum, static_cast<size_t>(N1) * 4, st) != hipSuccess)
     return m2f::fail(M2F_ELAUNCH, "%s: memset", fn);
   return m2f::ok();

@@ -1717,7 +1717,9 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
         gw[r][0] = (vy0 && vx0) ? hy * hx * a : 0.f;
         gw[r][1] = (vy0 && vx1) ? hy * lx * a : 0.f;
         gw[r][2] = (vy1 && vx0) ? ly * hx * a : 0.f;
-        gw[r][3] = (vy1 && vx1) ? ly * lx * a : 0.f;
+        // a skipped point (hs = ws = -2) has vy0 = vx0 = false, so only corner 4 needs ok: its LDS-only gather still
+        // runs the FMAs (on the zero row), and 0 * 0 * a would carry a NaN weight into the output
+        gw[r][3] = (ok && vy1 && vx1) ? ly * lx * a : 0.f;
         gy[r] = y0;
         gx[r] = x0;
         gfl[r] = (ok ? 1 : 0) | (ey << 1) | (ex << 2);
@@ -1983,63 +1985,60 @@ struct DetBufs {
 };
 
 template <int LT, bool FUSED, int TPB>
-void launch_tiled_t(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                    const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, const DetBufs& det,
-                    hipStream_t st) {
-  static bool attr = false;  // one flag per instantiation
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB, false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<LT, FUSED, TPB, true, true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
-    attr = true;
-  }
+int launch_tiled_t(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                   const TileGeom& geo, size_t lds, const Dims& d, float* gv, float* gl, float* ga, const DetBufs& det,
+                   hipStream_t st) {
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
-  if (det.acc)
-    msda_bwd_f32_tiled<LT, FUSED, TPB, true, true><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv,
-                                                                           gl, ga, det.acc, det.scale);
-  else if (m2f::option(m2f::kOptMsdaBwdOverlap, 1) != 0)
-    msda_bwd_f32_tiled<LT, FUSED, TPB, true><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
-  else
-    msda_bwd_f32_tiled<LT, FUSED, TPB, false><<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga);
+  const char* fn = "msda tiled backward";
+  constexpr int kLds = 160 * 1024 - 512;
+  if (det.acc) {
+    auto* k = &msda_bwd_f32_tiled<LT, FUSED, TPB, true, true>;
+    if (int rc = m2f::set_max_lds(reinterpret_cast<const void*>(k), kLds, fn)) return rc;
+    k<<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga, det.acc, det.scale, nullptr);
+  } else if (m2f::option(m2f::kOptMsdaBwdOverlap, 1) != 0) {
+    auto* k = &msda_bwd_f32_tiled<LT, FUSED, TPB, true>;
+    if (int rc = m2f::set_max_lds(reinterpret_cast<const void*>(k), kLds, fn)) return rc;
+    k<<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga, nullptr, nullptr, nullptr);
+  } else {
+    auto* k = &msda_bwd_f32_tiled<LT, FUSED, TPB, false>;
+    if (int rc = m2f::set_max_lds(reinterpret_cast<const void*>(k), kLds, fn)) return rc;
+    k<<<grid, TPB, lds, st>>>(value, loc, attn, fe, gout, geo, d.S, d.M, gv, gl, ga, nullptr, nullptr, nullptr);
+  }
+  return M2F_OK;
 }
 
 template <int LT, bool FUSED>
-void launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                  const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                  const DetBufs& det, hipStream_t st) {
+int launch_tiled(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                 const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
+                 const DetBufs& det, hipStream_t st) {
   if constexpr (LT < 4) {
-    if (threads == 1024) {
-      launch_tiled_t<LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
-      return;
-    }
+    if (threads == 1024) return launch_tiled_t<LT, FUSED, 1024>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
   }
-  launch_tiled_t<LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
+  return launch_tiled_t<LT, FUSED, 512>(value, loc, attn, fe, gout, geo, lds, d, gv, gl, ga, det, st);
 }
 
+// M2F status of the launch (an LDS-attribute failure returns before the kernel is launched)
 template <bool FUSED>
-void launch_tiled_levels(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
-                         const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
-                         hipStream_t st, const DetBufs& det = DetBufs{}) {
+int launch_tiled_levels(const float* value, const float* loc, const float* attn, const FrontEnd& fe, const float* gout,
+                        const TileGeom& geo, size_t lds, int threads, const Dims& d, float* gv, float* gl, float* ga,
+                        hipStream_t st, const DetBufs& det = DetBufs{}) {
   switch (d.L) {
-    case 1: launch_tiled<1, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st); break;
-    case 2: launch_tiled<2, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st); break;
-    case 3: launch_tiled<3, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st); break;
-    default: launch_tiled<4, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st); break;
+    case 1: return launch_tiled<1, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st);
+    case 2: return launch_tiled<2, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st);
+    case 3: return launch_tiled<3, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st);
+    default: return launch_tiled<4, FUSED>(value, loc, attn, fe, gout, geo, lds, threads, d, gv, gl, ga, det, st);
   }
 }
 
-bool launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,
-                      const int64_t* host_shapes, float* gv, float* gl, float* ga, hipStream_t st) {
-  if (m2f::option(m2f::kOptMsdaBwdTiled, 1) == 0) return false;
+// -1: the tiled kernel does not apply (the caller takes another kernel); else the M2F status of its launch
+int launch_bwd_tiled(const float* value, const float* loc, const float* attn, const float* gout, const Dims& d,
+                     const int64_t* host_shapes, float* gv, float* gl, float* ga, hipStream_t st) {
+  if (m2f::option(m2f::kOptMsdaBwdTiled, 1) == 0) return -1;
   TileGeom geo;
   size_t lds;
   int threads;
-  if (!make_tile_geom(d, host_shapes, geo, lds, threads)) return false;
-  launch_tiled_levels<false>(value, loc, attn, FrontEnd{}, gout, geo, lds, threads, d, gv, gl, ga, st);
-  return true;
+  if (!make_tile_geom(d, host_shapes, geo, lds, threads)) return -1;
+  return launch_tiled_levels<false>(value, loc, attn, FrontEnd{}, gout, geo, lds, threads, d, gv, gl, ga, st);
 }
 
 template <typename T>
@@ -2055,7 +2054,9 @@ int bwd_impl(const char* fn, const T* value, const int64_t* shapes, const int64_
   bool done = false;
   if constexpr (std::is_same<T, float>::value) {
     if (fast_f32_ok(d, value, loc, gout) && m2f::aligned(gv, 16) && m2f::aligned(gl, 8)) {
-      if (launch_bwd_tiled(value, loc, attn, gout, d, host_shapes, gv, gl, ga, st)) done = true;
+      const int trc = launch_bwd_tiled(value, loc, attn, gout, d, host_shapes, gv, gl, ga, st);
+      if (trc > 0) return trc;
+      if (trc == 0) done = true;
       else if (d.D == 16) launch_bwd_vec<16>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
       else if (d.D == 32) launch_bwd_vec<32>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
       else launch_bwd_vec<64>(value, shapes, lsi, loc, attn, gout, d, gv, gl, ga, st);
@@ -2374,8 +2375,9 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
     const int64_t n4 = static_cast<int64_t>(d.N) * d.Lq * d.M * d.D / 4;  // grad_output (N, Lq, M*32) fp32
     msda_det_scale_kernel<<<2048, 256, 0, st>>>(reinterpret_cast<const float4*>(grad_output), n4, det.scale);
   }
-  launch_tiled_levels<true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value, grad_proj,
-                            nullptr, st, det);
+  if (int trc = launch_tiled_levels<true>(value, nullptr, nullptr, fe, grad_output, geo, lds, threads, d, grad_value,
+                                          grad_proj, nullptr, st, det))
+    return trc;
   if (det.acc)
     msda_det_convert_kernel<<<4096, 256, 0, st>>>(reinterpret_cast<const long long*>(det.acc), nval, d.Lq, det.scale,
                                                   grad_value);

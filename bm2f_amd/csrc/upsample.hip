@@ -338,10 +338,12 @@ extern "C" int m2f_upsample2x_add_fwd_nhwc_f32(const float* src, int64_t sN, con
   const char* fn = "m2f_upsample2x_add_fwd_nhwc_f32";
   if (!src || !lateral || !out) return m2f::fail(M2F_EINVAL, "%s: null pointer", fn);
   if (N < 0 || C <= 0 || h <= 0 || w <= 0) return m2f::fail(M2F_EINVAL, "%s: bad sizes", fn);
-  if (C % kUpCT || w > kUpMaxW || sN % 4 || sN < static_cast<int64_t>(h) * w * C || !m2f::aligned(src, 16) ||
+  // the output rows are stored as float4s of 2w columns: w must be even (an odd w would leave the last two
+  // columns of every row unwritten and misalign the odd rows' vector accesses)
+  if (C % kUpCT || w % 2 || w > kUpMaxW || sN % 4 || sN < static_cast<int64_t>(h) * w * C || !m2f::aligned(src, 16) ||
       !m2f::aligned(lateral, 16) || !m2f::aligned(out, 16))
-    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs C %% %d == 0, w <= %d, sN %% 4 == 0, sN >= h*w*C and 16-byte aligned "
-                     "buffers", fn, kUpCT, kUpMaxW);
+    return m2f::fail(M2F_EUNSUPPORTED, "%s: needs C %% %d == 0, even w <= %d, sN %% 4 == 0, sN >= h*w*C and 16-byte "
+                     "aligned buffers", fn, kUpCT, kUpMaxW);
   const int64_t nblk = static_cast<int64_t>(N) * 2 * h * (C / kUpCT);
   if (nblk == 0) return m2f::ok();
   if (nblk > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many blocks", fn);

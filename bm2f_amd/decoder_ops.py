@@ -551,20 +551,24 @@ class _SavedLike:
 class GradSink:
     """The fp32 gradient of one memory-token tensor that several :func:`token_linear_sink` calls read (the K and V
     projections of the 3 decoder layers on one level): each call's input gradient -- the autocast-dtype GEMM result,
-    as the reference's per-call cast backward sees it -- is kept, and the call whose backward runs last sums them in
-    fp32 in arrival order in one pass (m2f_sum_to_f32: the values of a cast of the first and an fp32 add of each
-    further one, without re-reading and re-writing the fp32 sum per call) and hands the sum to autograd; the others
-    return no input gradient.  Autograd's path casts every call's gradient to fp32 and adds the fp32 tensors.  One
-    sink per tensor and forward."""
+    as the reference's per-call cast backward sees it -- is kept, and the call whose backward completes the set sums
+    them in fp32 in arrival order in one pass (m2f_sum_to_f32: the values of a cast of the first and an fp32 add of
+    each further one, without re-reading and re-writing the fp32 sum per call) and hands the sum to autograd; the
+    others return no input gradient.  Autograd's path casts every call's gradient to fp32 and adds the fp32 tensors.
+    One sink per tensor and forward.
+
+    ``count`` is the number of graph-recording calls, fixed by the forward and never consumed: every backward pass
+    over the graph (a second ``backward(retain_graph=True)``, a second ``autograd.grad``) collects its own ``count``
+    terms and gets its own complete sum.  Calls made without gradient recording (the no-grad first pass of a
+    reentrant activation checkpoint) are not counted, so the recompute's calls are."""
 
     def __init__(self):
         self.terms = []
-        self.pending = 0
+        self.count = 0
 
     def add(self, g):
         self.terms.append(g)
-        self.pending -= 1
-        if self.pending:
+        if len(self.terms) < self.count:
             return None
         terms, self.terms = self.terms, []
         return sum_to_f32(terms)
@@ -599,7 +603,6 @@ class _TokenLinearSink(Function):
         ctx.has_bias = bias is not None
         ctx.sink = sink
         ctx.x_shape = x.shape
-        sink.pending += 1
         return F.linear(x_lp, weight, bias)
 
     @staticmethod
@@ -628,6 +631,8 @@ def token_linear_sink(x, weight, bias, x_lp, sink):
     dt = x_lp.dtype
     weight = weight.to(dt)
     bias = bias.to(dt) if bias is not None else None
+    if torch.is_grad_enabled() and x.requires_grad:
+        sink.count += 1      # a call whose backward will deliver a term (see GradSink)
     with torch.autocast("cuda", enabled=False):
         return _TokenLinearSink.apply(x, x_lp, weight, bias, sink)
 

@@ -410,7 +410,7 @@ int m2f_upsample2x_add_fwd_f32(const float* src, int64_t sN, int64_t sC, int64_t
 int m2f_upsample2x_bwd_f32(const float* grad_out, float* grad_src, int N, int C, int h, int w, void* stream);
 /* Channels-last coarse map (the encoder's (N, HW, C) output seen as (N, C, h, w); msdeformattn.py:335-349): src is
  * (N, h, w, C) with batch stride sN elements (sN >= h*w*C, a multiple of 4: the level's slice of the (N, S, C) encoder
- * output), grad_src (N, h, w, C) contiguous, lateral / out / grad_out NCHW; C % 64 == 0, w <= 256 (bwd: w even); same
+ * output), grad_src (N, h, w, C) contiguous, lateral / out / grad_out NCHW; C % 64 == 0, even w <= 256; same
  * taps, products and summation order as the NCHW pair above.  Replace the transposing copy before the forward and the
  * mixed-layout gradient sum after the backward. */
 int m2f_upsample2x_add_fwd_nhwc_f32(const float* src, int64_t sN, const float* lateral, float* out, int N, int C, int h,

@@ -239,3 +239,41 @@ def test_gemm_nt_relu_bits(device, M, N, K, b_kn):
         got = linear_ops.gemm_nt_bits(g, w2, bits_in=bits)
         want = linear_ops.gemm_nt(g, w2, mask=h)
     assert torch.equal(got, want)
+
+
+def test_x3_tn_zero_rows_graph_capture_no_memset(device):
+    """The x3 TN GEMM over M = 0 rows writes C = 0 (and colsum = 0) with the library's fill kernels: captured in a
+    HIP graph it leaves no memset node (memsets replay wrongly under the runtime's graph packet capture), a strided C
+    keeps its padding columns, and every replay re-zeroes C."""
+    import ctypes
+    from bm2f_amd import _native
+    from bm2f_amd.bench_model import graph_node_counts
+    N1, N2, ldc = 40, 48, 64
+    dummy = torch.zeros(4, device=device)
+    C = torch.full((N1, ldc), 7.0, device=device)
+    cs = torch.full((N1,), 7.0, device=device)
+    wsb = ctypes.c_int64(0)
+    _native.call("m2f_gemm_f32x3_tn_workspace", 0, N1, N2, ctypes.byref(wsb))
+    ws = torch.empty(max(wsb.value, 16), device=device, dtype=torch.uint8)
+
+    def run():
+        _native.call("m2f_gemm_f32x3_tn", dummy.data_ptr(), ctypes.c_int64(N1), dummy.data_ptr(), ctypes.c_int64(N2),
+                     C.data_ptr(), ctypes.c_int64(ldc), cs.data_ptr(), 0, N1, N2, ws.data_ptr(),
+                     ctypes.c_int64(ws.numel()), torch.cuda.current_stream().cuda_stream)
+    run()
+    torch.cuda.synchronize()
+    assert (C[:, :N2] == 0).all() and (C[:, N2:] == 7).all() and (cs == 0).all()
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            run()
+    nodes = graph_node_counts(g)
+    assert not nodes.get("memset"), nodes
+    g.instantiate()
+    for _ in range(2):
+        C.fill_(7.0)
+        cs.fill_(7.0)
+        g.replay()
+        torch.cuda.synchronize()
+        assert (C[:, :N2] == 0).all() and (C[:, N2:] == 7).all() and (cs == 0).all()

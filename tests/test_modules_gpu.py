@@ -143,3 +143,33 @@ def test_decoder_amp_cast_once_matches_per_layer_casts(device, monkeypatch):
         for a, b in zip(res[mode][1], res["per_layer"][1]):
             assert rel_err(a.cpu(), b.cpu().numpy()) < 1e-5
         assert rel_err(res[mode][2].cpu(), res["per_layer"][2].cpu().numpy()) < 1e-5
+
+
+def test_decoder_sink_two_backward_passes(device, monkeypatch):
+    """The memory-gradient sink is complete on every backward pass over one graph: two
+    ``backward(retain_graph=True)`` calls give each input twice the gradient of one pass, and one pass equals the
+    plain autograd-sum path (sink_memory_grads False)."""
+    from bm2f_amd.transformer_decoder import MultiScaleMaskedTransformerDecoder as Dec
+    torch.manual_seed(0)
+    d = build_decoder().to(device)
+    x0 = [torch.randn(2, 256, s, s, device=device) for s in (4, 8, 16)]
+    mf0 = torch.randn(2, 256, 32, 32, device=device)
+    grads = {}
+    for mode in ("sink", "plain"):
+        if mode == "plain":
+            monkeypatch.setattr(Dec, "sink_memory_grads", False)
+        x = [t.clone().requires_grad_() for t in x0]
+        mf = mf0.clone().requires_grad_()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = d(x, mf)
+            loss = sum(h["pred_masks"].float().square().mean() + h["pred_logits"].float().square().mean()
+                       for h in [out] + out["aux_outputs"])
+        loss.backward(retain_graph=True)
+        one = [t.grad.clone() for t in x]
+        loss.backward()
+        grads[mode] = (one, [t.grad for t in x])
+    for a, b in zip(grads["sink"][0], grads["sink"][1]):
+        assert a.abs().max() > 0
+        assert rel_err(b.cpu(), (2 * a).cpu().numpy()) < 1e-6, "the second backward pass lost the sink's sum"
+    for a, b in zip(grads["sink"][0], grads["plain"][0]):
+        assert rel_err(a.cpu(), b.cpu().numpy()) < 1e-5

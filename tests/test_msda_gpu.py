@@ -401,3 +401,36 @@ def test_fused_backward_variants_vs_oracle(device, shapes, quad):
     from test_scale_gpu import fused_fwd_bwd_vs_oracle
     with _native.options(msda_bwd_overlap=quad, msda_fwd_quad=quad):
         fused_fwd_bwd_vs_oracle(device, shapes, N=2, far=0.05, seed=31 + len(shapes))
+
+
+@pytest.mark.parametrize("lds", [1, 0])
+def test_fused_forward_nan_weights_on_skipped_points(device, lds):
+    """A (query, head) whose every point lies outside its level adds nothing, whatever its attention weights hold:
+    the reference kernel tests the sample position before it touches the weight (ms_deform_im2col_cuda.cuh:257-262),
+    so NaN logits on such a row give a zero output.  Both the LDS-window forward (whose LDS-only gather runs the FMAs
+    of skipped points on a zero row: the weights must be zeroed, not multiplied by 0) and the quad kernel."""
+    from bm2f_amd import _native
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    from test_scale_gpu import _fused_case
+    shapes = [(32, 32), (64, 64), (128, 128)]
+    N, M, L, P = 2, 8, 3, 4
+    value, proj, ref = _fused_case(shapes, N, 0.0, seed=5)
+    S = value.shape[1]
+    off = proj[..., :M * L * P * 2].view(N, S, M, L, P, 2)
+    logit = proj[..., M * L * P * 2:].view(N, S, M, L * P)
+    rows = [(0, 7, 3), (0, 1500, 0), (1, 20000, 5), (1, 21000, 7)]   # (image, query, head), all three levels
+    for n, q, m in rows:
+        off[n, q, m] = 1e5
+        logit[n, q, m] = float("nan")
+    args = (value.to(device), proj.to(device), ref.float()[None, :, None, :].expand(N, S, L, 2).to(device),
+            tuple(shapes), P)
+    with _native.options(msda_fwd_lds=lds):
+        out = MSDeformAttnFusedFunction.apply(*args)
+    torch.cuda.synchronize()
+    out = out.cpu().view(N, S, M, 32)
+    assert torch.isfinite(out).all(), "a skipped point's NaN weight reached the output"
+    for n, q, m in rows:
+        assert (out[n, q, m] == 0).all()
+    with _native.options(msda_fwd_lds=1 - lds):
+        other = MSDeformAttnFusedFunction.apply(*args).cpu().view(N, S, M, 32)
+    assert torch.equal(out, other)
