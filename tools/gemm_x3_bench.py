@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--cfgs", default="0,2,3", help="x3_nt_cfg option values to time")
     ap.add_argument("--lib", default=None, help="another build of libbm2f.so (A/B)")
     ap.add_argument("--x3-only", action="store_true", help="time only the x3 engine (A/B runs)")
+    ap.add_argument("--tn-nw", default="", help="x3_tn_nw option values to time the wgrad with, e.g. 4,41")
+    ap.add_argument("--shapes", default="256x256,256x288,256x1024,1024x256", help="KxN forward shapes")
     a = ap.parse_args()
     if a.lib:
         from bm2f_amd import _native as _nat
@@ -40,7 +42,7 @@ def main():
     dev = torch.device("cuda")
     torch.manual_seed(0)
     sub = slice(0, 4096)
-    for (K, N) in [(256, 256), (256, 288), (256, 1024), (1024, 256)]:
+    for (K, N) in [tuple(int(v) for v in sh.split("x")) for sh in a.shapes.split(",")]:
         x = torch.randn(M, K, device=dev)
         w = torch.randn(N, K, device=dev) / K ** 0.5
         b = torch.randn(N, device=dev)
@@ -83,6 +85,14 @@ def main():
             dw, db = linear_ops.gemm_tn(g, x, colsum=True, engine=eng)
             res[eng] = (timeit(lambda: linear_ops.gemm_tn(g, x, colsum=True, engine=eng)), rel(dw, ref))
             res[eng + "_bias"] = (0.0, rel(db, refb))
+        for rnd, nw in enumerate([v for v in a.tn_nw.split(",") if v]):
+            _native.set_option("x3_tn_nw", int(nw))
+            try:
+                dw, db = linear_ops.gemm_tn(g, x, colsum=True, engine="x3")
+                res[f"nw{nw}.{rnd}"] = (timeit(lambda: linear_ops.gemm_tn(g, x, colsum=True, engine="x3")), rel(dw, ref))
+                res[f"nw{nw}_bias.{rnd}"] = (0.0, rel(db, refb))
+            finally:
+                _native.set_option("x3_tn_nw", -1)
         print(f"wgrad M={M} N1={N} N2={K}: " + "  ".join(f"{k} {t:.3f}ms {fl / max(t, 1e-9) / 1e9:.0f}TF err {e:.1e}" for k, (t, e) in res.items()), flush=True)
         del x, w, g
 
