@@ -45,14 +45,15 @@ def unpack_bits(bits, n):
 
 
 def ref_masked_attention(q, k, v, blocked, num_heads, scale=None):
-    """q (B,Lq,C), k/v (B,Lk,C), blocked (B,Lq,Lk) bool -> (B,Lq,C); computed in fp32."""
+    """q (B,Lq,C), k/v (B,Lk,C), blocked (B,Lq,Lk) bool -> (B,Lq,C); computed in fp32 (fp64 for fp64 inputs)."""
     B, Lq, C = q.shape
     Lk = k.shape[1]
     d = C // num_heads
     scale = 1.0 / math.sqrt(d) if scale is None else scale
-    qh = q.float().view(B, Lq, num_heads, d).transpose(1, 2)
-    kh = k.float().view(B, Lk, num_heads, d).transpose(1, 2)
-    vh = v.float().view(B, Lk, num_heads, d).transpose(1, 2)
+    ct = torch.float64 if q.dtype == torch.float64 else torch.float32
+    qh = q.to(ct).view(B, Lq, num_heads, d).transpose(1, 2)
+    kh = k.to(ct).view(B, Lk, num_heads, d).transpose(1, 2)
+    vh = v.to(ct).view(B, Lk, num_heads, d).transpose(1, 2)
     s = (qh * scale) @ kh.transpose(-1, -2)
     s = s.masked_fill(blocked[:, None], float("-inf"))
     p = s.softmax(-1)
