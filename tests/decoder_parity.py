@@ -9,7 +9,14 @@ Three runs of one decoder module on the same inputs and loss (sum over the heads
    mask2former_transformer_decoder.py:363-452 (and the video decoder's :365-474) evaluated in fp64.  Every attention
    mask it hands a cross-attention layer (and the logits it came from) is recorded;
 2. the same reference semantics in fp32 on the GPU, every layer given run 1's masks: the reference's own fp32
-   arithmetic, whose distance from run 1 is the noise floor the bars below scale with;
+   arithmetic, whose distance from run 1 is the noise floor the bars below scale with.  Run twice, with the
+   self-attention's SDPA on torch's default backend and on its MATH backend: two equally valid fp32 evaluations of the
+   reference, and the floor is the larger of their distances.  (Why two: at config 5 a layer-0 FFN pre-activation
+   sits within fp32 rounding of 0, so some fp32 evaluations flip its ReLU against fp64 -- the MATH-backend reference
+   and the HIP path do, the default-backend reference happens not to -- and the flip moves one hidden unit's row of
+   linear1's weight gradient and, through it, the query embeddings' gradients by up to 4.5e-3 of their max: the same
+   discrete event as a mask bit at the sigmoid threshold, tools/decoder_parity_diag.py,
+   profiles/r06_g_decoder_parity_diag.txt.)
 3. the HIP path (masked-attention kernels, the attention-mask kernel, the fp32 GEMM / einsum paths) in fp32, every
    layer given run 1's masks (teacher forcing: free-running, a logit within fp32 rounding of the sigmoid threshold
    flips a mask bit and that query's row then follows a different mask through the later layers -- a divergence that
@@ -18,8 +25,8 @@ Three runs of one decoder module on the same inputs and loss (sum over the heads
    threshold (|fp64 resized logit| below 1e-5 of its row's largest).
 
 Bars (the pixel decoder's rule, tests/test_scale_gpu.py::test_pixdec_config2_full_size_vs_reference_math): every
-tensor -- outputs, input gradients and every parameter gradient -- within max(1e-3, 2 x run 2's distance from run 1)
-of run 1, in both metrics (max |a - b| / max |b| and ||a - b|| / ||b||); outputs within 1e-3 outright
+tensor -- outputs, input gradients and every parameter gradient -- within max(1e-3, 2 x run 2's larger distance from
+run 1) of run 1, in both metrics (max |a - b| / max |b| and ||a - b|| / ||b||); outputs within 1e-3 outright
 (north_star's fp32 bar)."""
 import contextlib
 import copy
@@ -110,7 +117,10 @@ def decoder_parity(dec, xs, mf, device, hip=True, log=None, bit_tol=1e-5):
             return bits.to(logits.device)
         return hook
 
+    from torch.nn.attention import SDPBackend, sdpa_kernel
     ref32 = _run(dec, xs, mf, True, forced_hook(None))
+    with sdpa_kernel([SDPBackend.MATH]):
+        ref32m = _run(dec, xs, mf, True, forced_hook(None))
     own = []
     got = _run(dec, xs, mf, not hip, forced_hook(own))
     assert set(got) == set(want) == set(ref32), (set(want) ^ set(got))
@@ -137,11 +147,12 @@ def decoder_parity(dec, xs, mf, device, hip=True, log=None, bit_tol=1e-5):
     for k in sorted(want):
         assert got[k].shape == want[k].shape, k
         e_max, e_norm = _errs(got[k], want[k])
-        r_max, r_norm = _errs(ref32[k], want[k])
+        (d_max, d_norm), (m_max, m_norm) = _errs(ref32[k], want[k]), _errs(ref32m[k], want[k])
+        r_max, r_norm = max(d_max, m_max), max(d_norm, m_norm)
         bar, bar_n = max(1e-3, 2 * r_max), max(1e-3, 2 * r_norm)
         ok = e_max <= bar and e_norm <= bar_n and (not k.startswith("out_") or e_max < 1e-3)
-        lines.append(f"{k:64s} hip max {e_max:.2e} norm {e_norm:.2e} | ref-fp32 max {r_max:.2e} norm {r_norm:.2e}"
-                     f" | bars {bar:.1e} / {bar_n:.1e} {'ok' if ok else 'FAIL'}")
+        lines.append(f"{k:64s} hip max {e_max:.2e} norm {e_norm:.2e} | ref-fp32 max {d_max:.2e} / {m_max:.2e} norm "
+                     f"{d_norm:.2e} / {m_norm:.2e} | bars {bar:.1e} / {bar_n:.1e} {'ok' if ok else 'FAIL'}")
         if not ok:
             bad.append(k)
     n_tight = sum(1 for k in want if _errs(got[k], want[k])[0] < 1e-3)

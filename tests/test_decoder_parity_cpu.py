@@ -57,7 +57,7 @@ def test_decoder_parity_harness_detects_a_wrong_path(monkeypatch):
     def skewed(q, k, v, blocked, num_heads, scale=None):
         calls["n"] += 1
         out = real(q, k, v, blocked, num_heads, scale)
-        return out * 1.01 if q.dtype == torch.float32 and calls["n"] > 6 else out   # the third run only
+        return out * 1.01 if q.dtype == torch.float32 and calls["n"] > 9 else out   # the last run only
     monkeypatch.setattr(decoder_ref, "ref_masked_attention", skewed)
     _, bad, _, _ = decoder_parity(dec, xs, mf, "cpu", hip=False)
     assert bad
