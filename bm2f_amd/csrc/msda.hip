@@ -43,7 +43,7 @@ constexpr const char* kOptionNames[m2f::kOptCount] = {
     "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap",
     "msda_bwd_det", "msda_fwd_pb", "msda_bwd_ratio", "msda_fwd_lds", "msda_fwd_tile", "msda_fwd_tile_w",
     "msda_fwd_cap", "msda_fwd_halo", "mattn_fwd_minblk", "mattn_bwd_minblk", "mask_df_stage",
-    "mattn_bwd_keys", "mattn_xcd", "mattn_combine"};
+    "mattn_bwd_keys", "mattn_xcd", "mattn_combine", "msda_bwd_rowsort"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -371,7 +371,11 @@ struct TileState {
   int H[kTileMaxL], W[kTileMaxL], start[kTileMaxL];  // the level shapes in LDS: a kernarg array indexed by a
   float invW[kTileMaxL], invH[kTileMaxL];            // per-lane level is a global load per use
   int next_batch;            // phase-3 row batches handed out dynamically
+  int rbin[64];              // row sort: rows per record-count bin, then the bins' start positions
 };
+// the tiled backward's dynamic LDS (<= 156 KB, make_tile_geom) plus this static block within the CU's 160 KB, and
+// within the 160 KB - 1 KB the launcher raises the dynamic limit to
+static_assert(sizeof(TileState) <= 1024, "TileState must leave the dynamic LDS its 159 KB");
 
 // g rows in LDS: query qi's 16-byte chunk c (float offset)
 __device__ __forceinline__ int g_chunk_off(int qi, int c) { return qi * 32 + 4 * c; }
@@ -541,6 +545,7 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
   for (int i = tid; i < (nsamp_max + 31) / 32; i += blockDim.x) oow[i] = 0u;
   for (int i = tid; i <= geo.max_rows; i += blockDim.x) cstart[i] = 0;  // the sort's counters (any window fits)
   if (tid == 0) ts.next_batch = kBwdWaves;
+  if (tid < 64) ts.rbin[tid] = 0;
   __syncthreads();
   if (tid == 0) {
     ts.qc[0] = 0;
@@ -819,6 +824,55 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
     }
     __syncthreads();
   }
+  // ---- phase-3 rows in order of their record count, heaviest first -------------------------------------------------
+  // A phase-3 unit is 16 rows walked in lockstep by the wave's 4-lane groups, so it takes as long as its longest list;
+  // in window order neighbouring rows' lists differ several-fold (the lists of a 16-row unit averaged 0.43 of its
+  // longest at config 2 near-init, a host count).  A counting sort over 64 bins of 4 records each deals units of rows
+  // with lists of nearly equal length.  The permutation lives in the high halves of cstart's words (every cstart value
+  // is < 2^16; rows_total <= cells_total), read by phase 3 with 16-bit loads; a window too large for the per-thread
+  // row registers keeps window order.
+  constexpr int kRowsPT = 4, kRowBins = 64, kRowBinShift = 2;
+  const int rows_all = ts.roff[LT];
+  const bool rowsort = geo.rowsort != 0 && rows_all <= kRowsPT * kBwdThreads;
+  // window row -> (level, window y, window x, its cell index, the cell grid width)
+  auto row_cell = [&](int row, int& l, int& ey, int& ex, int& cbase, int& cw) {
+    l = 0;
+    while (row >= ts.roff[l + 1]) ++l;
+    const int ww = ts.ww[l], rr = row - ts.roff[l];
+    // rr / ww by the reciprocal: (rr + 0.5) / ww is at least 0.5 / ww from an integer and the product's error
+    // is below wh * ww * 2^-23 / ww, so the truncation is exact for windows of fewer than 2^22 cells
+    ey = static_cast<int>((static_cast<float>(rr) + 0.5f) * ts.iww[l]);
+    ex = rr - ey * ww;  // window coordinates; cells are offset by (1, 1)
+    cw = ww + 1;
+    cbase = ts.coff[l] + (ey + 1) * cw + ex + 1;
+  };
+  const unsigned short* cs16 = reinterpret_cast<const unsigned short*>(cstart);   // the cstart values (low halves)
+  if (rowsort) {
+    int rk[kRowsPT], bk[kRowsPT];
+#pragma unroll
+    for (int i = 0; i < kRowsPT; ++i) {
+      const int row = tid + i * kBwdThreads;
+      bk[i] = -1;
+      if (row < rows_all) {
+        int l, ey, ex, cbase, cw;
+        row_cell(row, l, ey, ex, cbase, cw);
+        const int n = (cstart[cbase + 1] - cstart[cbase - 1]) + (cstart[cbase - cw + 1] - cstart[cbase - cw - 1]);
+        bk[i] = kRowBins - 1 - min(n >> kRowBinShift, kRowBins - 1);
+        rk[i] = atomicAdd(&ts.rbin[bk[i]], 1);
+      }
+    }
+    __syncthreads();
+    if (wid == 0) {   // exclusive scan of the 64 bins
+      const int v = ts.rbin[lane];
+      ts.rbin[lane] = wave_incl_scan(v, lane) - v;
+    }
+    __syncthreads();
+    unsigned short* hi16 = reinterpret_cast<unsigned short*>(cstart);
+#pragma unroll
+    for (int i = 0; i < kRowsPT; ++i)
+      if (bk[i] >= 0) hi16[2 * (ts.rbin[bk[i]] + rk[i]) + 1] = static_cast<unsigned short>(tid + i * kBwdThreads);
+    __syncthreads();
+  }
   M2F_STAMP(2)
 
   // ---- phases 2 and 3: one work queue ----------------------------------------------------------------------
@@ -985,7 +1039,8 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
     const unsigned jlb = static_cast<unsigned>(CPL * 4 * jl);  // this lane's channel bytes (< 128: ORs into a row offset)
     auto phase3_unit = [&](int unit) {
       const int base = unit * RPW;
-      const int row = base + rw;
+      int row = base + rw;
+      if (rowsort && row < rows_total) row = cs16[2 * row + 1];   // the row sort's permutation
       float acc[CPL];
 #pragma unroll
       for (int k = 0; k < CPL; ++k) acc[k] = 0.f;
@@ -993,19 +1048,15 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
       int l = 0, ey = 0, ex = 0;
       bool any = false;
       if (row < rows_total) {
-        while (row >= ts.roff[l + 1]) ++l;
-        const int ww = ts.ww[l], rr = row - ts.roff[l];
-        // rr / ww by the reciprocal: (rr + 0.5) / ww is at least 0.5 / ww from an integer and the product's error
-        // is below wh * ww * 2^-23 / ww, so the truncation is exact for windows of fewer than 2^22 cells
-        ey = static_cast<int>((static_cast<float>(rr) + 0.5f) * ts.iww[l]);
-        ex = rr - ey * ww;  // window coordinates; cells are offset by (1, 1)
-        const int cw = ww + 1, cbase = ts.coff[l] + (ey + 1) * cw + ex + 1;
+        int cbase, cw;
+        row_cell(row, l, ey, ex, cbase, cw);
         // corner 1 of cell (y, x), corner 2 of (y, x-1), corner 3 of (y-1, x), corner 4 of (y-1, x-1).  Cells are
         // numbered row-major, so the slot ranges of (y, x-1) and (y, x) are one contiguous range, as are those of
-        // (y-1, x-1) and (y-1, x): two walks, the six range bounds read up front
-        const int* cs = cstart + cbase;
-        const int b0 = cs[-1], b1 = cs[0], b2 = cs[1];
-        const int u0 = cs[-cw - 1], u1 = cs[-cw], u2 = cs[-cw + 1];
+        // (y-1, x-1) and (y-1, x): two walks, the six range bounds read up front (16-bit reads: the high halves
+        // may hold the row sort's permutation)
+        const unsigned short* cs = cs16 + 2 * cbase;
+        const int b0 = cs[-2], b1 = cs[0], b2 = cs[2];
+        const int u0 = cs[-2 * cw - 2], u1 = cs[-2 * cw], u2 = cs[-2 * cw + 2];
         any = b2 > b0 || u2 > u0;
         // HI: the row above (corners 3 / 4: ly a, else (1 - ly) a); a record below `mid` comes from the cell at x-1
         // (corners 2 / 4: times lx, else (1 - lx)); the (1 - t) factors as fmas
@@ -1941,6 +1992,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   // four levels: 512-thread workgroups only (the L = 4 body needs more than the 128 VGPRs of a 1024-thread one)
   const int first = d.L == 4 ? 512 : m2f::option(m2f::kOptMsdaThreads, det ? 512 : 1024) >= 1024 ? 1024 : 512;
   geo.ratio23 = std::max(1, m2f::option(m2f::kOptMsdaBwdRatio, 1));
+  geo.rowsort = m2f::option(m2f::kOptMsdaBwdRowSort, 1) != 0 ? 1 : 0;
   const TileGeom base = geo;
   // a default 1024-thread geometry whose LDS does not fit (e.g. four levels: 16 samples per query) falls back to
   // the 512-thread one; an explicit msda_threads does not
@@ -1990,7 +2042,7 @@ int launch_tiled_t(const float* value, const float* loc, const float* attn, cons
                    hipStream_t st) {
   const dim3 grid(geo.nty * geo.ntx * d.M * d.N);
   const char* fn = "msda tiled backward";
-  constexpr int kLds = 160 * 1024 - 512;
+  constexpr int kLds = 160 * 1024 - 1024;   // the static TileState (< 1 KB) shares the 160 KB
   if (det.acc) {
     auto* k = &msda_bwd_f32_tiled<LT, FUSED, TPB, true, true>;
     if (int rc = m2f::set_max_lds(reinterpret_cast<const void*>(k), kLds, fn)) return rc;
@@ -2404,7 +2456,7 @@ extern "C" int m2f_diag_msda_bwd_stamps_f32(const float* value, const float* loc
 #define M2F_DIAG_LAUNCH(TPB, NF)                                                                                  \
   do {                                                                                                           \
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&msda_bwd_f32_tiled<3, false, TPB, false, false, true, NF>),      \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);                    \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);                   \
     msda_bwd_f32_tiled<3, false, TPB, false, false, true, NF><<<grid, TPB, lds, st>>>(value, loc, attn, FrontEnd{}, grad_output, \
                                                                        geo, d.S, d.M, grad_value, grad_loc,     \
                                                                        grad_attn, nullptr, nullptr, stamps);    \

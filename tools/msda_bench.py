@@ -122,6 +122,9 @@ def main():
     ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE",
                     help="library option (m2f_set_option) for this run, repeatable; e.g. --opt msda_fwd_quad=0")
     ap.add_argument("--lib", default=None, help="another build of libbm2f.so to load (A/B against a baseline build)")
+    ap.add_argument("--ab", default=None, metavar="NAME=V1,V2",
+                    help="time the backward with option NAME at each value, alternating, --rounds times (one process)")
+    ap.add_argument("--rounds", type=int, default=4)
     a = ap.parse_args()
     from bm2f_amd import _native
     if a.lib:
@@ -142,6 +145,18 @@ def main():
     else:
         fwd = lambda: msda.ms_deform_attn_forward(v, st, lsi, loc, attn, 64)  # noqa: E731
         bwd = lambda: msda.ms_deform_attn_backward(v, st, lsi, loc, attn, gout, 64)  # noqa: E731
+    if a.ab:
+        name, vals = a.ab.split("=")
+        res = {v_: [] for v_ in vals.split(",")}
+        for _ in range(a.rounds):
+            for v_ in res:
+                _native.set_option(name, int(v_))
+                res[v_].append(timeit(bwd, a.iters))
+        _native.set_option(name, -1)
+        for v_, ts in res.items():
+            print(f"ab {name}={v_} fused={a.fused} noise={a.noise} N={a.n}: bwd ms per round {[round(t, 4) for t in ts]} "
+                  f"min {min(ts):.4f} median {sorted(ts)[len(ts) // 2]:.4f}", flush=True)
+        return
     tf = 0.0 if a.bwd_only else timeit(fwd, a.iters)
     tb = float("nan") if a.fwd_only else timeit(bwd, a.iters)
     tf = tf or float("nan")
