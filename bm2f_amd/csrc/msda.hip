@@ -43,7 +43,7 @@ constexpr const char* kOptionNames[m2f::kOptCount] = {
     "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap",
     "msda_bwd_det", "msda_fwd_pb", "msda_bwd_ratio", "msda_fwd_lds", "msda_fwd_tile", "msda_fwd_tile_w",
     "msda_fwd_cap", "msda_fwd_halo", "mattn_fwd_minblk", "mattn_bwd_minblk", "mask_df_stage",
-    "mattn_bwd_keys", "mattn_xcd", "mattn_combine", "msda_bwd_rowsort"};
+    "mattn_bwd_keys", "mattn_xcd", "mattn_combine", "msda_bwd_rowsort", "msda_bwd_walk4"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -500,10 +500,11 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int rs = M * D;  // value row stride (elements); N*S*M*D < 2^31 is checked on the host
   const int nsamp_max = geo.max_qt * LP;
-  // LDS carve-up (16-byte aligned pieces): g rows [max_qt][32] | desc [max_qt * LP][4] | stage [waves][264]
-  //   | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32 | slots [max_qt * LP + 8] u32 | qmap [max_qt] i32
+  // LDS carve-up (16-byte aligned pieces): g rows [max_qt + 1][32] (the last a zero row: phase 3's padding records) |
+  //   desc [max_qt * LP][4] | stage [waves][264] | cstart [max_cells + 1] i32 | oow [ceil(nsamp / 32)] u32
+  //   | slots [max_qt * LP + 8] u32 | qmap [max_qt] i32
   float* gsh = reinterpret_cast<float*>(lds_raw);
-  float* desc = gsh + geo.max_qt * D;
+  float* desc = gsh + (geo.max_qt + 1) * D;
   float* stage = desc + nsamp_max * 4;
   int* cstart = reinterpret_cast<int*>(stage + kBwdWaves * kStageFloats);
   unsigned* oow = reinterpret_cast<unsigned*>(cstart + ((geo.max_rows + 1 + 3) & ~3));
@@ -546,6 +547,7 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
   for (int i = tid; i <= geo.max_rows; i += blockDim.x) cstart[i] = 0;  // the sort's counters (any window fits)
   if (tid == 0) ts.next_batch = kBwdWaves;
   if (tid < 64) ts.rbin[tid] = 0;
+  if (tid < D) gsh[geo.max_qt * D + tid] = 0.f;   // the zero g row
   __syncthreads();
   if (tid == 0) {
     ts.qc[0] = 0;
@@ -1090,8 +1092,50 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
           }
           if (i < s1) rec(npa, i);
         };
-        walk(std::false_type{}, b0, b1, b2);
-        walk(std::true_type{}, u0, u1, u2);
+        // quad form (msda_bwd_walk4, the default): four records per step, lane jl of the row's quad decoding record
+        // i + jl once (slot, descriptor, coefficient) and the quad taking the four in turn with the coefficient and
+        // the g-row offset broadcast by DPP (the broadcast folds into the FMAs / the address add): per record 1 + 8
+        // VALU per lane instead of ~6 + 8 and a quarter of the descriptor reads; a range's tail records carry
+        // coefficient 0 (any in-range slot read: the 8-entry pad covers the read past the range)
+        auto walk4 = [&](auto hi_c, int s0, int mid, int s1) {
+          constexpr bool HI = decltype(hi_c)::value;
+          unsigned np = slots[s0 + jl];
+          for (int i = s0; i < s1; i += 4) {
+            const int idx = i + jl;
+            // a padding record: descriptor 0, the zero g row (coefficient 0 times zeros: nothing added, whatever
+            // non-finite values other g rows hold)
+            const unsigned p = idx < s1 ? np : static_cast<unsigned>(geo.max_qt * D * 4);
+            np = slots[idx + 4];
+            const f4 dk = *reinterpret_cast<const f4*>(reinterpret_cast<const char*>(desc) + ((p >> 12) & 0xffff0u));
+            const float ly = dk[0], lx = dk[1], a = dk[2];
+            const float A = HI ? ly * a : fmaf(-ly, a, a);
+            float cf = idx < mid ? A * lx : fmaf(-A, lx, A);
+            cf = idx < s1 ? cf : 0.f;
+            const unsigned gb = p & 0xffffu;
+            auto rec4 = [&](auto cc) {
+              constexpr int C = decltype(cc)::value;
+              const float c = qpermf<C>(cf);
+              const f4* g = reinterpret_cast<const f4*>(gbytes + (static_cast<unsigned>(qpermi<C>(static_cast<int>(gb))) | jlb));
+#pragma unroll
+              for (int k = 0; k < CPL / 4; ++k) {
+                const f4 v = g[k];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[4 * k + e] = fmaf(c, v[e], acc[4 * k + e]);
+              }
+            };
+            rec4(std::integral_constant<int, 0x00>{});
+            rec4(std::integral_constant<int, 0x55>{});
+            rec4(std::integral_constant<int, 0xAA>{});
+            rec4(std::integral_constant<int, 0xFF>{});
+          }
+        };
+        if (geo.walk4) {
+          walk4(std::false_type{}, b0, b1, b2);
+          walk4(std::true_type{}, u0, u1, u2);
+        } else {
+          walk(std::false_type{}, b0, b1, b2);
+          walk(std::true_type{}, u0, u1, u2);
+        }
       }
       if (any) {
         const int y = ts.wy0[l] + ey, x = ts.wx0[l] + ex;
@@ -1993,6 +2037,7 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
   const int first = d.L == 4 ? 512 : m2f::option(m2f::kOptMsdaThreads, det ? 512 : 1024) >= 1024 ? 1024 : 512;
   geo.ratio23 = std::max(1, m2f::option(m2f::kOptMsdaBwdRatio, 1));
   geo.rowsort = m2f::option(m2f::kOptMsdaBwdRowSort, 1) != 0 ? 1 : 0;
+  geo.walk4 = m2f::option(m2f::kOptMsdaBwdWalk4, 1) != 0 ? 1 : 0;
   const TileGeom base = geo;
   // a default 1024-thread geometry whose LDS does not fit (e.g. four levels: 16 samples per query) falls back to
   // the 512-thread one; an explicit msda_threads does not
@@ -2018,11 +2063,11 @@ bool make_tile_geom(const Dims& d, const int64_t* host_shapes, TileGeom& geo, si
     geo.max_rows = m2f::option(m2f::kOptMsdaWinRows, full);
     geo.max_qt = qt;
     const int lp = d.L * d.P;
-    // phase 3's 32-bit slots hold the g-row byte offset 128 * qs (qs < qt) in their low 16 bits: qt <= 512
-    if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff || qt > 512) continue;
+    // phase 3's 32-bit slots hold the g-row byte offset 128 * qs (qs <= qt: the zero row) in their low 16 bits
+    if (own > geo.max_rows || static_cast<int64_t>(qt) * lp >= 0xffff || qt > 511) continue;
     if (static_cast<int64_t>(qt) * lp > kSortSamples) continue;
     const size_t ns = static_cast<size_t>(qt) * lp;
-    lds = (static_cast<size_t>(qt) * 32 + ns * 4 + (threads / 64) * kStageFloats) * 4 +
+    lds = ((static_cast<size_t>(qt) + 1) * 32 + ns * 4 + (threads / 64) * kStageFloats) * 4 +
           ((static_cast<size_t>(geo.max_rows) + 1 + 3) & ~static_cast<size_t>(3)) * 4 +
           (((ns + 31) / 32 + 3) & ~static_cast<size_t>(3)) * 4 + (ns + 8) * 4 + static_cast<size_t>(qt) * 4;
     if (lds <= 156 * 1024) return true;

@@ -201,8 +201,8 @@ def test_tiled_backward_vs_oracle(device, monkeypatch, tile, rows, halo, overlap
 @pytest.mark.parametrize("shapes,tile,tile_w", [([(48, 48)], 24, 24), ([(24, 24), (48, 48)], 24, 24),
                                                 ([(64, 64)], 16, 32), ([(32, 64)], 16, 32)])
 def test_tiled_backward_large_tiles_vs_oracle(device, shapes, tile, tile_w):
-    """Tiles of more than 512 queries (phase 3's slots hold a g-row byte offset below 2^16) take the untiled
-    kernel; 512 exactly stays tiled.  1- and 2-level pyramids, against the C oracle."""
+    """Tiles of 512 or more queries (phase 3's slots hold a g-row byte offset below 2^16, the zero row's included)
+    take the untiled kernel.  1- and 2-level pyramids, against the C oracle."""
     from bm2f_amd import _native
     with _native.options(msda_tile=tile, msda_tile_w=tile_w, msda_threads=1024):
         _tiled_backward_case(device, tile, 0, shapes)
@@ -434,3 +434,35 @@ def test_fused_forward_nan_weights_on_skipped_points(device, lds):
     with _native.options(msda_fwd_lds=1 - lds):
         other = MSDeformAttnFusedFunction.apply(*args).cpu().view(N, S, M, 32)
     assert torch.equal(out, other)
+
+
+@pytest.mark.parametrize("walk4,rowsort", [(1, 1), (0, 1), (1, 0), (0, 0)])
+def test_fused_backward_phase3_forms_vs_oracle(device, walk4, rowsort):
+    """Phase 3 of the tiled backward in its four forms -- records four per step decoded once per quad (msda_bwd_walk4
+    1, the default) or two per step (0); rows dealt in order of their record count (msda_bwd_rowsort 1, the default) or
+    window order (0) -- against the C oracle, odd level shapes and 5 % far samples."""
+    from bm2f_amd import _native
+    from test_scale_gpu import fused_fwd_bwd_vs_oracle
+    with _native.options(msda_bwd_walk4=walk4, msda_bwd_rowsort=rowsort):
+        fused_fwd_bwd_vs_oracle(device, [(5, 7), (10, 13), (20, 26)], N=2, far=0.05, seed=77)
+
+
+@pytest.mark.parametrize("walk4", [1, 0])
+def test_tiled_backward_nonfinite_grad_stays_local(device, walk4):
+    """A non-finite grad_output row reaches only the value rows its own samples touch, as in the reference's scatter:
+    phase 3's padding records (quad form) read a zero g row, not another query's.  The finite / non-finite pattern
+    of grad_value equals the oracle's."""
+    from bm2f_amd import _native, msda
+    shapes = [(6, 10), (12, 20), (24, 40)]
+    value, st, lsi, loc, attn, gout = _pyramid_case(shapes, 2, 8, 0.0, 11)
+    gout = gout.clone()
+    gout[0, 37, :5] = float("inf")
+    gout[1, 500, 40] = float("nan")
+    dst = msda.attach_host_shapes(st.to(device), shapes)
+    with _native.options(msda_bwd_walk4=walk4, msda_threads=1024):
+        gv, _, _ = msda.ms_deform_attn_backward(value.to(device), dst, lsi.to(device), loc.to(device),
+                                                attn.to(device), gout.to(device), 64)
+    wv, _, _ = msda_ref.msda_backward(value.double(), st, lsi, loc.double(), attn.double(), gout.double())
+    fin = torch.isfinite(gv.cpu()).numpy()
+    assert (~fin).any() and fin.any()
+    assert (fin == np.isfinite(wv)).all(), f"{(fin != np.isfinite(wv)).sum()} elements differ in finiteness"

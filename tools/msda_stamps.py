@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--noise", type=float, default=1.0)
     ap.add_argument("--threads", type=int, default=512)
     ap.add_argument("--tile", type=int, default=0, help="tile edge on the finest level (0: the default)")
+    ap.add_argument("--opt", action="append", default=[], metavar="NAME=VALUE", help="library option, repeatable")
     a = ap.parse_args()
     if a.build:
         build()
@@ -59,6 +60,9 @@ def main():
     lib.m2f_set_option.argtypes = [ctypes.c_char_p, ctypes.c_int64]
     lib.m2f_set_option(b"msda_threads", thr)
     lib.m2f_set_option(b"msda_tile", th)
+    for kv in a.opt:
+        k, v_ = kv.split("=")
+        lib.m2f_set_option(k.encode(), int(v_))
     nwg = _m.ceil(128 / th) * _m.ceil(128 / tw) * M * N
     stamps = torch.zeros(nwg * 8, dtype=torch.int64, device=v.device)
     hs = (ctypes.c_int64 * 6)(*[x for hw in shapes for x in hw])
