@@ -46,7 +46,7 @@ enum Option : int {
   kOptMsdaThreads, kOptMsdaTile, kOptMsdaTileW, kOptMsdaHalo, kOptMsdaWinRows, kOptMsdaBwdTiled, kOptMsdaFwdTiled,
   kOptMattnDqAtomic, kOptGemmNtCfg, kOptX3TnNw, kOptX3TnBlocks, kOptX3NtCfg, kOptMsdaFwdQuad, kOptMsdaBwdOverlap, kOptMsdaBwdDet, kOptMsdaFwdPb, kOptMsdaBwdRatio,
   kOptMsdaFwdLds, kOptMsdaFwdTile, kOptMsdaFwdTileW, kOptMsdaFwdCap, kOptMsdaFwdHalo,
-  kOptMattnFwdMinblk, kOptMattnBwdMinblk, kOptMaskDfStage, kOptMattnBwdKeys, kOptMattnXcd, kOptMattnCombine, kOptMsdaBwdRowSort, kOptMsdaBwdWalk4, kOptCount
+  kOptMattnFwdMinblk, kOptMattnBwdMinblk, kOptMaskDfStage, kOptMattnBwdKeys, kOptMattnXcd, kOptMattnCombine, kOptMsdaBwdRowSort, kOptMsdaBwdWalk4, kOptMsdaFwdXcd, kOptMsdaFwdPair, kOptCount
 };
 int64_t option_raw(Option o);  // -1 when unset
 

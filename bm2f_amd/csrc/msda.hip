@@ -43,7 +43,7 @@ constexpr const char* kOptionNames[m2f::kOptCount] = {
     "mattn_dq_atomic", "gemm_nt_cfg", "x3_tn_nw", "x3_tn_blocks", "x3_nt_cfg", "msda_fwd_quad", "msda_bwd_overlap",
     "msda_bwd_det", "msda_fwd_pb", "msda_bwd_ratio", "msda_fwd_lds", "msda_fwd_tile", "msda_fwd_tile_w",
     "msda_fwd_cap", "msda_fwd_halo", "mattn_fwd_minblk", "mattn_bwd_minblk", "mask_df_stage",
-    "mattn_bwd_keys", "mattn_xcd", "mattn_combine", "msda_bwd_rowsort", "msda_bwd_walk4"};
+    "mattn_bwd_keys", "mattn_xcd", "mattn_combine", "msda_bwd_rowsort", "msda_bwd_walk4", "msda_fwd_xcd", "msda_fwd_pair"};
 std::atomic<int64_t> g_options[m2f::kOptCount] = {};
 struct OptionInit {
   OptionInit() {
@@ -1670,6 +1670,21 @@ __device__ __forceinline__ unsigned win_row(int r) {
   return (static_cast<unsigned>(r >> 3) << 10) | (static_cast<unsigned>(r & 7) << 6);
 }
 
+// block -> (image * tiles + tile, head).  Blocks are dealt to the 8 XCDs round-robin.  Default: the head fastest,
+// so XCD x gathers head x's value rows.  xcdmap (msda_fwd_xcd=1): XCD x takes the x-th eighth of the (image, tile)
+// list, every head of a tile in turn, so a query's projection row (its heads' offsets and logits share 128-byte
+// lines) is fetched into one L2 (config 2: FETCH -15 %, WRITE +29 %, time unchanged: not the default).
+__device__ __forceinline__ void fwd_block(const TileGeom& geo, int M, int& m, int& b) {
+  if (geo.xcdmap) {
+    const int s = static_cast<int>(blockIdx.x >> 3), x = static_cast<int>(blockIdx.x & 7u);
+    m = s % M;
+    b = x * static_cast<int>(gridDim.x / (8u * static_cast<unsigned>(M))) + s / M;
+  } else {
+    m = static_cast<int>(blockIdx.x % static_cast<unsigned>(M));
+    b = static_cast<int>(blockIdx.x / static_cast<unsigned>(M));
+  }
+}
+
 // FUSED: the samples come from the projection and the reference points (fe); otherwise (the reference op's
 // interface, m2f_msda_fwd_f32) from materialised sampling locations loc (N, S, M, L, P, 2) and attention weights
 // attn (N, S, M, L, P), the encoder layout (query i at pyramid position i; host shapes).
@@ -1687,11 +1702,9 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, j = lane & 3;
   // the zero row (window row kFwdWinRows, beyond every window): the LDS-only gather's skipped points read it
   if (tid < 64) reinterpret_cast<f4*>(smem + kFwdWinRows * 128)[tid] = f4{0.f, 0.f, 0.f, 0.f};   // before any barrier
-  // block -> (image, tile, head), the head fastest: XCD x (blocks are dealt round-robin) gathers one head's rows
-  int b = blockIdx.x;
-  const int m = b % M;
-  b /= M;
   const int ntiles = geo.nty * geo.ntx;
+  int m, b;
+  fwd_block(geo, M, m, b);
   const int n = b / ntiles, tile = b - n * ntiles;
   const int ty = tile / geo.ntx, tx = tile - ty * geo.ntx;
   int qy0[LT], qy1[LT], qx0[LT], qx1[LT], qc[LT + 1];
@@ -1908,6 +1921,332 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
 }
 
 // ------------------------------------------------------------------------------------------------
+// Fused forward, two lanes per (query, head) (msda_fwd_pair=1; measured and not the default: 0.535-0.542 ms against
+// the quad-per-query LDS-window kernel's 0.519-0.531 at config 2 near-init, 0.85 against 0.77 ms under N(0, 4 px),
+// profiles/r06_o_msda_fwd_pair_ab.txt).
+//
+// The LDS-window kernel above runs a lane quad per query: lane j derives point j's geometry and every lane gathers
+// 8 channels of each point, so a point costs each lane 8 DPP broadcasts (4 corner addresses, 4 weights) for 16
+// packed FMAs, and a workgroup holds 3 rounds of 64 queries whose geometry and accumulators stay live across the
+// gathers (146 VGPRs: three workgroups per CU).  Here lane h of a pair owns channels 8k + 4h .. 8k + 4h + 3 (k < 4)
+// of its query and points 2h and 2h+1 of each level: a point costs 8 broadcasts for 32 packed FMAs (a corner's 64 bytes are four
+// ds_read_b128 off one address), a workgroup takes one round of 128 queries (8 x 12 finest-level tiles) and needs
+// 138 VGPRs (three workgroups per CU; four at 128 VGPRs with a few spills).  Banking: a ds_read_b128 serves 16 lanes per LDS cycle (MI355X_MICROARCH.md
+// §LDS), here 8 pairs, so the 8 pairs of each lane group take 8 consecutive queries (x-adjacent, so their corner
+// rows are too), and the window holds rows in 1 KB blocks of 8 whose 32-byte pieces k sit in line k (256 bytes)
+// at (row & 7) * 32: at each step the group's 8 pairs read 8 distinct 32-byte bank slots when their rows are 8
+// consecutive window rows (lane h: the piece's 16 bytes at +16h, channels 8k + 4h .. 8k + 4h + 3).  Window
+// staging, the HBM path for corners outside the window and the zero row for skipped points are the LDS-window
+// kernel's; every output element is accumulated in the quad kernel's order (levels, points, corners), so the
+// output is the quad kernel's bit for bit.
+// ------------------------------------------------------------------------------------------------
+constexpr int kFwdPairThreads = 256;
+constexpr int kFwdPairQueries = kFwdPairThreads / 2;
+#ifndef M2F_FWD_PAIR_WGS
+#define M2F_FWD_PAIR_WGS 3  // workgroups per CU, 416-row windows (4 with 312-row windows: 128 VGPRs, 11 spilled,
+                            // 0.537-0.553 vs 0.535-0.542 ms)
+#endif
+constexpr int kFwdPairWgs = M2F_FWD_PAIR_WGS;
+constexpr int kFwdPairCap = kFwdPairWgs == 4 ? 312 : 416;  // window rows incl. the zero row's 1 KB block
+constexpr int kFwdPairWinRows = kFwdPairCap - 8;
+static_assert(kFwdPairWgs * (kFwdPairCap * 128 + kTileMaxL * 4 * 16) <= 160 * 1024, "pair forward LDS per CU");
+
+// pair broadcasts: quad_perm [0,0,2,2] (lane 0 of each pair) or [1,1,3,3] (lane 1)
+template <int HS>
+__device__ __forceinline__ float pbcast(float v) { return qpermf<HS ? 0xF5 : 0xA0>(v); }
+template <int HS>
+__device__ __forceinline__ int pbcasti(int v) { return qpermi<HS ? 0xF5 : 0xA0>(v); }
+
+// b_i = (pair lane HS's a_i) + c, as v_add_u32_dpp (see dpp_add4)
+template <int HS>
+__device__ __forceinline__ void dpp_add4p(unsigned& b1, unsigned& b2, unsigned& b3, unsigned& b4, unsigned a1,
+                                          unsigned a2, unsigned a3, unsigned a4, unsigned c) {
+#define M2F_DPP4P(QP)                                                                                        \
+  asm("s_nop 1\n\t"                                                                                          \
+      "v_add_u32_dpp %0, %4, %8 quad_perm:" QP " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                \
+      "v_add_u32_dpp %1, %5, %8 quad_perm:" QP " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                \
+      "v_add_u32_dpp %2, %6, %8 quad_perm:" QP " row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"                \
+      "v_add_u32_dpp %3, %7, %8 quad_perm:" QP " row_mask:0xf bank_mask:0xf bound_ctrl:1"                     \
+      : "=&v"(b1), "=&v"(b2), "=&v"(b3), "=&v"(b4)                                                            \
+      : "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(c))
+  if constexpr (HS == 0) M2F_DPP4P("[0,0,2,2]");
+  else M2F_DPP4P("[1,1,3,3]");
+#undef M2F_DPP4P
+}
+
+// window layout of the pair kernel: row r's piece k (bytes 32k .. 32k + 31) at pwin_row(r) + 256k
+__device__ __forceinline__ unsigned pwin_row(int r) {
+  return (static_cast<unsigned>(r >> 3) << 10) | (static_cast<unsigned>(r & 7) << 5);
+}
+
+template <int LT>
+__global__ void __launch_bounds__(kFwdPairThreads, kFwdPairWgs) msda_fused_fwd_pair(const float* __restrict__ value,
+                                                                                   FrontEnd fe, TileGeom geo, int S,
+                                                                                   int M, float* __restrict__ out) {
+  constexpr int D = 32, P = 4, LP = LT * P, NW = kFwdPairThreads / 64;
+  // window rows | per-wave boxes [LT][NW]
+  __shared__ __attribute__((aligned(16))) unsigned char smem[kFwdPairCap * 128 + kTileMaxL * NW * 16];
+  const int cap = geo.max_rows;  // window rows in use (a multiple of 8, <= kFwdPairWinRows)
+  int4* bbw = reinterpret_cast<int4*>(smem + kFwdPairCap * 128);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, h = lane & 1;
+  // the zero row (window row kFwdPairWinRows, beyond every window): skipped points' corners in the LDS-only gather
+  if (tid < 64) reinterpret_cast<f4*>(smem + kFwdPairWinRows * 128)[tid] = f4{0.f, 0.f, 0.f, 0.f};
+  const int ntiles = geo.nty * geo.ntx;
+  int m, b;
+  fwd_block(geo, M, m, b);
+  const int n = b / ntiles, tile = b - n * ntiles;
+  const int ty = tile / geo.ntx, tx = tile - ty * geo.ntx;
+  int qy0[LT], qy1[LT], qx0[LT], qx1[LT], qc[LT + 1];
+  qc[0] = 0;
+#pragma unroll
+  for (int l = 0; l < LT; ++l) {
+    qy0[l] = tile_lo(ty, geo.H[l], geo.nty); qy1[l] = tile_lo(ty + 1, geo.H[l], geo.nty);
+    qx0[l] = tile_lo(tx, geo.W[l], geo.ntx); qx1[l] = tile_lo(tx + 1, geo.W[l], geo.ntx);
+    qc[l + 1] = qc[l] + (qy1[l] - qy0[l]) * (qx1[l] - qx0[l]);
+  }
+  const int Qt = qc[LT];
+  const char* vbytes = reinterpret_cast<const char*>(value);
+  const int rsb = M * D * 4;  // value row stride in bytes; value bytes < 2^31 (host check)
+  unsigned chw = 16u * h;     // this lane's 16 bytes of each 32-byte piece (window and HBM rows alike)
+  asm volatile("" : "+v"(chw));
+  const char* pbytes = reinterpret_cast<const char*>(fe.proj);
+  const char* rbytes = reinterpret_cast<const char*>(fe.ref) + static_cast<int64_t>(n) * fe.ref_bs * 4;
+  const unsigned pld = static_cast<unsigned>(fe.ld) * 4u;
+  // this pair's query: the tile's queries level by level, row-major in each level's rectangle; ds_read_b128 lane
+  // group g of the wave ({0-3, 12-15, 20-27} + 32 (g >> 1) for even g, {4-11, 16-19, 28-31} + 32 (g >> 1) for odd)
+  // takes the wave's queries 8g .. 8g + 7, quad u of the group's lanes (in lane order) queries 2u, 2u + 1
+  int qi;
+  {
+    const int u = (lane >> 2) & 7;                             // quad within the wave's half
+    const int g = ((lane >> 5) << 1) | ((0x96 >> u) & 1);      // quads 1, 2, 4, 7 are the odd groups' lanes
+    qi = wid * 32 + g * 8 + (u >> 1) * 2 + ((lane >> 1) & 1);
+  }
+  const bool qv = qi < Qt;
+  int qpos;
+  {
+    const int qq = min(qi, Qt - 1);
+    int lq = 0;
+#pragma unroll
+    for (int l = 1; l < LT; ++l) lq = qq >= qc[l] ? l : lq;
+    int qb = 0, qw = 1, y0 = 0, x0 = 0, W = 1, st = 0;
+#pragma unroll
+    for (int l = 0; l < LT; ++l)
+      if (l == lq) { qb = qc[l]; qw = qx1[l] - qx0[l]; y0 = qy0[l]; x0 = qx0[l]; W = geo.W[l]; st = geo.start[l]; }
+    const int rr = qq - qb;
+    const int yy = static_cast<int>((static_cast<float>(rr) + 0.5f) * __builtin_amdgcn_rcpf(static_cast<float>(qw)));
+    const int xx = rr - yy * qw;
+    qpos = st + (y0 + yy) * W + x0 + xx;
+  }
+  const unsigned prow = static_cast<unsigned>(n * S + qpos) * pld;
+  // softmax over the pair's L*P logits with the quad kernels' arithmetic: the exact max, then the exps summed in
+  // logit order (lane h holds logits l*P + 2h, l*P + 2h + 1)
+  float wa[LT][2];
+  {
+    const unsigned lgb = prow + static_cast<unsigned>(M * LP * 2 + m * LP + 2 * h) * 4u;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int l = 0; l < LT; ++l) {
+      const float2 t = *reinterpret_cast<const float2*>(pbytes + lgb + l * P * 4);
+      wa[l][0] = t.x;
+      wa[l][1] = t.y;
+      mx = fmaxf(mx, t.x);
+      mx = fmaxf(mx, t.y);
+    }
+    mx = fmaxf(mx, qpermf<0xB1>(mx));
+    float sum = 0.f;
+#pragma unroll
+    for (int l = 0; l < LT; ++l) {
+      wa[l][0] = expf(wa[l][0] - mx);
+      wa[l][1] = expf(wa[l][1] - mx);
+      sum += pbcast<0>(wa[l][0]);
+      sum += pbcast<0>(wa[l][1]);
+      sum += pbcast<1>(wa[l][0]);
+      sum += pbcast<1>(wa[l][1]);
+    }
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int l = 0; l < LT; ++l) { wa[l][0] *= inv; wa[l][1] *= inv; }
+  }
+  const f4 z = {0.f, 0.f, 0.f, 0.f};
+  f4 acc[4] = {z, z, z, z};  // channels 8k + 4h .. 8k + 4h + 3
+
+#pragma unroll
+  for (int l = 0; l < LT; ++l) {
+    const int H = geo.H[l], W = geo.W[l];
+    const int lbase = ((n * S + geo.start[l]) * M + m) * D * 4;
+    int zq = 0;  // the level's loads after the previous level's gather (else hoisted to the start: spills)
+    asm volatile("" : "+v"(zq));
+    // 1. points 2h and 2h + 1 of the level: corner block (y0, x0) clamped into the level, +1 row / column inside the
+    //    level (ey, ex), the four weights (x attention weight), ok; the wave's box of touched corners
+    int gy[2], gx[2], gfl[2];
+    float gw[2][4];
+    int bmin_y = 0x7fffffff, bmax_y = -1, bmin_x = 0x7fffffff, bmax_x = -1;
+    auto geometry = [&](auto pow2) {
+      constexpr bool POW2 = decltype(pow2)::value;
+      const float fH = static_cast<float>(H), fW = static_cast<float>(W);
+      const float fHm1 = static_cast<float>(H - 1), fWm1 = static_cast<float>(W - 1);
+      const float2 rf = *reinterpret_cast<const float2*>(rbytes + static_cast<unsigned>((qpos + zq) * LT + l) * 8u);
+      const f4 off = *reinterpret_cast<const f4*>(pbytes + prow + static_cast<unsigned>(zq) * pld +
+                                                  static_cast<unsigned>((m * LP + l * P + 2 * h) * 2) * 4u);
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const float sx = rf.x + div_norm(s ? off.z : off.x, fW, geo.invW[l], POW2);
+        const float sy = rf.y + div_norm(s ? off.w : off.y, fH, geo.invH[l], POW2);
+        const float hh = sy * H - 0.5f, ww = sx * W - 0.5f;
+        const bool ok = qv && hh > -1.f && ww > -1.f && hh < fH && ww < fW;
+        const float hs = ok ? hh : -2.f, ws = ok ? ww : -2.f;
+        const float fh = floorf(hs), fw = floorf(ws);
+        const float ly = hs - fh, lx = ws - fw, hy = 1.f - ly, hx = 1.f - lx;
+        const bool vy0 = fh >= 0.f, vy1 = fh < fHm1, vx0 = fw >= 0.f, vx1 = fw < fWm1;
+        const int y0 = static_cast<int>(__builtin_amdgcn_fmed3f(fh, 0.f, fHm1));
+        const int x0 = static_cast<int>(__builtin_amdgcn_fmed3f(fw, 0.f, fWm1));
+        const int ey = (vy0 && vy1) ? 1 : 0, ex = (vx0 && vx1) ? 1 : 0;
+        const float a = wa[l][s];
+        gw[s][0] = (vy0 && vx0) ? hy * hx * a : 0.f;
+        gw[s][1] = (vy0 && vx1) ? hy * lx * a : 0.f;
+        gw[s][2] = (vy1 && vx0) ? ly * hx * a : 0.f;
+        gw[s][3] = (ok && vy1 && vx1) ? ly * lx * a : 0.f;  // ok: a skipped point's 0 * 0 * a could be a NaN
+        gy[s] = y0;
+        gx[s] = x0;
+        gfl[s] = (ok ? 1 : 0) | (ey << 1) | (ex << 2);
+        asm volatile("" : "+v"(gw[s][0]), "+v"(gw[s][1]), "+v"(gw[s][2]), "+v"(gw[s][3]), "+v"(gy[s]), "+v"(gx[s]),
+                     "+v"(gfl[s]));
+        if (ok) {
+          bmin_y = min(bmin_y, y0); bmax_y = max(bmax_y, y0 + ey);
+          bmin_x = min(bmin_x, x0); bmax_x = max(bmax_x, x0 + ex);
+        }
+      }
+    };
+    if (((W & (W - 1)) | (H & (H - 1))) == 0) geometry(std::true_type{});
+    else geometry(std::false_type{});
+    bmin_y = wave_minmax<false>(bmin_y); bmax_y = wave_minmax<true>(bmax_y);
+    bmin_x = wave_minmax<false>(bmin_x); bmax_x = wave_minmax<true>(bmax_x);
+    if (lane == 0) bbw[l * NW + wid] = make_int4(bmin_y, bmax_y, bmin_x, bmax_x);
+    __syncthreads();  // the boxes are in; every wave is done reading the previous level's window
+    // 2. the window: the box clipped to the tile +- halo, the halo shrinking until the rows fit (uniform)
+    int by0 = 0x7fffffff, by1 = -1, bx0 = 0x7fffffff, bx1 = -1;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      const int4 t = bbw[l * NW + w];
+      by0 = min(by0, t.x); by1 = max(by1, t.y); bx0 = min(bx0, t.z); bx1 = max(bx1, t.w);
+    }
+    by0 = __builtin_amdgcn_readfirstlane(by0); by1 = __builtin_amdgcn_readfirstlane(by1);
+    bx0 = __builtin_amdgcn_readfirstlane(bx0); bx1 = __builtin_amdgcn_readfirstlane(bx1);
+    int wy0 = 0, wy1 = -1, wx0 = 0, wx1 = -1;
+    for (int halo = geo.max_halo; halo >= 0 && by1 >= 0; --halo) {
+      wy0 = max(by0, qy0[l] - halo); wy1 = min(by1, qy1[l] - 1 + halo);
+      wx0 = max(bx0, qx0[l] - halo); wx1 = min(bx1, qx1[l] - 1 + halo);
+      if (wy1 < wy0 || wx1 < wx0) { wy1 = wy0 - 1; break; }
+      if ((wy1 - wy0 + 1) * (wx1 - wx0 + 1) <= cap) break;
+      if (halo == 0) wy1 = wy0 - 1;
+    }
+    const int wh = wy1 >= wy0 ? wy1 - wy0 + 1 : 0, wwid = wh > 0 ? wx1 - wx0 + 1 : 0;
+    const int rows = wh * wwid;
+    {
+      const float iww = wwid > 0 ? 1.f / static_cast<float>(wwid) : 0.f;
+      const int nblk = (rows + 7) >> 3;
+      for (int blk = wid; blk < nblk; blk += NW) {
+        // lane l fills 16 bytes of line l >> 4: row blk * 8 + ((l >> 1) & 7), 16-byte chunk 2 (l >> 4) + (l & 1)
+        const int r = min(blk * 8 + ((lane >> 1) & 7), rows - 1);
+        const int yy = static_cast<int>((static_cast<float>(r) + 0.5f) * iww), xx = r - yy * wwid;
+        const unsigned c = static_cast<unsigned>(((lane >> 4) << 1) | (lane & 1));
+        const unsigned goff = static_cast<unsigned>(mad_u24((wy0 + yy) * W + wx0 + xx, rsb, lbase)) + 16u * c;
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(vbytes + goff),
+                                         (__attribute__((address_space(3))) void*)(smem + blk * 1024), 16, 0, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();  // the window is in LDS
+    // 3. gather: the pair's four points in order, lane h reading its 16 bytes of each 32-byte piece of a corner row
+    const auto* win = (const __attribute__((address_space(3))) unsigned char*)smem;
+    auto lds4 = [&](unsigned o) { return *(const __attribute__((address_space(3))) f4*)(win + o); };
+    int md[2];
+    unsigned a1[2], a2[2], a3[2], a4[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int fl = gfl[s], y0 = gy[s], x0 = gx[s];
+      const int ey = (fl >> 1) & 1, ex = (fl >> 2) & 1;
+      const bool ok = fl & 1;
+      const bool inwin = ok && y0 >= wy0 && y0 + ey <= wy1 && x0 >= wx0 && x0 + ex <= wx1;
+      md[s] = ok ? (inwin ? 1 : 2) : 0;
+      // window form (a skipped point's corners on the zero row) or, out of the window, HBM byte offsets
+      const int q1 = inwin ? (y0 - wy0) * wwid + (x0 - wx0) : kFwdPairWinRows;
+      const int qx = inwin ? ex : 0, q3 = q1 + (inwin && ey ? wwid : 0);
+      const unsigned g1 = static_cast<unsigned>(mad_u24(mad_u24(y0, W, x0), rsb, lbase));
+      const unsigned dx = ex ? rsb : 0u, dy = ey ? static_cast<unsigned>(W * rsb) : 0u;
+      const bool hbm = md[s] == 2;
+      a1[s] = hbm ? g1 : pwin_row(q1);
+      a2[s] = hbm ? g1 + dx : pwin_row(q1 + qx);
+      a3[s] = hbm ? g1 + dy : pwin_row(q3);
+      a4[s] = hbm ? g1 + dy + dx : pwin_row(q3 + qx);
+    }
+    auto fmas = [&](const f4* v, float u1, float u2, float u3, float u4) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += u1 * v[k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += u2 * v[4 + k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += u3 * v[8 + k];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[k] += u4 * v[12 + k];
+    };
+    if (!__any(md[0] == 2 || md[1] == 2)) {
+      // window rows only (the common case): no mode broadcast or branch per point
+      auto point = [&](auto pp) {
+        constexpr int p = decltype(pp)::value, HS = p >> 1, SL = p & 1;
+        unsigned b1, b2, b3, b4;
+        dpp_add4p<HS>(b1, b2, b3, b4, a1[SL], a2[SL], a3[SL], a4[SL], chw);
+        f4 v[16];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v[k] = lds4(b1 + 256u * k); v[4 + k] = lds4(b2 + 256u * k);
+          v[8 + k] = lds4(b3 + 256u * k); v[12 + k] = lds4(b4 + 256u * k);
+        }
+        fmas(v, pbcast<HS>(gw[SL][0]), pbcast<HS>(gw[SL][1]), pbcast<HS>(gw[SL][2]), pbcast<HS>(gw[SL][3]));
+      };
+      point(std::integral_constant<int, 0>{});
+      point(std::integral_constant<int, 1>{});
+      point(std::integral_constant<int, 2>{});
+      point(std::integral_constant<int, 3>{});
+    } else {
+      auto point = [&](auto pp) {
+        constexpr int p = decltype(pp)::value, HS = p >> 1, SL = p & 1;
+        const int mq = pbcasti<HS>(md[SL]);
+        unsigned b1, b2, b3, b4;
+        dpp_add4p<HS>(b1, b2, b3, b4, a1[SL], a2[SL], a3[SL], a4[SL], chw);
+        const float u1 = pbcast<HS>(gw[SL][0]), u2 = pbcast<HS>(gw[SL][1]);
+        const float u3 = pbcast<HS>(gw[SL][2]), u4 = pbcast<HS>(gw[SL][3]);
+        f4 v[16];
+        if (mq == 2) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[k] = ldb4(vbytes, b1 + 32u * k); v[4 + k] = ldb4(vbytes, b2 + 32u * k);
+            v[8 + k] = ldb4(vbytes, b3 + 32u * k); v[12 + k] = ldb4(vbytes, b4 + 32u * k);
+          }
+          fmas(v, u1, u2, u3, u4);
+        } else if (mq == 1) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            v[k] = lds4(b1 + 256u * k); v[4 + k] = lds4(b2 + 256u * k);
+            v[8 + k] = lds4(b3 + 256u * k); v[12 + k] = lds4(b4 + 256u * k);
+          }
+          fmas(v, u1, u2, u3, u4);
+        }
+      };
+      point(std::integral_constant<int, 0>{});
+      point(std::integral_constant<int, 1>{});
+      point(std::integral_constant<int, 2>{});
+      point(std::integral_constant<int, 3>{});
+    }
+  }
+  if (qv) {
+    char* o = reinterpret_cast<char*>(out) + (static_cast<unsigned>((n * S + qpos) * M + m) * 128u + 16u * h);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) *reinterpret_cast<f4*>(o + 32 * k) = acc[k];
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Host side
 // ------------------------------------------------------------------------------------------------
 
@@ -1962,7 +2301,8 @@ void launch_bwd_vec(const float* value, const int64_t* shapes, const int64_t* ls
                                                   d.L, d.Lq, d.P, gv, gl, ga);
 }
 
-bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeom& geo, size_t& lds);
+bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeom& geo, size_t& lds,
+                       bool pair = false);
 bool launch_fwd_lds_unfused(const float* value, const float* loc, const float* attn, const Dims& d,
                             const int64_t* host_shapes, float* out, hipStream_t st);
 
@@ -2262,7 +2602,7 @@ int fused_check(const char* fn, const float* value, const float* proj, int ld, c
 // Options: msda_fwd_tile / msda_fwd_tile_w (8 / 16): tile rows / columns on the finest level; msda_fwd_cap (416):
 // window rows (three workgroups per CU at 52 KB); msda_fwd_halo (8): window halo.  Partition only: every setting
 // computes the same output.
-bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeom& geo, size_t& lds) {
+bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeom& geo, size_t& lds, bool pair) {
   if (d.D != 32 || d.P != 4 || d.Lq != d.S || d.L > kTileMaxL) return false;
   // 32-bit byte offsets into value / out, proj and one image's reference points
   if (static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 >= (int64_t{1} << 31)) return false;
@@ -2275,20 +2615,23 @@ bool make_fwd_lds_geom(const Dims& d, int proj_ld, const TileGeom& base, TileGeo
     if (static_cast<int64_t>(geo.H[l]) * geo.W[l] > static_cast<int64_t>(geo.H[fi]) * geo.W[fi]) fi = l;
   }
   const int th = std::max(1, m2f::option(m2f::kOptMsdaFwdTile, 8));
-  const int tw = std::max(1, m2f::option(m2f::kOptMsdaFwdTileW, 16));
+  const int tw = std::max(1, m2f::option(m2f::kOptMsdaFwdTileW, pair ? 12 : 16));
   geo.nty = (geo.H[fi] + th - 1) / th;
   geo.ntx = (geo.W[fi] + tw - 1) / tw;
   geo.max_halo = std::max(0, m2f::option(m2f::kOptMsdaFwdHalo, 8));
-  const int cap = std::min(m2f::option(m2f::kOptMsdaFwdCap, kFwdWinRows), kFwdWinRows) & ~7;
+  const int win_rows = pair ? kFwdPairWinRows : kFwdWinRows;
+  const int cap = std::min(m2f::option(m2f::kOptMsdaFwdCap, win_rows), win_rows) & ~7;
   int qt = 0, own = 0;
   for (int l = 0; l < d.L; ++l) {
     const int h = (geo.H[l] + geo.nty - 1) / geo.nty, w = (geo.W[l] + geo.ntx - 1) / geo.ntx;
     qt += h * w;
     own = std::max(own, std::min(h + 1, geo.H[l]) * std::min(w + 1, geo.W[l]));
   }
-  if (qt > kFwdLdsRounds * (kFwdLdsThreads / 4) || cap < own) return false;
+  if (qt > (pair ? kFwdPairQueries : kFwdLdsRounds * (kFwdLdsThreads / 4)) || cap < own) return false;
   geo.max_rows = cap;
   geo.max_qt = qt;
+  geo.xcdmap = m2f::option(m2f::kOptMsdaFwdXcd, 0) != 0 &&
+               (static_cast<int64_t>(d.N) * geo.nty * geo.ntx) % 8 == 0 ? 1 : 0;
   lds = 0;  // static
   return true;
 }
@@ -2351,6 +2694,22 @@ extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int
   const bool boff31 = static_cast<int64_t>(d.N) * d.S * d.M * d.D * 4 < (int64_t{1} << 31);
   TileGeom lgeo;
   size_t llds = 0;
+  if (m2f::option(m2f::kOptMsdaFwdLds, 1) != 0 && m2f::option(m2f::kOptMsdaFwdQuad, 1) != 0 &&
+      m2f::option(m2f::kOptMsdaFwdTiled, 1) != 0 && m2f::option(m2f::kOptMsdaFwdPair, 0) != 0 &&
+      make_fwd_lds_geom(d, proj_ld, geo, lgeo, llds, true)) {
+    const int64_t nb = static_cast<int64_t>(lgeo.nty) * lgeo.ntx * d.M * d.N;
+    if (nb > 0x7fffffff) return m2f::fail(M2F_EUNSUPPORTED, "%s: too many workgroups", fn);
+    const unsigned tg = static_cast<unsigned>(nb);
+#define M2F_FP(LT) msda_fused_fwd_pair<LT><<<tg, kFwdPairThreads, 0, st>>>(value, fe, lgeo, d.S, d.M, output)
+    switch (d.L) {
+      case 1: M2F_FP(1); break;
+      case 2: M2F_FP(2); break;
+      case 3: M2F_FP(3); break;
+      default: M2F_FP(4); break;
+    }
+#undef M2F_FP
+    return m2f::check_launch(fn);
+  }
   if (m2f::option(m2f::kOptMsdaFwdLds, 1) != 0 && m2f::option(m2f::kOptMsdaFwdQuad, 1) != 0 &&
       m2f::option(m2f::kOptMsdaFwdTiled, 1) != 0 && make_fwd_lds_geom(d, proj_ld, geo, lgeo, llds)) {
     const int64_t nb = static_cast<int64_t>(lgeo.nty) * lgeo.ntx * d.M * d.N;

@@ -102,6 +102,8 @@ struct TileGeom {
   int ratio23;    // backward: phase-2 units per phase-3 unit at the head of the merged queue
   int rowsort;    // backward: phase-3 rows dealt in order of their record count (1) or window order (0)
   int walk4;      // backward: phase-3 records four per step, decoded once per quad (1) or two per step (0)
+  int xcdmap;     // forward: block b's (tile, head) from XCD b % 8 (a contiguous tile range per XCD, all heads of a
+                  // tile on one XCD) (1) or the head fastest (0)
 };
 
 __device__ __forceinline__ int tile_lo(int t, int n, int nt) { return (t * n) / nt; }

@@ -339,10 +339,11 @@ def test_fused_front_end_matches_unfused(device, monkeypatch, shapes):
 
 @pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(5, 7), (10, 13), (20, 26)],
                                     [(9, 17)], [(4, 4), (8, 8), (16, 16), (32, 32)], [(6, 10), (12, 20)]])
-@pytest.mark.parametrize("quad,pb,lds", [(0, 2, 0), (1, 1, 0), (1, 2, 0), (1, 4, 0), (1, 2, 1)])
-def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb, lds):
-    """The fused forward (m2f_msda_fused_fwd_f32) in its LDS-window form (value windows staged in LDS per tile and
-    level, the default), its quad form (a lane quad per (query, head), point geometry by DPP broadcast,
+@pytest.mark.parametrize("quad,pb,lds,pair", [(0, 2, 0, 0), (1, 1, 0, 0), (1, 2, 0, 0), (1, 4, 0, 0), (1, 2, 1, 0),
+                                              (1, 2, 1, 1)])
+def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb, lds, pair):
+    """The fused forward (m2f_msda_fused_fwd_f32) in its LDS-window forms (value windows staged in LDS per tile and
+    level; two lanes per query, the default, or a lane quad per query), its quad form (a lane quad per (query, head), point geometry by DPP broadcast,
     out-of-range points skipped by the exec mask; 1, 2 or 4 points per load batch) and its 8-lane form, against
     the C oracle on the loc / attn the reference front end derives from the same projection: power-of-two and odd
     level shapes (tile edges), 1-4 levels, 5 % of the samples thrown far (out of the level and out of range)."""
@@ -354,7 +355,7 @@ def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb, lds):
     value, proj, ref = _fused_case(shapes, N, 0.05, seed=21 + L)
     S = value.shape[1]
     rf = ref.float()[None, :, None, :].expand(N, S, L, 2).to(device)
-    with _native.options(msda_fwd_quad=quad, msda_fwd_pb=pb, msda_fwd_lds=lds):
+    with _native.options(msda_fwd_quad=quad, msda_fwd_pb=pb, msda_fwd_lds=lds, msda_fwd_pair=pair):
         out = MSDeformAttnFusedFunction.apply(value.to(device), proj.to(device), rf, tuple(shapes), P)
     torch.cuda.synchronize()
     loc, attn = _loc_attn(proj, ref, shapes)
@@ -367,11 +368,14 @@ def test_fused_forward_variants_vs_oracle(device, shapes, quad, pb, lds):
 @pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(5, 7), (10, 13), (20, 26)], [(9, 17)],
                                     [(4, 4), (8, 8), (16, 16), (32, 32)], [(6, 10), (12, 20)]])
 @pytest.mark.parametrize("tile,tile_w,cap,halo", [(4, 8, 64, 2), (16, 16, 1024, 8), (8, 16, 96, 0), (3, 5, 48, 1),
-                                               (8, 16, 312, 4)])
-def test_fused_forward_lds_geometries_bitwise(device, shapes, tile, tile_w, cap, halo):
-    """The LDS-window forward computes each output element with the quad kernel's arithmetic in the same order,
-    so every window geometry (tile, window rows, halo; small budgets force the halo to shrink and send samples
-    to the HBM path) returns the quad kernel's output bit for bit, 5 % of the samples thrown far."""
+                                               (8, 16, 312, 4), (8, 12, 304, 3), (4, 12, 40, 1)])
+@pytest.mark.parametrize("pair,xcd", [(1, 0), (0, 0), (1, 1)])
+def test_fused_forward_lds_geometries_bitwise(device, shapes, tile, tile_w, cap, halo, pair, xcd):
+    """The LDS-window forwards (two lanes per query, or a lane quad; a tile of more than 128 queries runs the quad
+    form) compute each output element with the quad kernel's arithmetic in the same order, so every window
+    geometry (tile, window rows, halo; small budgets force the halo to shrink and send samples to the HBM path)
+    returns the quad kernel's output bit for bit, 5 % of the samples thrown far; under both block -> (tile, head)
+    mappings (msda_fwd_xcd: a tile range per XCD, or the head fastest)."""
     from bm2f_amd import _native
     from bm2f_amd.msda import MSDeformAttnFusedFunction
     from test_scale_gpu import _fused_case
@@ -384,7 +388,7 @@ def test_fused_forward_lds_geometries_bitwise(device, shapes, tile, tile_w, cap,
     with _native.options(msda_fwd_lds=0):
         want = MSDeformAttnFusedFunction.apply(*args)
     with _native.options(msda_fwd_lds=1, msda_fwd_tile=tile, msda_fwd_tile_w=tile_w, msda_fwd_cap=cap,
-                         msda_fwd_halo=halo):
+                         msda_fwd_halo=halo, msda_fwd_xcd=xcd, msda_fwd_pair=pair):
         got = MSDeformAttnFusedFunction.apply(*args)
     torch.cuda.synchronize()
     assert torch.equal(got, want)
@@ -403,12 +407,13 @@ def test_fused_backward_variants_vs_oracle(device, shapes, quad):
         fused_fwd_bwd_vs_oracle(device, shapes, N=2, far=0.05, seed=31 + len(shapes))
 
 
-@pytest.mark.parametrize("lds", [1, 0])
-def test_fused_forward_nan_weights_on_skipped_points(device, lds):
+@pytest.mark.parametrize("lds,pair", [(1, 1), (1, 0), (0, 0)])
+def test_fused_forward_nan_weights_on_skipped_points(device, lds, pair):
     """A (query, head) whose every point lies outside its level adds nothing, whatever its attention weights hold:
     the reference kernel tests the sample position before it touches the weight (ms_deform_im2col_cuda.cuh:257-262),
-    so NaN logits on such a row give a zero output.  Both the LDS-window forward (whose LDS-only gather runs the FMAs
-    of skipped points on a zero row: the weights must be zeroed, not multiplied by 0) and the quad kernel."""
+    so NaN logits on such a row give a zero output.  The LDS-window forwards, two lanes or a lane quad per query
+    (whose LDS-only gathers run the FMAs of skipped points on a zero row: the weights must be zeroed, not multiplied
+    by 0), and the quad kernel."""
     from bm2f_amd import _native
     from bm2f_amd.msda import MSDeformAttnFusedFunction
     from test_scale_gpu import _fused_case
@@ -424,14 +429,14 @@ def test_fused_forward_nan_weights_on_skipped_points(device, lds):
         logit[n, q, m] = float("nan")
     args = (value.to(device), proj.to(device), ref.float()[None, :, None, :].expand(N, S, L, 2).to(device),
             tuple(shapes), P)
-    with _native.options(msda_fwd_lds=lds):
+    with _native.options(msda_fwd_lds=lds, msda_fwd_pair=pair):
         out = MSDeformAttnFusedFunction.apply(*args)
     torch.cuda.synchronize()
     out = out.cpu().view(N, S, M, 32)
     assert torch.isfinite(out).all(), "a skipped point's NaN weight reached the output"
     for n, q, m in rows:
         assert (out[n, q, m] == 0).all()
-    with _native.options(msda_fwd_lds=1 - lds):
+    with _native.options(msda_fwd_lds=1 - lds, msda_fwd_pair=1 - pair):
         other = MSDeformAttnFusedFunction.apply(*args).cpu().view(N, S, M, 32)
     assert torch.equal(out, other)
 
