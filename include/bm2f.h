@@ -347,7 +347,10 @@ int m2f_maxpool3s2_nhwc(int backward, const void* src, void* dst, uint8_t* windo
  * environment).  value < 0 restores the built-in default.  Names: msda_threads, msda_tile, msda_tile_w,
  * msda_halo, msda_win_rows, msda_bwd_tiled, msda_fwd_tiled, msda_fwd_quad, msda_fwd_pb, msda_bwd_overlap,
  * msda_bwd_ratio, msda_bwd_det, msda_fwd_lds, msda_fwd_tile, msda_fwd_tile_w, msda_fwd_cap, msda_fwd_halo (MSDA
- * partitions, variants, LDS windows, deterministic mode), mattn_dq_atomic, mattn_fwd_minblk, mattn_bwd_minblk,
+ * partitions, variants, LDS windows, deterministic mode), msda_bwd_rowsort, msda_bwd_walk4 (tiled backward phase 3:
+ * rows by record count, four records per step; both 1 by default), msda_fwd_pair (LDS-window forward with two lanes
+ * per query: 1, or a lane quad: 0, the default), msda_fwd_xcd (forward blocks: all heads of a tile on one XCD: 1, or
+ * the head fastest: 0, the default), mattn_dq_atomic, mattn_fwd_minblk, mattn_bwd_minblk,
  * mattn_bwd_keys, mattn_xcd (masked-attention dQ variant, key blocks per workgroup at least, keys per wave in the
  * backward: 32 or 16, the heads of one image and key chunk on one XCD: 1 or 0), mattn_combine (forward chunk
  * combine: a thread per row part 0, a wave per row 1), mask_df_stage (mask-einsum feature
