@@ -156,8 +156,10 @@ def _x3(M, N, K):
 ENTRIES = {
     # name: (family, bound, work(args) -> (bytes, flops))
     "m2f_msda_fused_bwd_f32": ("msda_bwd", "hbm", lambda a: _msda_bytes(a, True, True)),
+    "m2f_msda_fused_bwd_hm_f32": ("msda_bwd", "hbm", lambda a: _msda_bytes(a, True, True)),
     "m2f_msda_bwd_f32": ("msda_bwd", "hbm", lambda a: _msda_bytes(a, False, True)),
     "m2f_msda_fused_fwd_f32": ("msda_fwd", "hbm", lambda a: _msda_bytes(a, True, False)),
+    "m2f_msda_fused_fwd_hm_f32": ("msda_fwd", "hbm", lambda a: _msda_bytes(a, True, False)),
     "m2f_msda_fwd_f32": ("msda_fwd", "hbm", lambda a: _msda_bytes(a, False, False)),
     "m2f_attn_mask_bits": ("attn_mask_bits", "hbm", lambda a: (
         a[2] * a[3] * a[4] * a[5] * a[6] * (4 if a[1] == 0 else 2) + a[2] * a[3] * a[11] * 4, 0)),
@@ -671,7 +673,8 @@ def main():
             roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": (tr or {}).get("hbm_bytes_per_launch") if tr else None,
-                    "kernel": "MSDA backward (m2f_msda_fused_bwd_f32)",
+                    "kernel": "MSDA backward (m2f_msda_fused_bwd_hm_f32: the fused backward on the module's "
+                              "head-major projection)",
                     "algorithmic_bytes_per_launch": nbytes, "mean_launch_ms": round(bwd["mean_ms"], 4)}
             if bwd.get("gather_bytes"):
                 roof["gather_gbs"] = round(bwd["gather_bytes"] / (bwd["total_ms"] * 1e-3) / 1e9, 1)

@@ -33,6 +33,8 @@ _SIGNATURES = {
     "m2f_msda_fused_fwd_f32": [_p, _p, _i, _p, _l, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p],
     "m2f_msda_fused_bwd_workspace": [_p, _i, _i, _i, _i, _i, _i, _p],
     "m2f_msda_fused_bwd_f32": [_p, _p, _i, _p, _l, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _l, _p],
+    "m2f_msda_fused_fwd_hm_f32": [_p, _p, _i, _p, _l, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p],
+    "m2f_msda_fused_bwd_hm_f32": [_p, _p, _i, _p, _l, _p, _p, _i, _i, _i, _i, _i, _i, _i, _p, _p, _p, _l, _p],
     "m2f_attn_mask_bits": [_p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _p, _i, _p],
     "m2f_mask_heads_fwd": [_i, _p, _p, _i, _i, _i, _i, _i, _i, _i, _i, _p, _p, _i, _p],
     "m2f_mask_row_fix": [_p, _i, _i, _i, _p],

@@ -382,10 +382,15 @@ __device__ __forceinline__ int g_chunk_off(int qi, int c) { return qi * 32 + 4 *
 
 // Fused-front-end inputs (raw projection + reference points).
 struct FrontEnd {
-  const float* proj;   // (N, Lq, ld): offsets (M, L, P, 2) then logits (M, L*P)
+  const float* proj;   // (N, Lq, ld): offsets (M, L, P, 2) then logits (M, L*P); hm: per head m a record
+                       // [offsets (L, P, 2) | logits (L*P)] (m2f_msda_fused_*_hm_f32); grad_proj alike
   int ld;
   const float* ref;    // (N or broadcast, Lq, L, 2) [x, y]
   int64_t ref_bs;      // batch stride of ref in elements (0 = broadcast)
+  int hm;
+  // where head m's offsets / logits start in a projection (or grad_proj) row (LP = L * P)
+  __device__ __forceinline__ int off0(int m, int LP) const { return hm ? m * 3 * LP : m * LP * 2; }
+  __device__ __forceinline__ int lg0(int m, int M, int LP) const { return hm ? m * 3 * LP + 2 * LP : M * LP * 2 + m * LP; }
 };
 
 // pyramid position of the tile's query qi (levels in order, rows of the tile's rectangle on each level)
@@ -597,8 +602,8 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
       const int64_t nq = static_cast<int64_t>(n) * S + qmap[qi];
       if constexpr (FUSED) {
         const float* prow = fe.proj + nq * fe.ld;
-        const float* lg = prow + M * LP * 2 + m * LP + l * P;
-        const float* of = prow + (m * LP + l * P) * 2;
+        const float* lg = prow + fe.lg0(m, M, LP) + l * P;
+        const float* of = prow + fe.off0(m, LP) + l * P * 2;
 #pragma unroll
         for (int p = 0; p < P; ++p) { in.x[p] = lg[p]; in.xy[p] = *reinterpret_cast<const float2*>(of + 2 * p); }
         in.rf = *reinterpret_cast<const float2*>(fe.ref + n * fe.ref_bs + (static_cast<int64_t>(qmap[qi]) * LT + l) * 2);
@@ -986,7 +991,7 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
           dot = fmaf(a, gak, dot);
           gaown[l] = gak;
           aown[l] = a;
-          *reinterpret_cast<float2*>(gloc + nq * (3 * M * LP) + (m * LT + l) * P * 2 + 2 * j) =
+          *reinterpret_cast<float2*>(gloc + nq * (3 * M * LP) + fe.off0(m, LP) + l * P * 2 + 2 * j) =
               ok ? make_float2(px, py) : make_float2(0.f, 0.f);
         } else {
           const unsigned kl = ((static_cast<unsigned>(n * S + q) * M + m) * LT + l) * P + j;  // < 2^28 (host)
@@ -1028,7 +1033,7 @@ __global__ void __launch_bounds__(TPB, (LT == 4 && TPB == 512) ? 2 : 4) msda_bwd
         // softmax backward over the pair's L*P logits: d logit_k = a_k (d a_k - sum_i a_i d a_i)
         dot += qpermf<0xB1>(dot);
         dot += qpermf<0x4E>(dot);
-        float* gl = gloc + nq * (3 * M * LP) + 2 * M * LP + m * LP;
+        float* gl = gloc + nq * (3 * M * LP) + fe.lg0(m, M, LP);
 #pragma unroll
         for (int l = 0; l < LT; ++l) gl[l * P + j] = aown[l] * (gaown[l] - dot);
       }
@@ -1251,7 +1256,7 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
   const int64_t rs = static_cast<int64_t>(M) * D;
   const float* prow = fe.proj + nq * fe.ld;
   const float* rrow = fe.ref + n * fe.ref_bs + static_cast<int64_t>(q) * LT * 2;
-  const float* lg = prow + M * LP * 2 + m * LP;
+  const float* lg = prow + fe.lg0(m, M, LP);
   // softmax over the pair's L*P logits (ms_deform_attn.py:103-104), each exp computed once in the group:
   // lane j owns logits j and j + 8, the group max is a DPP reduction (exact), and every lane gathers the
   // twelve exps and sums them in logit order (the backward recomputes the same sum, msda_bwd_f32_tiled)
@@ -1282,7 +1287,7 @@ __global__ void __launch_bounds__(256) msda_fused_fwd(const float* __restrict__ 
       constexpr bool POW2 = decltype(pow2)::value;
 #pragma unroll
       for (int p = 0; p < P; ++p) {
-        const float2 off = *reinterpret_cast<const float2*>(prow + (m * LP + l * P + p) * 2);
+        const float2 off = *reinterpret_cast<const float2*>(prow + fe.off0(m, LP) + (l * P + p) * 2);
         const float sx = rf.x + div_norm(off.x, fW, iW, POW2);
         const float sy = rf.y + div_norm(off.y, fH, iH, POW2);
         f4 val;
@@ -1460,7 +1465,7 @@ __global__ void __launch_bounds__(256) msda_fused_fwd_q4(const float* __restrict
   // softmax over the pair's L*P logits (ms_deform_attn.py:103-104): lane j exps logit l*P + j of every level,
   // the quad max is exact, and every lane sums the exps in logit order (the sequential sum the backward
   // recomputes, msda_bwd_f32_tiled), so the attention weights are bit-identical to the other kernels'
-  const float* lg = prow + M * LP * 2 + m * LP;
+  const float* lg = prow + fe.lg0(m, M, LP);
   float e[LT];
   float mx = -INFINITY;
 #pragma unroll
@@ -1485,7 +1490,7 @@ __global__ void __launch_bounds__(256) msda_fused_fwd_q4(const float* __restrict
     const int H = geo.H[l], W = geo.W[l];
     const int obase = ((n * S + geo.start[l]) * M + m) * D * 4;
     const float2 rf = *reinterpret_cast<const float2*>(rrow + 2 * l);
-    const float2 off = *reinterpret_cast<const float2*>(prow + (m * LP + l * P + j) * 2);
+    const float2 off = *reinterpret_cast<const float2*>(prow + fe.off0(m, LP) + (l * P + j) * 2);
     const float sx = rf.x + div_norm(off.x, static_cast<float>(W), geo.invW[l], POW2);
     const float sy = rf.y + div_norm(off.y, static_cast<float>(H), geo.invH[l], POW2);
     // this lane's point: corner byte offsets and weights (a corner outside the level weighted 0: its clamped row
@@ -1750,7 +1755,7 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
     qpos[r] = st + (y0 + yy) * W + x0 + xx;
     if constexpr (!FUSED) continue;  // the attention weights are read per level
     // softmax over the pair's L*P logits, exactly as msda_fused_fwd_q4 (and the backward's recomputation)
-    const unsigned lgb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>(M * LP * 2 + m * LP + j) * 4u;
+    const unsigned lgb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>(fe.lg0(m, M, LP) + j) * 4u;
     float e[LT];
     float mx = -INFINITY;
 #pragma unroll
@@ -1800,7 +1805,7 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
         float sx, sy;
         if constexpr (FUSED) {
           const unsigned rfb = static_cast<unsigned>((qpos[r] + zq) * LT + l) * 8u;
-          const unsigned ofb = static_cast<unsigned>(n * S + qpos[r] + zq) * pld + static_cast<unsigned>((m * LP + l * P + j) * 2) * 4u;
+          const unsigned ofb = static_cast<unsigned>(n * S + qpos[r] + zq) * pld + static_cast<unsigned>(fe.off0(m, LP) + (l * P + j) * 2) * 4u;
           const float2 rf = *reinterpret_cast<const float2*>(rbytes + rfb);
           const float2 off = *reinterpret_cast<const float2*>(pbytes + ofb);
           sx = rf.x + div_norm(off.x, fW, geo.invW[l], POW2);
@@ -2042,7 +2047,7 @@ __global__ void __launch_bounds__(kFwdPairThreads, kFwdPairWgs) msda_fused_fwd_p
   // logit order (lane h holds logits l*P + 2h, l*P + 2h + 1)
   float wa[LT][2];
   {
-    const unsigned lgb = prow + static_cast<unsigned>(M * LP * 2 + m * LP + 2 * h) * 4u;
+    const unsigned lgb = prow + static_cast<unsigned>(fe.lg0(m, M, LP) + 2 * h) * 4u;
     float mx = -INFINITY;
 #pragma unroll
     for (int l = 0; l < LT; ++l) {
@@ -2087,7 +2092,7 @@ __global__ void __launch_bounds__(kFwdPairThreads, kFwdPairWgs) msda_fused_fwd_p
       const float fHm1 = static_cast<float>(H - 1), fWm1 = static_cast<float>(W - 1);
       const float2 rf = *reinterpret_cast<const float2*>(rbytes + static_cast<unsigned>((qpos + zq) * LT + l) * 8u);
       const f4 off = *reinterpret_cast<const f4*>(pbytes + prow + static_cast<unsigned>(zq) * pld +
-                                                  static_cast<unsigned>((m * LP + l * P + 2 * h) * 2) * 4u);
+                                                  static_cast<unsigned>(fe.off0(m, LP) + (l * P + 2 * h) * 2) * 4u);
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
         const float sx = rf.x + div_norm(s ? off.z : off.x, fW, geo.invW[l], POW2);
@@ -2676,17 +2681,16 @@ bool launch_fwd_lds_unfused(const float* value, const float* loc, const float* a
 
 }  // namespace
 
-extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+static int fused_fwd(int hm, const char* fn, const float* value, const float* proj, int proj_ld, const float* ref,
                                       int64_t ref_batch_stride, const int64_t* host_spatial_shapes, int batch,
                                       int spatial_size, int num_heads, int channels, int num_levels,
                                       int num_query, int num_point, float* output, void* stream) {
-  const char* fn = "m2f_msda_fused_fwd_f32";
   const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
   TileGeom geo;
   int rc = fused_check(fn, value, proj, proj_ld, ref, host_spatial_shapes, d, geo);
   if (rc) return rc;
   if (!output || !m2f::aligned(output, 16)) return m2f::fail(M2F_EINVAL, "%s: bad output", fn);
-  const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
+  const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride, hm};
   hipStream_t st = static_cast<hipStream_t>(stream);
   // value and out hold N * Lq(=S) * M * 32 elements; 32-bit offsets when those fit
   const bool off32 = static_cast<int64_t>(d.N) * std::max(d.S, d.Lq) * d.M * d.D < (int64_t{1} << 31);
@@ -2793,13 +2797,12 @@ extern "C" int m2f_msda_fused_bwd_workspace(const int64_t* host_spatial_shapes, 
   return m2f::ok();
 }
 
-extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+static int fused_bwd(int hm, const char* fn, const float* value, const float* proj, int proj_ld, const float* ref,
                                       int64_t ref_batch_stride, const int64_t* host_spatial_shapes,
                                       const float* grad_output, int batch, int spatial_size, int num_heads,
                                       int channels, int num_levels, int num_query, int num_point,
                                       float* grad_value, float* grad_proj, void* workspace, int64_t workspace_bytes,
                                       void* stream) {
-  const char* fn = "m2f_msda_fused_bwd_f32";
   const Dims d{batch, spatial_size, num_heads, channels, num_levels, num_query, num_point};
   TileGeom geo0;
   int rc = fused_check(fn, value, proj, proj_ld, ref, host_spatial_shapes, d, geo0);
@@ -2817,7 +2820,7 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
   const size_t gv_bytes = static_cast<size_t>(nval) * sizeof(float);
   hipError_t e = m2f::zero_async(grad_value, gv_bytes, st);
   if (e != hipSuccess) return m2f::fail(M2F_ELAUNCH, "%s: memset grad_value: %s", fn, hipGetErrorString(e));
-  const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride};
+  const FrontEnd fe{proj, proj_ld, ref, ref_batch_stride, hm};
   DetBufs det;
   if (m2f::option(m2f::kOptMsdaBwdDet, 0) != 0) {
     const int64_t need = det_workspace_bytes(d);
@@ -2838,6 +2841,44 @@ extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int
     msda_det_convert_kernel<<<4096, 256, 0, st>>>(reinterpret_cast<const long long*>(det.acc), nval, d.Lq, det.scale,
                                                   grad_value);
   return m2f::check_launch(fn);
+}
+
+extern "C" int m2f_msda_fused_fwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+                                      int64_t ref_batch_stride, const int64_t* host_spatial_shapes, int batch,
+                                      int spatial_size, int num_heads, int channels, int num_levels,
+                                      int num_query, int num_point, float* output, void* stream) {
+  return fused_fwd(0, "m2f_msda_fused_fwd_f32", value, proj, proj_ld, ref, ref_batch_stride, host_spatial_shapes,
+                   batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, output, stream);
+}
+
+extern "C" int m2f_msda_fused_fwd_hm_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+                                      int64_t ref_batch_stride, const int64_t* host_spatial_shapes, int batch,
+                                      int spatial_size, int num_heads, int channels, int num_levels,
+                                      int num_query, int num_point, float* output, void* stream) {
+  return fused_fwd(1, "m2f_msda_fused_fwd_hm_f32", value, proj, proj_ld, ref, ref_batch_stride, host_spatial_shapes,
+                   batch, spatial_size, num_heads, channels, num_levels, num_query, num_point, output, stream);
+}
+
+extern "C" int m2f_msda_fused_bwd_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+                                      int64_t ref_batch_stride, const int64_t* host_spatial_shapes,
+                                      const float* grad_output, int batch, int spatial_size, int num_heads,
+                                      int channels, int num_levels, int num_query, int num_point,
+                                      float* grad_value, float* grad_proj, void* workspace, int64_t workspace_bytes,
+                                      void* stream) {
+  return fused_bwd(0, "m2f_msda_fused_bwd_f32", value, proj, proj_ld, ref, ref_batch_stride, host_spatial_shapes,
+                   grad_output, batch, spatial_size, num_heads, channels, num_levels, num_query, num_point,
+                   grad_value, grad_proj, workspace, workspace_bytes, stream);
+}
+
+extern "C" int m2f_msda_fused_bwd_hm_f32(const float* value, const float* proj, int proj_ld, const float* ref,
+                                      int64_t ref_batch_stride, const int64_t* host_spatial_shapes,
+                                      const float* grad_output, int batch, int spatial_size, int num_heads,
+                                      int channels, int num_levels, int num_query, int num_point,
+                                      float* grad_value, float* grad_proj, void* workspace, int64_t workspace_bytes,
+                                      void* stream) {
+  return fused_bwd(1, "m2f_msda_fused_bwd_hm_f32", value, proj, proj_ld, ref, ref_batch_stride, host_spatial_shapes,
+                   grad_output, batch, spatial_size, num_heads, channels, num_levels, num_query, num_point,
+                   grad_value, grad_proj, workspace, workspace_bytes, stream);
 }
 
 #ifdef M2F_DIAG

@@ -235,11 +235,13 @@ class MSDeformAttnFusedFunction(Function):
     logits (M, L*P)], the raw output of the two projections of ms_deform_attn.py:102-103; ref (N, S, L, 2)
     reference points.  Computes softmax and loc = ref + offset / (W, H) in-kernel (ms_deform_attn.py:104-109)
     instead of materialising sampling_locations / attention_weights; the backward returns d value and
-    d proj directly (reference points are constants of the encoder and get no gradient).
+    d proj directly (reference points are constants of the encoder and get no gradient).  ``head_major``: proj
+    rows hold one [offsets (L, P, 2) | logits (L*P)] record per head instead (:func:`head_major_wb`; the
+    m2f_msda_fused_*_hm_f32 entry points), and d proj comes back in that layout.
     """
 
     @staticmethod
-    def forward(ctx, value, proj, ref, host_shapes, n_points):
+    def forward(ctx, value, proj, ref, host_shapes, n_points, head_major=False):
         N, S, M, D = value.shape
         L = len(host_shapes)
         if ref.stride(-1) != 1 or ref.stride(-2) != 2 or ref.stride(-3) != 2 * L:
@@ -248,17 +250,18 @@ class MSDeformAttnFusedFunction(Function):
             proj = proj.contiguous()
         hs = _host_shape_buffer(host_shapes)
         out = torch.empty((N, S, M * D), dtype=value.dtype, device=value.device)
-        _native.call("m2f_msda_fused_fwd_f32", _ptr(value), _ptr(proj), proj.stride(1), _ptr(ref), ref.stride(0),
-                     ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, S, n_points, _ptr(out), _stream(value.device))
+        _native.call("m2f_msda_fused_fwd_hm_f32" if head_major else "m2f_msda_fused_fwd_f32", _ptr(value), _ptr(proj),
+                     proj.stride(1), _ptr(ref), ref.stride(0), ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, S,
+                     n_points, _ptr(out), _stream(value.device))
         ctx.save_for_backward(value, proj, ref)
-        ctx.meta = (tuple(host_shapes), n_points)
+        ctx.meta = (tuple(host_shapes), n_points, bool(head_major))
         return out
 
     @staticmethod
     @once_differentiable
     def backward(ctx, grad_out):
         value, proj, ref = ctx.saved_tensors
-        host_shapes, n_points = ctx.meta
+        host_shapes, n_points, head_major = ctx.meta
         N, S, M, D = value.shape
         L = len(host_shapes)
         grad_out = grad_out.contiguous()
@@ -274,11 +277,24 @@ class MSDeformAttnFusedFunction(Function):
         _native.call("m2f_msda_fused_bwd_workspace", ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, n_points,
                      ctypes.byref(ws_bytes))
         ws = torch.empty(ws_bytes.value, dtype=torch.uint8, device=value.device) if ws_bytes.value else None
-        _native.call("m2f_msda_fused_bwd_f32", _ptr(value), _ptr(proj), proj.stride(1), _ptr(ref), ref.stride(0),
-                     ctypes.cast(hs, ctypes.c_void_p), _ptr(grad_out), N, S, M, D, L, S, n_points, _ptr(grad_value),
-                     _ptr(grad_proj), None if ws is None else _ptr(ws), ctypes.c_int64(ws_bytes.value),
-                     _stream(value.device))
-        return grad_value, grad_proj, None, None, None
+        _native.call("m2f_msda_fused_bwd_hm_f32" if head_major else "m2f_msda_fused_bwd_f32", _ptr(value),
+                     _ptr(proj), proj.stride(1), _ptr(ref), ref.stride(0), ctypes.cast(hs, ctypes.c_void_p),
+                     _ptr(grad_out), N, S, M, D, L, S, n_points, _ptr(grad_value), _ptr(grad_proj),
+                     None if ws is None else _ptr(ws), ctypes.c_int64(ws_bytes.value), _stream(value.device))
+        return grad_value, grad_proj, None, None, None, None
+
+
+def head_major_wb(w_off, b_off, w_attn, b_attn, n_heads):
+    """The sampling-offset and attention-logit projections (ms_deform_attn.py:59-60) as one weight / bias whose
+    output rows are head-major: per head m its offsets (L, P, 2) then its logits (L*P).  Built from views and a
+    cat, so the parameters' gradients come back through slices (deterministic; no scatter)."""
+    C = w_off.shape[1]
+    w = torch.cat([w_off.view(n_heads, -1, C), w_attn.view(n_heads, -1, C)], 1).reshape(-1, C)
+    b = torch.cat([b_off.view(n_heads, -1), b_attn.view(n_heads, -1)], 1).reshape(-1)
+    return w, b
+
+
+HEAD_MAJOR = True  # the module's fused path projects head-major (m2f_msda_fused_*_hm_f32); False: reference order
 
 
 FUSED = True   # the encoder's fused MSDA front end; False: the reference's op chain (tests, A/B)
@@ -365,6 +381,15 @@ class MSDeformAttn(nn.Module):
                 and reference_points.shape[-1] == 2 and not reference_points.requires_grad
                 and not torch.is_autocast_enabled("cuda"))
 
+    def _sampling_wb(self):
+        """The fused path's projection weight / bias: both sampling projections in one GEMM, head-major rows
+        (:func:`head_major_wb`) unless ``HEAD_MAJOR`` is off."""
+        if HEAD_MAJOR:
+            return head_major_wb(self.sampling_offsets.weight, self.sampling_offsets.bias,
+                                 self.attention_weights.weight, self.attention_weights.bias, self.n_heads)
+        return (torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0),
+                torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0))
+
     def forward_src_pos(self, src, pos, reference_points, input_spatial_shapes, input_level_start_index,
                         input_padding_mask=None):
         """``(self.forward(src + pos, reference_points, src, ...), src)`` for an encoder layer whose query is
@@ -377,13 +402,12 @@ class MSDeformAttn(nn.Module):
                                      and pos.shape[1:] == src.shape[1:]))
                 and linear_ops.residual_fusable(src, self.value_proj)):
             N, Len_in, _ = src.shape
-            w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)
-            b = torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0)
+            w, b = self._sampling_wb()
             value, proj, src_res = linear_ops.EncoderInProjF32.apply(src, pos, self.value_proj.weight,
                                                                      self.value_proj.bias, w, b)
             value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
             out = MSDeformAttnFusedFunction.apply(value, proj, reference_points,
-                                                  _host_shapes(input_spatial_shapes), self.n_points)
+                                                  _host_shapes(input_spatial_shapes), self.n_points, HEAD_MAJOR)
             return linear_ops.linear(out, self.output_proj), src_res
         query = src if pos is None else src + pos
         return self.forward(query, reference_points, src, input_spatial_shapes, input_level_start_index,
@@ -400,11 +424,10 @@ class MSDeformAttn(nn.Module):
             # weight-gradient GEMM
             value = linear_ops.linear(input_flatten, self.value_proj).view(
                 N, Len_in, self.n_heads, self.d_model // self.n_heads)
-            w = torch.cat([self.sampling_offsets.weight, self.attention_weights.weight], 0)
-            b = torch.cat([self.sampling_offsets.bias, self.attention_weights.bias], 0)
+            w, b = self._sampling_wb()
             proj = linear_ops.linear_wb(query, w, b)
             out = MSDeformAttnFusedFunction.apply(value, proj, reference_points,
-                                                  _host_shapes(input_spatial_shapes), self.n_points)
+                                                  _host_shapes(input_spatial_shapes), self.n_points, HEAD_MAJOR)
             return linear_ops.linear(out, self.output_proj)
         value = self.value_proj(input_flatten)
         if input_padding_mask is not None:

@@ -44,3 +44,28 @@ def test_shape_preconditions_rejected_without_gpu():
     # the 16-bit NHWC input-gradient epilogue writes 8 channels per store: output channels % 16 != 0 is refused
     rc = lib.m2f_conv_x3_io(p, 0, 0, p, None, p, 1, 1, 1, 24, 32, 16, 16, 1, 1, p, ctypes.c_int64(1 << 30), None)
     assert rc == 3 and b"output channels" in lib.m2f_last_error()
+
+
+def test_head_major_wb_rows():
+    """msda.head_major_wb: the fused projection's rows regrouped per head -- head m's sampling offsets (L, P, 2)
+    then its attention logits (L*P) -- from the two Linear layers (ms_deform_attn.py:59-60), gradients included."""
+    import torch
+    from bm2f_amd.msda import head_major_wb
+    M, L, P, C = 8, 3, 4, 16
+    g = torch.Generator().manual_seed(0)
+    wo = torch.randn(M * L * P * 2, C, generator=g, requires_grad=True)
+    bo = torch.randn(M * L * P * 2, generator=g, requires_grad=True)
+    wa = torch.randn(M * L * P, C, generator=g, requires_grad=True)
+    ba = torch.randn(M * L * P, generator=g, requires_grad=True)
+    w, b = head_major_wb(wo, bo, wa, ba, M)
+    LP = L * P
+    for m in range(M):
+        assert torch.equal(w[m * 3 * LP:m * 3 * LP + 2 * LP], wo[m * 2 * LP:(m + 1) * 2 * LP])
+        assert torch.equal(w[m * 3 * LP + 2 * LP:(m + 1) * 3 * LP], wa[m * LP:(m + 1) * LP])
+        assert torch.equal(b[m * 3 * LP:m * 3 * LP + 2 * LP], bo[m * 2 * LP:(m + 1) * 2 * LP])
+        assert torch.equal(b[m * 3 * LP + 2 * LP:(m + 1) * 3 * LP], ba[m * LP:(m + 1) * LP])
+    gw = torch.randn(w.shape, generator=g)
+    (w * gw).sum().backward()
+    for m in range(M):
+        assert torch.equal(wo.grad[m * 2 * LP:(m + 1) * 2 * LP], gw[m * 3 * LP:m * 3 * LP + 2 * LP])
+        assert torch.equal(wa.grad[m * LP:(m + 1) * LP], gw[m * 3 * LP + 2 * LP:(m + 1) * 3 * LP])

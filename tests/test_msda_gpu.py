@@ -471,3 +471,41 @@ def test_tiled_backward_nonfinite_grad_stays_local(device, walk4):
     fin = torch.isfinite(gv.cpu()).numpy()
     assert (~fin).any() and fin.any()
     assert (fin == np.isfinite(wv)).all(), f"{(fin != np.isfinite(wv)).sum()} elements differ in finiteness"
+
+
+def _to_head_major(t, M, LP):
+    """(N, S, M*3*LP) rows in the reference order [offsets (M, LP, 2) | logits (M, LP)] -> one record per head."""
+    N, S, _ = t.shape
+    return torch.cat([t[..., :2 * M * LP].reshape(N, S, M, 2 * LP), t[..., 2 * M * LP:].reshape(N, S, M, LP)],
+                     -1).reshape(N, S, -1).contiguous()
+
+
+@pytest.mark.parametrize("shapes", [[(32, 32), (64, 64), (128, 128)], [(5, 7), (10, 13), (20, 26)],
+                                    [(4, 4), (8, 8), (16, 16), (32, 32)]])
+@pytest.mark.parametrize("quad,lds,pair", [(1, 1, 0), (1, 0, 0), (0, 0, 0), (1, 1, 1)])
+def test_fused_head_major_matches_reference_layout(device, shapes, quad, lds, pair):
+    """The head-major entry points (m2f_msda_fused_{fwd,bwd}_hm_f32: one [offsets | logits] record per head in
+    each projection row, the module's layout) return the reference-layout calls' output and gradients bit for
+    bit -- grad_value in deterministic mode, d proj in the head-major layout -- for every forward form, 5 % of
+    the samples thrown far."""
+    from bm2f_amd import _native
+    from bm2f_amd.msda import MSDeformAttnFusedFunction
+    from test_scale_gpu import _fused_case
+    N, M, P = 2, 8, 4
+    L = len(shapes)
+    value, proj, ref = _fused_case(shapes, N, 0.05, seed=61 + L)
+    S = value.shape[1]
+    rf = ref.float()[None, :, None, :].expand(N, S, L, 2).to(device)
+    gout = torch.randn(N, S, M * 32, generator=torch.Generator().manual_seed(3)).to(device)
+    res = []
+    with _native.options(msda_fwd_quad=quad, msda_fwd_lds=lds, msda_fwd_pair=pair, msda_bwd_det=1):
+        for hm in (False, True):
+            v = value.to(device).requires_grad_()
+            pj = (_to_head_major(proj, M, L * P) if hm else proj).to(device).requires_grad_()
+            out = MSDeformAttnFusedFunction.apply(v, pj, rf, tuple(shapes), P, hm)
+            out.backward(gout)
+            res.append((out.detach(), v.grad, pj.grad))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    assert torch.equal(_to_head_major(res[0][2], M, L * P), res[1][2])

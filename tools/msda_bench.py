@@ -48,6 +48,9 @@ def make_inputs(N, shapes, M=8, D=32, P=4, stress=False, device="cuda", seed=0, 
     return value, st, lsi, loc.contiguous(), attn, gout
 
 
+HEAD_MAJOR = False
+
+
 def fused_calls(value, shapes, gout, noise, M=8, P=4, seed=1):
     """Forward / backward closures of the fused-front-end kernels (m2f_msda_fused_{fwd,bwd}_f32) on the
     encoder layout: reference points at the pixel centres, offsets on the reference init rays (pixel units,
@@ -71,6 +74,8 @@ def fused_calls(value, shapes, gout, noise, M=8, P=4, seed=1):
     off = off[None, None] + noise * torch.randn(N, S, M, L, P, 2, device=dev, generator=g)
     logits = torch.randn(N, S, M * L * P, device=dev, generator=g)
     proj = torch.cat([off.reshape(N, S, -1), logits], -1).contiguous()
+    if HEAD_MAJOR:  # one [offsets | logits] record per (query, head): the m2f_msda_fused_*_hm_f32 entry points
+        proj = torch.cat([off.reshape(N, S, M, -1), logits.view(N, S, M, -1)], -1).reshape(N, S, -1).contiguous()
     hs = msda._host_shape_buffer(shapes)
     out = torch.empty(N, S, M * 32, device=dev)
     gv = torch.empty_like(value)
@@ -79,7 +84,7 @@ def fused_calls(value, shapes, gout, noise, M=8, P=4, seed=1):
     D = value.shape[-1]
 
     def fwd():
-        _native.call("m2f_msda_fused_fwd_f32", msda._ptr(value), msda._ptr(proj), proj.stride(1), msda._ptr(ref),
+        _native.call("m2f_msda_fused_fwd_hm_f32" if HEAD_MAJOR else "m2f_msda_fused_fwd_f32", msda._ptr(value), msda._ptr(proj), proj.stride(1), msda._ptr(ref),
                      ref.stride(0), ctypes.cast(hs, ctypes.c_void_p), N, S, M, D, L, S, P, msda._ptr(out), st)
 
     wsb = ctypes.c_int64(0)  # deterministic mode (--opt msda_bwd_det=1) needs a workspace
@@ -87,10 +92,24 @@ def fused_calls(value, shapes, gout, noise, M=8, P=4, seed=1):
     ws = torch.empty(wsb.value, dtype=torch.uint8, device=dev) if wsb.value else None
 
     def bwd():
-        _native.call("m2f_msda_fused_bwd_f32", msda._ptr(value), msda._ptr(proj), proj.stride(1), msda._ptr(ref),
+        _native.call("m2f_msda_fused_bwd_hm_f32" if HEAD_MAJOR else "m2f_msda_fused_bwd_f32", msda._ptr(value), msda._ptr(proj), proj.stride(1), msda._ptr(ref),
                      ref.stride(0), ctypes.cast(hs, ctypes.c_void_p), msda._ptr(gout), N, S, M, D, L, S, P,
                      msda._ptr(gv), msda._ptr(gp), None if ws is None else msda._ptr(ws), ctypes.c_int64(wsb.value), st)
+    fwd.tensors = {"out": out, "grad_value": gv, "grad_proj": gp, "M": M, "LP": len(shapes) * P}
     return fwd, bwd
+
+
+def digest(fwd):
+    """Hashes of the fused calls' outputs, the projection gradient in the reference layout (A/B builds compare)."""
+    import hashlib
+    t = fwd.tensors
+    gp = t["grad_proj"]
+    if HEAD_MAJOR:
+        M, LP = t["M"], t["LP"]
+        r = gp.view(*gp.shape[:2], M, 3 * LP)
+        gp = torch.cat([r[..., :2 * LP].reshape(*gp.shape[:2], -1), r[..., 2 * LP:].reshape(*gp.shape[:2], -1)], -1)
+    return {k: hashlib.sha1(v.contiguous().cpu().numpy().tobytes()).hexdigest()[:12]
+            for k, v in (("out", t["out"]), ("grad_value", t["grad_value"]), ("grad_proj", gp))}
 
 
 def timeit(fn, iters):
@@ -125,7 +144,13 @@ def main():
     ap.add_argument("--ab", default=None, metavar="NAME=V1,V2",
                     help="time the backward with option NAME at each value, alternating, --rounds times (one process)")
     ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--digest", action="store_true", help="print hashes of the fused outputs after timing")
+    ap.add_argument("--head-major", action="store_true",
+                    help="projection rows as one [offsets | logits] record per head (the _hm_ entry points, as the "
+                         "module calls them)")
     a = ap.parse_args()
+    global HEAD_MAJOR
+    HEAD_MAJOR = a.head_major
     from bm2f_amd import _native
     if a.lib:
         _native._LIB_PATH = os.path.abspath(a.lib)
@@ -162,6 +187,11 @@ def main():
     tf = tf or float("nan")
     print(f"lib={os.path.basename(a.lib) if a.lib else '-'} N={a.n} res={r} fused={a.fused} opts={','.join(a.opt) or '-'} stress={a.stress} noise={a.noise} : fwd {tf:.3f} ms ({fwd_bytes / tf / 1e6:.0f} GB/s alg), "
           f"bwd {tb:.3f} ms ({bwd_bytes / tb / 1e6:.0f} GB/s alg)")
+    if a.fused and a.digest:
+        fwd()
+        bwd()
+        torch.cuda.synchronize()
+        print("digest", digest(fwd), flush=True)
 
 
 if __name__ == "__main__":
