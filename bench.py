@@ -74,7 +74,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-modes", action="store_true", help="skip the bf16 / fp32 mode lines")
     ap.add_argument("--no-peaks", action="store_true", help="skip the achievable-peak probes")
     ap.add_argument("--no-dropin", action="store_true", help="skip the op-level MSDeformAttnFunction timing")
-    ap.add_argument("--mode-steps", type=int, default=4)
+    ap.add_argument("--mode-steps", type=int, default=10)
+    ap.add_argument("--mode-warmup", type=int, default=3)
     ap.add_argument("--kernel-steps", type=int, default=2, help="instrumented steps for roofline_all")
     ap.add_argument("--graph", type=int, default=None, choices=[0, 1],
                     help="capture the step in a HIP graph and replay it (default: on for the per-rank configs 4 / 5 "
@@ -654,10 +655,10 @@ def main():
             # the channels-last backbone only under fp16 autocast (the shipped NHWC find-db entries are fp16)
             cl_mode = bool(args.channels_last) and name == "fp16"
             model.backbone.channels_last = cl_mode
-            el = run(name, args.mode_steps, 2, f"mode {name}")
+            el = run(name, args.mode_steps, args.mode_warmup, f"mode {name}")
             key = {"fp16": "amp_fp16", "bf16": "amp_bf16", "none": "fp32_parity"}[name]
             modes[key] = {"value": round(world * args.batch * args.mode_steps / el, 3), "unit": "images/s",
-                          "ms_per_step": round(el / args.mode_steps * 1e3, 3), "steps": args.mode_steps, "warmup": 2,
+                          "ms_per_step": round(el / args.mode_steps * 1e3, 3), "steps": args.mode_steps, "warmup": args.mode_warmup,
                           "autocast": None if name == "none" else name,
                           "grad_scaler": name == "fp16", "backbone_layout": "channels_last" if cl_mode else "nchw"}
         model.backbone.channels_last = bool(args.channels_last)
