@@ -1753,14 +1753,27 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
 #pragma unroll
     for (int l = 0; l < LT; ++l) st = l == lq ? geo.start[l] : st;
     qpos[r] = st + (y0 + yy) * W + x0 + xx;
-    if constexpr (!FUSED) continue;  // the attention weights are read per level
+  }
+  // every round's logits are loaded before any round's softmax: the IEEE division (1 / sum) toggles the denorm mode,
+  // a scheduling barrier, so loads written inside the round loop were waited on round by round
+  float el[R][LT];
+  if constexpr (FUSED) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const unsigned lgb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>(fe.lg0(m, M, LP) + j) * 4u;
+#pragma unroll
+      for (int l = 0; l < LT; ++l) el[r][l] = *reinterpret_cast<const float*>(pbytes + lgb + l * P * 4);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if constexpr (!FUSED) break;  // the attention weights are read per level
     // softmax over the pair's L*P logits, exactly as msda_fused_fwd_q4 (and the backward's recomputation)
-    const unsigned lgb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>(fe.lg0(m, M, LP) + j) * 4u;
     float e[LT];
     float mx = -INFINITY;
 #pragma unroll
     for (int l = 0; l < LT; ++l) {
-      e[l] = *reinterpret_cast<const float*>(pbytes + lgb + l * P * 4);
+      e[l] = el[r][l];
       mx = fmaxf(mx, e[l]);
     }
     mx = fmaxf(mx, qpermf<0xB1>(mx));
@@ -1800,22 +1813,31 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
       constexpr bool POW2 = decltype(pow2)::value;
       const float fH = static_cast<float>(H), fW = static_cast<float>(W);
       const float fHm1 = static_cast<float>(H - 1), fWm1 = static_cast<float>(W - 1);
+      // every round's loads first: the per-round asm pins below (and, off powers of two, the IEEE divisions) are
+      // scheduling barriers, so loads written inside the round loop were waited on round by round
+      float2 rfs[R], offs[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (FUSED) {
+          const unsigned rfb = static_cast<unsigned>((qpos[r] + zq) * LT + l) * 8u;
+          const unsigned ofb = static_cast<unsigned>(n * S + qpos[r] + zq) * pld + static_cast<unsigned>(fe.off0(m, LP) + (l * P + j) * 2) * 4u;
+          rfs[r] = *reinterpret_cast<const float2*>(rbytes + rfb);
+          offs[r] = *reinterpret_cast<const float2*>(pbytes + ofb);
+        } else {
+          const unsigned ki = static_cast<unsigned>(((n * S + qpos[r] + zq) * M + m) * LP + l * P + j);
+          offs[r] = *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(loc) + ki * 8u);
+          wa[r][l] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(attn) + ki * 4u);
+        }
+      }
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         float sx, sy;
         if constexpr (FUSED) {
-          const unsigned rfb = static_cast<unsigned>((qpos[r] + zq) * LT + l) * 8u;
-          const unsigned ofb = static_cast<unsigned>(n * S + qpos[r] + zq) * pld + static_cast<unsigned>(fe.off0(m, LP) + (l * P + j) * 2) * 4u;
-          const float2 rf = *reinterpret_cast<const float2*>(rbytes + rfb);
-          const float2 off = *reinterpret_cast<const float2*>(pbytes + ofb);
-          sx = rf.x + div_norm(off.x, fW, geo.invW[l], POW2);
-          sy = rf.y + div_norm(off.y, fH, geo.invH[l], POW2);
+          sx = rfs[r].x + div_norm(offs[r].x, fW, geo.invW[l], POW2);
+          sy = rfs[r].y + div_norm(offs[r].y, fH, geo.invH[l], POW2);
         } else {
-          const unsigned ki = static_cast<unsigned>(((n * S + qpos[r] + zq) * M + m) * LP + l * P + j);
-          const float2 xy = *reinterpret_cast<const float2*>(reinterpret_cast<const char*>(loc) + ki * 8u);
-          sx = xy.x;
-          sy = xy.y;
-          wa[r][l] = *reinterpret_cast<const float*>(reinterpret_cast<const char*>(attn) + ki * 4u);
+          sx = offs[r].x;
+          sy = offs[r].y;
         }
         const float h = sy * H - 0.5f, w = sx * W - 0.5f;
         const bool ok = ((vmask >> r) & 1u) && h > -1.f && w > -1.f && h < fH && w < fW;
