@@ -1758,12 +1758,18 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
   // a scheduling barrier, so loads written inside the round loop were waited on round by round
   float el[R][LT];
   if constexpr (FUSED) {
+    // the byte offsets first, materialised (else the first load's destination is reused in the next round's 64-bit
+    // address arithmetic and waited on)
+    unsigned lgb[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const unsigned lgb = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>(fe.lg0(m, M, LP) + j) * 4u;
-#pragma unroll
-      for (int l = 0; l < LT; ++l) el[r][l] = *reinterpret_cast<const float*>(pbytes + lgb + l * P * 4);
+      lgb[r] = static_cast<unsigned>(n * S + qpos[r]) * pld + static_cast<unsigned>(fe.lg0(m, M, LP) + j) * 4u;
+      asm volatile("" : "+v"(lgb[r]));
     }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int l = 0; l < LT; ++l) el[r][l] = *reinterpret_cast<const float*>(pbytes + lgb[r] + l * P * 4);
   }
 #pragma unroll
   for (int r = 0; r < R; ++r) {
