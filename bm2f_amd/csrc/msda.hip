@@ -1754,8 +1754,8 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
     for (int l = 0; l < LT; ++l) st = l == lq ? geo.start[l] : st;
     qpos[r] = st + (y0 + yy) * W + x0 + xx;
   }
-  // every round's logits are loaded before any round's softmax: the IEEE division (1 / sum) toggles the denorm mode,
-  // a scheduling barrier, so loads written inside the round loop were waited on round by round
+  // every round's logits are loaded before any round's softmax: written inside the round loop, each round's loads
+  // were waited on before the next round's were issued (ISA), three memory round trips instead of one
   float el[R][LT];
   if constexpr (FUSED) {
     // the byte offsets first, materialised (else the first load's destination is reused in the next round's 64-bit
@@ -1819,8 +1819,8 @@ __global__ void __launch_bounds__(kFwdLdsThreads, 3) msda_fused_fwd_lds(const fl
       constexpr bool POW2 = decltype(pow2)::value;
       const float fH = static_cast<float>(H), fW = static_cast<float>(W);
       const float fHm1 = static_cast<float>(H - 1), fWm1 = static_cast<float>(W - 1);
-      // every round's loads first: the per-round asm pins below (and, off powers of two, the IEEE divisions) are
-      // scheduling barriers, so loads written inside the round loop were waited on round by round
+      // every round's loads first: the per-round asm pins below are scheduling barriers, so loads written inside the
+      // round loop were waited on round by round
       float2 rfs[R], offs[R];
 #pragma unroll
       for (int r = 0; r < R; ++r) {
