@@ -508,16 +508,23 @@ __global__ void __launch_bounds__(256) transpose_f32(const float* __restrict__ i
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const float* ip = in + b * in_bs;
   float* op = out + b * out_bs;
+  // all 16 loads in flight before any is used: an out-of-range element loads element 0 (R, Q > 0) and fills a tile
+  // entry no in-range output reads (a guarded load per element had been 16 dependent round trips)
+  float v[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int r = r0 + ty + 4 * k, q = q0 + tx;
-    if (r < R && q < Q) tile[ty + 4 * k][tx] = ip[static_cast<int64_t>(r) * in_ld + q];
+    v[k] = ip[(r < R && q < Q) ? static_cast<int64_t>(r) * in_ld + q : 0];
   }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) tile[ty + 4 * k][tx] = v[k];
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = tile[tx][ty + 4 * k];
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
     const int q = q0 + ty + 4 * k, r = r0 + tx;
-    if (r < R && q < Q) op[static_cast<int64_t>(q) * out_ld + r] = tile[tx][ty + 4 * k];
+    if (r < R && q < Q) op[static_cast<int64_t>(q) * out_ld + r] = v[k];
   }
 }
 

@@ -234,6 +234,26 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
       else
         for (int t = 0; t < 4; ++t) bv[t] = col + t < N ? bias[col + t] : 0.f;
     }
+    const bool vec = col + 3 < N && ((ldc & 3) == 0) && (!(EPI & kMask) || (ldm & 3) == 0);
+    // the 4 row groups' epilogue operands (residual rows, mask rows, ReLU bit words), all loaded before any is used:
+    // loaded inside the row loop (behind its range test), each had been a memory round trip of its own
+    f4 d1v[4], d2v[4], mkv[4];
+    unsigned nibv[4];
+    if constexpr ((EPI & (kAdd | kMask | kBitsIn)) != 0) {
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int rowc = min(m0 + w * 32 + rr * 8 + er, M - 1);
+        if constexpr ((EPI & kBitsIn) != 0)
+          nibv[rr] = bits[static_cast<int64_t>(rowc) * ldm + min((n0 + j * 32) >> 5, (N - 1) >> 5)] >> ec;
+        if (vec) {
+          if constexpr ((EPI & kMask) != 0) mkv[rr] = *reinterpret_cast<const f4*>(mask + static_cast<int64_t>(rowc) * ldm + col);
+          if constexpr ((EPI & kAdd) != 0) {
+            d1v[rr] = *reinterpret_cast<const f4*>(D1 + static_cast<int64_t>(dper ? rowc % dper : rowc) * ldd + col);
+            if (D2) d2v[rr] = *reinterpret_cast<const f4*>(D2 + static_cast<int64_t>(rowc) * ldd + col);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int lr = rr * 8 + er, row = m0 + w * 32 + lr;
@@ -254,21 +274,20 @@ __global__ void __launch_bounds__(64 * NW, 2) x3_nt_kernel(const float* __restri
       }
       if (row >= M || col >= N) continue;
       if constexpr ((EPI & kBitsIn) != 0) {
-        const unsigned nib = bits[static_cast<int64_t>(row) * ldm + ((n0 + j * 32) >> 5)] >> ec;
+        const unsigned nib = nibv[rr];
         v.x = (nib & 1u) ? v.x : 0.f; v.y = (nib & 2u) ? v.y : 0.f;
         v.z = (nib & 4u) ? v.z : 0.f; v.w = (nib & 8u) ? v.w : 0.f;
       }
-      const bool vec = col + 3 < N && ((ldc & 3) == 0) && (!(EPI & kMask) || (ldm & 3) == 0);
       if (vec) {
         if constexpr ((EPI & kMask) != 0) {
-          const f4 mk = *reinterpret_cast<const f4*>(mask + static_cast<int64_t>(row) * ldm + col);
+          const f4 mk = mkv[rr];
           v.x = mk.x > 0.f ? v.x : 0.f; v.y = mk.y > 0.f ? v.y : 0.f;
           v.z = mk.z > 0.f ? v.z : 0.f; v.w = mk.w > 0.f ? v.w : 0.f;
         }
         if constexpr ((EPI & kAdd) != 0) {
           // (A.B + bias) + D1 + D2, left to right: the sum autograd would form, one rounding per add
-          v = v + *reinterpret_cast<const f4*>(D1 + static_cast<int64_t>(dper ? row % dper : row) * ldd + col);
-          if (D2) v = v + *reinterpret_cast<const f4*>(D2 + static_cast<int64_t>(row) * ldd + col);
+          v = v + d1v[rr];
+          if (D2) v = v + d2v[rr];
         }
         *reinterpret_cast<f4*>(C + static_cast<int64_t>(row) * ldc + col) = v;
       } else {

@@ -2,7 +2,8 @@
 
     python tools/bench_ab.py --set bm2f_amd.bench_model.CONV1X1_GEMM=0 -- [bench.py arguments]
 
-Each --set MODULE.ATTR=INT assigns int(value) (or bool for a bool attribute) before bench.main() runs."""
+Each --set MODULE.ATTR=VALUE assigns VALUE converted to the attribute's type (int, bool or str) before bench.main()
+runs; e.g. --set bm2f_amd._native._LIB_PATH=tools/lib/libbm2f_x.so times another build of the library."""
 import importlib
 import os
 import sys
@@ -24,7 +25,7 @@ def main():
         mod, attr = path.rsplit(".", 1)
         m = importlib.import_module(mod)
         old = getattr(m, attr)
-        setattr(m, attr, type(old)(int(val)))
+        setattr(m, attr, os.path.abspath(val) if isinstance(old, str) else type(old)(int(val)))
         print(f"[bench_ab] {path} = {getattr(m, attr)!r}", file=sys.stderr, flush=True)
     sys.argv = [os.path.join(ROOT, "bench.py")] + argv
     import bench
