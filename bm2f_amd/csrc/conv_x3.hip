@@ -287,12 +287,19 @@ __global__ void __launch_bounds__(256, 2) x3_conv_kernel(const TI* __restrict__ 
         }
       }
     } else {
+      // the 4 output channels' biases loaded before any is used (behind the range test, each load had been a
+      // memory round trip of its own)
+      float bq[4] = {0.f, 0.f, 0.f, 0.f};
+      if (bias) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bq[q] = bias[min(n20 + j * 32 + q * 8 + er, Cout - 1)];
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int lr = q * 8 + er, co = n20 + j * 32 + lr;
         f4 v = *reinterpret_cast<const f4*>(&img[lr * EP + ec]);
         if (co < Cout) {
-          if (bias) v += bias[co];
+          if (bias) v += bq[q];
           TO* dst = Ob + static_cast<int64_t>(co) * HW + p0 + w * 32 + ec;
           if constexpr (std::is_same<TO, float>::value) {
             *reinterpret_cast<f4*>(dst) = v;
